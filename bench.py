@@ -1,0 +1,231 @@
+"""Throughput bench for the MI355X streaming-DSP hot path (BASELINE.json metric).
+
+Default workload (--config c5, one stream per GPU): BASELINE config C5's per-GPU slice,
+i.e. a 61.44 MS/s-class IQ stream pushed as fast as the GPU takes it through
+  * the IQ front end's spectrum: 65,536-point BH7 window * FFT * 10log10|X|^2, frames
+    back to back (fftRate = fs/N -> skip 0), and
+  * one VFO: RxVFO(61.44 MHz -> 240 kHz, bw 200 kHz, offset +2.5 MHz; plan_256 + 91-tap
+    LPF) -> BroadcastFM mono (dev 100 kHz, 228-tap audio LPF) -> stereo_t,
+with every rank's last 16 spectra gathered to rank 0 over RCCL each step (N > 1).
+A step = one batch of B synthetic complex-float IQ samples resident in HBM
+(uniform [-1, 1), SpeedTester distribution). Other configs: c2 (1M-point BH7 spectrum,
+nz = 1e6, zero-padded), c3 (xlator + 256-tap FIR /8 + FM quadrature, fused).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import sdrpp_amd  # noqa: E402
+from sdrpp_amd import dsp  # noqa: E402
+
+METRIC = "IQ Msamples/s through FFT+FIR+demod chain; % HBM roofline at 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c5", choices=["c5", "c2", "c3"])
+    ap.add_argument("--log2-batch", type=int, default=28, help="IQ samples per GPU per step = 2^k (c5/c3)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+class C5:
+    """FFT(64k BH7) spectra + RxVFO + BroadcastFM mono, one stream per GPU."""
+    N = 65536
+    FS = 61.44e6
+
+    def __init__(self, B, rank, dev):
+        self.B = (B // self.N) * self.N
+        self.frames = self.B // self.N
+        self.fft = dsp.FFTSpectrum(self.N, self.N, 6, device=dev)
+        self.vfo = dsp.RxVFO(self.FS, 240000, 200000, 2.5e6 + 1e5 * rank, device=dev)
+        self.wfm = dsp.BroadcastFM(100000, 240000, True, device=dev)
+        self.spectra = torch.empty(self.frames * self.N, dtype=torch.float32, device="cuda")
+        self.ifbuf = torch.empty(2 * (self.B // 256 + 64), dtype=torch.float32, device="cuda")
+        self.audio = torch.empty(2 * (self.B // 256 + 64), dtype=torch.float32, device="cuda")
+        self.bytes_per_sample = 8 + 4 + 8 / 256 + 8 / 256   # ~12.06 B
+        self.kernel_bytes = 12.0 * self.B                   # spectrum pair: 8 B in + 4 B dB out per sample
+        self.kernel_name = "spectrum (fft_passA + fft_passB, N=65536)"
+
+    def dominant(self, x, s):
+        self.fft.execute_dev(x.data_ptr(), self.N, self.frames, self.spectra.data_ptr(), s)
+
+    def rest(self, x, s):
+        m = self.vfo.process_dev(x.data_ptr(), self.B, self.ifbuf.data_ptr(), s)
+        self.wfm.process_dev(self.ifbuf.data_ptr(), m, self.audio.data_ptr(), s)
+
+    def gather_src(self):
+        return self.spectra[-16 * self.N:]
+
+
+class C2:
+    """1,048,576-point BH7 spectrum, fftRate 10 at 10 MS/s -> nz = 1e6, zero-padded."""
+    N = 1 << 20
+    NZ = 1000000
+
+    def __init__(self, B, rank, dev):
+        self.frames = max(1, B // self.NZ)
+        self.B = self.frames * self.NZ
+        self.fft = dsp.FFTSpectrum(self.N, self.NZ, 6, device=dev)
+        self.spectra = torch.empty(self.frames * self.N, dtype=torch.float32, device="cuda")
+        self.bytes_per_sample = 8 + 4 * self.N / self.NZ
+        self.kernel_bytes = self.bytes_per_sample * self.B
+        self.kernel_name = "spectrum (fft_passA + fft_passB, N=2^20, nz=1e6)"
+
+    def dominant(self, x, s):
+        self.fft.execute_dev(x.data_ptr(), self.NZ, self.frames, self.spectra.data_ptr(), s)
+
+    def rest(self, x, s):
+        pass
+
+    def gather_src(self):
+        return self.spectra[-2 * self.N:]
+
+
+class C3:
+    """FrequencyXlator(-1.5 MHz) -> 256-tap DecimatingFIR /8 -> Quadrature(100 kHz), fused kernel."""
+    FS = 61.44e6
+
+    def __init__(self, B, rank, dev):
+        self.B = B
+        taps = dsp.low_pass(3.0e6, 912000.0, self.FS)
+        w = 2 * np.pi * (-1.5e6 / self.FS)
+        self.ddc = dsp.DDCFM(w, taps, 8, 2 * np.pi * 100e3 / (self.FS / 8), device=dev)
+        self.out = torch.empty(B // 8 + 64, dtype=torch.float32, device="cuda")
+        self.bytes_per_sample = 8 + 4 / 8
+        self.kernel_bytes = self.bytes_per_sample * B
+        self.kernel_name = "fir_kernel<xlator+256-tap/8+quadrature>"
+
+    def dominant(self, x, s):
+        self.ddc.process_dev(x.data_ptr(), self.B, self.out.data_ptr(), s)
+
+    def rest(self, x, s):
+        pass
+
+    def gather_src(self):
+        return self.out[:65536]
+
+
+def cpu_baseline(seconds):
+    """The oracle's C port of the C5 chain on one host core, time-bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    blk = 1 << 20
+    rng = np.random.default_rng(0xACE1)
+    x = (rng.uniform(-1, 1, blk) + 1j * rng.uniform(-1, 1, blk)).astype(np.complex64)
+    chain = oracle.Chain(61.44e6, 65536, 2.5e6, precise=False)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        chain.process(x)
+        n += blk
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    return n / dt / 1e6, n, dt
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+    B = 1 << a.log2_batch
+    if a.config == "c2":
+        B = 256 * 1000000
+    wl = {"c5": C5, "c2": C2, "c3": C3}[a.config](B, rank, dev)
+    B = wl.B
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0xACE1 + rank)
+    x = (torch.rand(2 * B, device="cuda", generator=g) * 2 - 1).contiguous()   # complex_t interleaved
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+    gather_bufs = None
+    if world > 1:
+        src = wl.gather_src()
+        gather_bufs = [torch.empty_like(src) for _ in range(world)] if rank == 0 else None
+
+    ev = []
+
+    def step(timed):
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        wl.dominant(x, s)
+        if timed:
+            e1.record(stream)
+            ev.append((e0, e1))
+        wl.rest(x, s)
+        if world > 1:
+            dist.gather(wl.gather_src(), gather_bufs, dst=0)
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / max(len(ev), 1)
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+
+    if rank == 0:
+        total = world * B * a.steps
+        value = total / elapsed / 1e6
+        achieved = wl.kernel_bytes / (kern_ms * 1e-3) / 1e9
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "MS/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic uniform[-1,1) complex IQ in HBM",
+            "config": {"workload": {"c5": "C5 per-GPU slice: 64k BH7 FFT+log-mag (back-to-back) + RxVFO 61.44M->240k "
+                                          "+ BroadcastFM mono; RCCL gather of 16 spectra/rank/step",
+                                    "c2": "C2: 1M-point BH7 FFT + log-mag, nz=1e6 zero-padded",
+                                    "c3": "C3: xlator + 256-tap FIR /8 + FM quadrature (fused)"}[a.config],
+                       "samples_per_gpu_per_step": B, "parallelism": f"replica-streams x{world}",
+                       "bytes_per_sample": round(wl.bytes_per_sample, 4)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": wl.kernel_name, "kernel_ms": round(kern_ms, 4)},
+            "chain_hbm_GBs": round(wl.bytes_per_sample * value * 1e6 / world / 1e9, 1),
+        }
+        if world == 1 and not a.no_cpu and a.config == "c5":
+            v, n, dt = cpu_baseline(a.cpu_seconds)
+            out["cpu_baseline"] = {"value": round(v, 3), "unit": "MS/s", "cores": 1, "kind": "port",
+                                   "sample": f"oracle C port of the same C5 chain (fp32, VOLK-style rotator/dots), "
+                                             f"{n} samples in 1M blocks, {dt:.1f} s on 1 host core"}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

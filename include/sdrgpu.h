@@ -1,0 +1,140 @@
+/*
+ * sdrgpu.h -- C ABI of the MI355X (gfx950) streaming-DSP hot path of SDR++.
+ *
+ * Plain pointers and sizes only; no C++ or torch types. Two calling styles:
+ *   *_process(...)      drop-in for the reference's host-buffer process(count, in, out)
+ *                       (synchronous, host pointers; staged through pinned memory)
+ *   *_process_dev(...)  device-resident batches on a caller stream (hipStream_t as void*,
+ *                       NULL = the handle's own stream); asynchronous, host-side state
+ *                       (decimation offsets, output counts) is updated at call time.
+ * Every call returns >= 0 on success (an output count where meaningful) or a
+ * negative SDRGPU_E* code; sdrgpu_last_error() gives the thread's last message.
+ * A handle is used by one thread at a time (the reference's one-worker-per-block
+ * model, core/src/dsp/block.h:70-76).
+ *
+ * Reference interfaces replaced (paths in qrp73/SDRPP, core/src/...):
+ *   spectrum  : IQFrontEnd::handler + updateFFTSize, signal_path/iq_frontend.cpp:230-249,272-296
+ *   windows   : dsp::window::createWindow, dsp/window/window.h:38-64
+ *   taps      : dsp::taps::{lowPass,highPass,bandPass,windowedSinc}, dsp/taps/
+ *   FIR       : dsp::filter::FIR::process, dsp/filter/fir.h:62-83
+ *   decim FIR : dsp::filter::DecimatingFIR::process, dsp/filter/decimating_fir.h:45-68
+ *   xlator    : dsp::channel::FrequencyXlator::process, dsp/channel/frequency_xlator.h:43-50
+ *   power dec : dsp::multirate::PowerDecimator::process, dsp/multirate/power_decimator.h:51-70
+ *   polyphase : dsp::multirate::PolyphaseResampler::process, dsp/multirate/polyphase_resampler.h:69-99
+ *   rational  : dsp::multirate::RationalResampler, dsp/multirate/rational_resampler.h:83-167
+ *   VFO       : dsp::channel::RxVFO::process, dsp/channel/rx_vfo.h:89-100
+ *   quadrature: dsp::demod::Quadrature::process, dsp/demod/quadrature.h:41-56
+ *   FM        : dsp::demod::FM<float>::process, dsp/demod/fm.h:86-103
+ *   WFM       : dsp::demod::BroadcastFM::process (mono), dsp/demod/broadcast_fm.h:144-215
+ *   ingest    : file_source converters, source_modules/file_source/src/main.cpp:361-542
+ */
+#ifndef SDRGPU_H
+#define SDRGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDRGPU_VERSION 100
+
+enum {
+    SDRGPU_OK = 0,
+    SDRGPU_EARG = -1,     /* invalid argument (reference: assert / std::runtime_error) */
+    SDRGPU_EHIP = -2,     /* HIP runtime error (name in sdrgpu_last_error) */
+    SDRGPU_ENOMEM = -3,
+    SDRGPU_ESTATE = -4,   /* wrong handle kind / not initialised */
+    SDRGPU_ENODEV = -5
+};
+
+/* element types (dsp::complex_t is {float re, im}, dsp/types.h:6; stereo_t {float l, r}) */
+enum { SDRGPU_F32 = 0, SDRGPU_C64 = 1 };
+
+/* window ids = dsp::window::windowType (dsp/window/window.h:27-35) */
+enum { SDRGPU_WIN_RECTANGULAR = 0, SDRGPU_WIN_HAMMING, SDRGPU_WIN_HANN, SDRGPU_WIN_BLACKMAN,
+       SDRGPU_WIN_NUTTALL, SDRGPU_WIN_BLACKMAN_HARRIS4, SDRGPU_WIN_BLACKMAN_HARRIS7 };
+
+/* ----------------------------------------------------------- runtime ---- */
+int         sdrgpu_version(void);
+const char* sdrgpu_last_error(void);
+int         sdrgpu_device_count(void);
+int         sdrgpu_malloc(int device, void** dptr, size_t bytes);
+int         sdrgpu_free(void* dptr);
+int         sdrgpu_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+int         sdrgpu_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+int         sdrgpu_stream_create(int device, void** stream);
+int         sdrgpu_stream_destroy(void* stream);
+int         sdrgpu_stream_synchronize(void* stream);
+int         sdrgpu_host_register(void* ptr, size_t bytes);   /* pin a dsp::stream buffer */
+int         sdrgpu_host_unregister(void* ptr);
+
+/* ------------------------------------------- host-side design (exact) ---- */
+/* Bit-exact restatements evaluated on the host, as the reference does. */
+int  sdrgpu_create_window(int type, float* buffer, int size, int centered);          /* window.h:38 */
+void sdrgpu_gen_reshape_params(double sampleRate, int size, double rate, int* skip, int* nz); /* iq_frontend.h:56 */
+int  sdrgpu_taps_estimate_count(double transWidth, double sampleRate);               /* estimate_tap_count.h:4 */
+int  sdrgpu_taps_low_pass(double cutoff, double transWidth, double sampleRate, int odd, float* out); /* low_pass.h:7; out NULL -> count */
+int  sdrgpu_taps_high_pass(double cutoff, double transWidth, double sampleRate, int odd, float* out); /* high_pass.h:7 */
+int  sdrgpu_taps_band_pass_f(double start, double stop, double transWidth, double sampleRate, int odd, float* out); /* band_pass.h:11 */
+int  sdrgpu_taps_band_pass_c(double start, double stop, double transWidth, double sampleRate, int odd, float* out);
+int  sdrgpu_decim_plan(int ratio, int* decims, int* ntaps, const float** taps);      /* decim/plans.h */
+
+/* --------------------------------------------------------- spectrum ---- */
+/* Window * FFT(N, forward, unnormalised) * 10*log10(|X|^2) of nz <= N samples,
+ * zero-padded to N (iq_frontend.cpp:230-249 + :295). N = 2^k, 64 <= N <= 2^20. */
+typedef struct sdrgpu_fft sdrgpu_fft;
+int sdrgpu_fft_create(sdrgpu_fft** h, int device, int fftSize, int nz, int windowType);
+int sdrgpu_fft_set_window(sdrgpu_fft* h, const float* window, int nz);   /* exact host floats */
+int sdrgpu_fft_set_window_type(sdrgpu_fft* h, int windowType, int nz);
+/* device batch: frame f starts at in + f*frameStride complex samples; out: frames x N floats */
+int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, void* stream);
+/* drop-in for IQFrontEnd::handler: in = host complex_t[nz]; out = host float[N] or NULL
+ * (acquireFFTBuffer may return NULL; the spectrum is then computed but not written). */
+int sdrgpu_fft_logmag(sdrgpu_fft* h, const void* in, float* out);
+int sdrgpu_fft_size(sdrgpu_fft* h);
+int sdrgpu_fft_destroy(sdrgpu_fft* h);
+
+/* ---------------------------------------------------- stream blocks ---- */
+typedef struct sdrgpu_block sdrgpu_block;
+/* FrequencyXlator (offset in rad/sample, like init(in, offset)) */
+int sdrgpu_xlator_create(sdrgpu_block** h, int device, double offsetRad);
+int sdrgpu_xlator_set_offset(sdrgpu_block* h, double offsetRad);
+/* FIR<D,T> (decim = 1) and DecimatingFIR<D,T>: dtype/ttype SDRGPU_F32 or SDRGPU_C64 */
+int sdrgpu_fir_create(sdrgpu_block** h, int device, int dtype, int ttype, const float* taps, int ntaps, int decim);
+int sdrgpu_fir_set_taps(sdrgpu_block* h, const float* taps, int ntaps);
+int sdrgpu_fir_set_decimation(sdrgpu_block* h, int decim);
+/* Quadrature (deviation in rad/sample) */
+int sdrgpu_quadrature_create(sdrgpu_block** h, int device, double deviationRad);
+int sdrgpu_quadrature_set_deviation(sdrgpu_block* h, double deviationRad);
+/* PowerDecimator<T> (ratio = 1 or 2^k <= 8192), PolyphaseResampler<T>, RationalResampler<T> */
+int sdrgpu_power_decimator_create(sdrgpu_block** h, int device, int dtype, int ratio);
+int sdrgpu_polyphase_resampler_create(sdrgpu_block** h, int device, int dtype, int interp, int decim, const float* taps, int ntaps);
+int sdrgpu_rational_resampler_create(sdrgpu_block** h, int device, int dtype, double inSamplerate, double outSamplerate);
+/* RxVFO: xlator(-offset) -> rational resampler -> LPF(bw/2) if bw != outSr */
+int sdrgpu_rxvfo_create(sdrgpu_block** h, int device, double inSamplerate, double outSamplerate, double bandwidth, double offset);
+int sdrgpu_rxvfo_set_offset(sdrgpu_block* h, double offset);
+/* Fused DDC: xlator(offsetRad) -> DecimatingFIR<complex_t,float>(taps, decim) -> Quadrature(deviationRad); float out */
+int sdrgpu_ddc_fm_create(sdrgpu_block** h, int device, double offsetRad, const float* taps, int ntaps, int decim, double deviationRad);
+/* FM<float> (demod/fm.h) and BroadcastFM mono (stereo_t out, broadcast_fm.h) */
+int sdrgpu_fm_create(sdrgpu_block** h, int device, double samplerate, double bandwidth, int lowPass, int highPass);
+int sdrgpu_wfm_create(sdrgpu_block** h, int device, double deviation, double samplerate, int lowPass);
+
+int sdrgpu_block_process(sdrgpu_block* h, const void* in, int count, void* out);      /* host buffers */
+int sdrgpu_block_process_dev(sdrgpu_block* h, const void* in, int count, void* out, void* stream);
+int sdrgpu_block_out_count(sdrgpu_block* h, int count);   /* exact output count of the next call */
+int sdrgpu_block_reset(sdrgpu_block* h);
+int sdrgpu_block_destroy(sdrgpu_block* h);
+
+/* ------------------------------------------------------------ ingest ---- */
+/* file_source / rtl_sdr / hackrf sample converters (elementwise, n scalars):
+ * kind 0 u8 (b-128+0.5f)/127.5f, 1 i16 (s+0.5f)/32767.5f, 2 i24 packed LE,
+ * 3 i32 ((v+0.5)/(2^31-0.5) in double), 4 f64 -> f32, 5 i8 x*(1/128) */
+enum { SDRGPU_CONV_U8 = 0, SDRGPU_CONV_I16, SDRGPU_CONV_I24, SDRGPU_CONV_I32, SDRGPU_CONV_F64, SDRGPU_CONV_I8 };
+int sdrgpu_convert_dev(int device, int kind, const void* in, long long n, float* out, void* stream);
+int sdrgpu_convert(int device, int kind, const void* in, long long n, float* out);      /* host buffers */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,106 @@
+"""sdrpp_amd: MI355X-native streaming-DSP hot path of SDR++ (qrp73/SDRPP).
+
+The product is the C-ABI shared library ``sdrpp_amd/lib/libsdrgpu.so`` (HIP
+kernels for gfx950, declared in ``include/sdrgpu.h``). This module is a thin
+ctypes binding used by the tests and ``bench.py``; the drop-in C++ host classes
+live in ``sdrpp_amd/dsp/``. There is no CPU fallback:
+loading fails loudly if the library is missing.
+"""
+import ctypes
+import os
+
+__all__ = ["lib", "LIB_PATH", "check", "SdrGpuError"]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libsdrgpu.so")
+
+F32, C64 = 0, 1
+WIN_RECTANGULAR, WIN_HAMMING, WIN_HANN, WIN_BLACKMAN, WIN_NUTTALL, WIN_BH4, WIN_BH7 = range(7)
+CONV_U8, CONV_I16, CONV_I24, CONV_I32, CONV_F64, CONV_I8 = range(6)
+
+
+class SdrGpuError(RuntimeError):
+    pass
+
+
+def _load():
+    # PyTorch wheels bundle their own libamdhip64.so.7 (same SONAME as /opt/rocm's). Load
+    # torch first so libsdrgpu binds to the already-loaded runtime: one HIP/HSA runtime
+    # per process, shared device pointers and streams with torch (bench, RCCL).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the HIP extension is required; there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i, d, ll, fp = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_longlong, ctypes.c_void_p
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "sdrgpu_version": (i, []),
+        "sdrgpu_last_error": (ctypes.c_char_p, []),
+        "sdrgpu_device_count": (i, []),
+        "sdrgpu_malloc": (i, [i, pp, ctypes.c_size_t]),
+        "sdrgpu_free": (i, [vp]),
+        "sdrgpu_memcpy_h2d": (i, [vp, vp, ctypes.c_size_t, vp]),
+        "sdrgpu_memcpy_d2h": (i, [vp, vp, ctypes.c_size_t, vp]),
+        "sdrgpu_stream_create": (i, [i, pp]),
+        "sdrgpu_stream_destroy": (i, [vp]),
+        "sdrgpu_stream_synchronize": (i, [vp]),
+        "sdrgpu_host_register": (i, [vp, ctypes.c_size_t]),
+        "sdrgpu_host_unregister": (i, [vp]),
+        "sdrgpu_create_window": (i, [i, fp, i, i]),
+        "sdrgpu_gen_reshape_params": (None, [d, i, d, ctypes.POINTER(i), ctypes.POINTER(i)]),
+        "sdrgpu_taps_estimate_count": (i, [d, d]),
+        "sdrgpu_taps_low_pass": (i, [d, d, d, i, fp]),
+        "sdrgpu_taps_high_pass": (i, [d, d, d, i, fp]),
+        "sdrgpu_taps_band_pass_f": (i, [d, d, d, d, i, fp]),
+        "sdrgpu_taps_band_pass_c": (i, [d, d, d, d, i, fp]),
+        "sdrgpu_decim_plan": (i, [i, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(ctypes.POINTER(ctypes.c_float))]),
+        "sdrgpu_fft_create": (i, [pp, i, i, i, i]),
+        "sdrgpu_fft_set_window": (i, [vp, fp, i]),
+        "sdrgpu_fft_set_window_type": (i, [vp, i, i]),
+        "sdrgpu_fft_execute_dev": (i, [vp, vp, ll, i, vp, vp]),
+        "sdrgpu_fft_logmag": (i, [vp, vp, vp]),
+        "sdrgpu_fft_size": (i, [vp]),
+        "sdrgpu_fft_destroy": (i, [vp]),
+        "sdrgpu_xlator_create": (i, [pp, i, d]),
+        "sdrgpu_xlator_set_offset": (i, [vp, d]),
+        "sdrgpu_fir_create": (i, [pp, i, i, i, fp, i, i]),
+        "sdrgpu_fir_set_taps": (i, [vp, fp, i]),
+        "sdrgpu_fir_set_decimation": (i, [vp, i]),
+        "sdrgpu_quadrature_create": (i, [pp, i, d]),
+        "sdrgpu_quadrature_set_deviation": (i, [vp, d]),
+        "sdrgpu_power_decimator_create": (i, [pp, i, i, i]),
+        "sdrgpu_polyphase_resampler_create": (i, [pp, i, i, i, i, fp, i]),
+        "sdrgpu_rational_resampler_create": (i, [pp, i, i, d, d]),
+        "sdrgpu_rxvfo_create": (i, [pp, i, d, d, d, d]),
+        "sdrgpu_rxvfo_set_offset": (i, [vp, d]),
+        "sdrgpu_ddc_fm_create": (i, [pp, i, d, fp, i, i, d]),
+        "sdrgpu_fm_create": (i, [pp, i, d, d, i, i]),
+        "sdrgpu_wfm_create": (i, [pp, i, d, d, i]),
+        "sdrgpu_block_process": (i, [vp, vp, i, vp]),
+        "sdrgpu_block_process_dev": (i, [vp, vp, i, vp, vp]),
+        "sdrgpu_block_out_count": (i, [vp, i]),
+        "sdrgpu_block_reset": (i, [vp]),
+        "sdrgpu_block_destroy": (i, [vp]),
+        "sdrgpu_convert_dev": (i, [i, i, vp, ll, vp, vp]),
+        "sdrgpu_convert": (i, [i, i, vp, ll, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+lib = _load()
+
+
+def check(rc):
+    """Raise SdrGpuError for a negative C-ABI status; return rc otherwise."""
+    if rc is not None and rc < 0:
+        raise SdrGpuError(f"sdrgpu error {rc}: {lib.sdrgpu_last_error().decode(errors='replace')}")
+    return rc

@@ -1,0 +1,71 @@
+"""Build libsdrgpu.so (gfx950 HIP kernels + C ABI) and the oracle library in-tree.
+
+Explicit hipcc/gcc command lines, no build system: each translation unit is
+compiled to an object under build/ and linked into sdrpp_amd/lib/libsdrgpu.so.
+Host-side design code (windows, taps) is compiled with -ffp-contract=off so it
+rounds exactly like the reference source; device code keeps the default FMA
+contraction (its parity bar is a stated tolerance).
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "sdrpp_amd", "csrc")
+LIBDIR = os.path.join(ROOT, "sdrpp_amd", "lib")
+BUILD = os.path.join(ROOT, "build")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+SOURCES = [
+    # (file, extra flags)
+    ("host_design.cpp", ["-ffp-contract=off"]),
+    ("capi.cpp", []),
+    ("fft.hip", []),
+    ("blocks.hip", []),
+]
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_lib(force=False):
+    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(BUILD, exist_ok=True)
+    headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
+    headers.append(os.path.join(ROOT, "include", "sdrgpu.h"))
+    objs = []
+    for src, extra in SOURCES:
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(BUILD, src + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [path] + headers):
+            lang = ["-x", "hip"] if src.endswith(".hip") else []
+            _run([HIPCC, "--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17",
+                  "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+                  "-I", os.path.join(ROOT, "include")] + extra + lang + ["-c", path, "-o", obj])
+    lib = os.path.join(LIBDIR, "libsdrgpu.so")
+    if force or _stale(lib, objs):
+        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs)
+    return lib
+
+
+def build_oracle():
+    odir = os.path.join(ROOT, "oracle")
+    _run(["make", "-C", odir, "-s"])
+    return os.path.join(odir, "libsdr_oracle.so")
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    build_lib(force)
+    build_oracle()

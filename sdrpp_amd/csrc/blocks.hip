@@ -1,0 +1,979 @@
+// Channel-chain kernels and stateful blocks: frequency xlator, FIR / decimating
+// FIR (optionally with the xlator fused into its load and the FM quadrature
+// demodulator fused into its store), power-of-two decimator, polyphase and
+// rational resamplers, RxVFO, FM / broadcast-FM (mono) demodulators, ingest
+// converters. Reference semantics are cited per block; DESIGN.md has the layout.
+#include <cmath>
+#include <cstring>
+#include <algorithm>
+#include <memory>
+#include <numeric>
+#include "sdrgpu_internal.h"
+
+namespace sdrgpu {
+
+// ------------------------------------------------------------------- helpers
+__device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+// NCO phasor for stream sample `idx` of a call whose first sample has phase theta0:
+// angle = theta0 + w*idx in double, reduced to [-pi, pi], then an accurate float sincos.
+__device__ __forceinline__ float2 nco(double theta0, double w, long long idx) {
+    const double TWO_PI = 6.283185307179586476925286766559;
+    const double INV_TWO_PI = 0.15915494309189533576888376337251;
+    double a = fma(w, (double)idx, theta0);
+    a = fma(-rint(a * INV_TWO_PI), TWO_PI, a);
+    float s, c;
+    sincosf((float)a, &s, &c);
+    return make_float2(c, s);
+}
+
+template <typename T> __device__ __forceinline__ T zero_of();
+template <> __device__ __forceinline__ float zero_of<float>() { return 0.0f; }
+template <> __device__ __forceinline__ float2 zero_of<float2>() { return make_float2(0.f, 0.f); }
+
+// acc += x * h for the four (data, tap) type pairs of filter/fir.h:69-75
+__device__ __forceinline__ void mac(float& acc, float x, float h) { acc = fmaf(x, h, acc); }
+__device__ __forceinline__ void mac(float2& acc, float2 x, float h) { acc.x = fmaf(x.x, h, acc.x); acc.y = fmaf(x.y, h, acc.y); }
+__device__ __forceinline__ void mac(float2& acc, float2 x, float2 h) {
+    acc.x = fmaf(x.x, h.x, acc.x); acc.x = fmaf(-x.y, h.y, acc.x);
+    acc.y = fmaf(x.x, h.y, acc.y); acc.y = fmaf(x.y, h.x, acc.y);
+}
+
+// ------------------------------------------------------------ FIR engine
+// out[m] = sum_{j<ntaps} buf[offset0 + m*D + j] * taps[j],  buf = hist(H) | in(count)
+// (correlation order, filter/fir.h:62-83, decimating_fir.h:45-68).
+// LDS holds one tile's input span "phase-major": span element s goes to phase
+// p = s % D, row r = s / D, at p*RSP + (r % K)*RSK + r / K. Thread l computes K
+// consecutive outputs from a K-deep register window that slides one row per tap
+// step, so lanes read consecutive LDS words (conflict-free for any D) and every
+// row load feeds K outputs.
+struct FirArgs {
+    const void* hist;
+    const void* in;
+    const void* taps;   // ntaps elements of TT
+    void* out;
+    const float2* din;  // QUAD: y[-1] (carried)
+    float2* dinNext;    // QUAD: y[M-1]
+    double theta0, w;   // XL: phase of in[0], increment
+    int ntaps, H, count, D, Q, offset0, M, TMS, RSK, RSP;
+    float invDev;
+};
+
+template <typename DT, typename TT, int K, bool XL, bool QUAD, bool STEREO>
+__global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
+    const int NT = blockDim.x;       // 64, 128 or 256 (host picks the largest tile that fits LDS)
+    const int TM = NT * K;
+    constexpr int QOFF = QUAD ? 1 : 0;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    DT* X = reinterpret_cast<DT*>(smem);
+    TT* Hs = reinterpret_cast<TT*>(smem + sizeof(DT) * (size_t)a.D * a.RSP);
+
+    const int tid = threadIdx.x;
+    const int tile = blockIdx.x;
+    const int mFirst = tile * a.TMS - QOFF;                    // output of local index 0
+    const long long b0 = (long long)a.offset0 + (long long)mFirst * a.D;
+    const int rows = TM + a.Q;                                   // + 1 prefetch row
+    const int span = rows * a.D;
+    const DT* hist = reinterpret_cast<const DT*>(a.hist);
+    const DT* in = reinterpret_cast<const DT*>(a.in);
+    const TT* taps = reinterpret_cast<const TT*>(a.taps);
+
+    // taps -> LDS as [p][q] = taps[q*D + p] (zero past ntaps)
+    for (int e = tid; e < a.D * a.Q; e += NT) {
+        const int p = e / a.Q, q = e % a.Q;
+        const int j = q * a.D + p;
+        Hs[e] = j < a.ntaps ? taps[j] : zero_of<TT>();
+    }
+    // input span -> LDS (phase-major, row-swizzled)
+    for (int s = tid; s < span; s += NT) {
+        const long long b = b0 + s;
+        DT v = zero_of<DT>();
+        if (b >= 0) {
+            if (b < a.H) {
+                v = hist[b];
+            } else if (b - a.H < a.count) {
+                const long long i = b - a.H;
+                v = in[i];
+                if constexpr (XL) v = cmulf(v, nco(a.theta0, a.w, i));
+            }
+        }
+        const int p = s % a.D, r = s / a.D;
+        X[p * a.RSP + (r % K) * a.RSK + r / K] = v;
+    }
+    __syncthreads();
+
+    DT acc[K];
+#pragma unroll
+    for (int i = 0; i < K; i++) acc[i] = zero_of<DT>();
+    const int l = tid;
+    for (int p = 0; p < a.D; p++) {
+        const DT* Xp = X + p * a.RSP;
+        const TT* Hp = Hs + p * a.Q;
+        DT w[K];
+#pragma unroll
+        for (int i = 0; i < K; i++) w[i] = Xp[i * a.RSK + l];   // rows l*K + i
+        for (int q0 = 0; q0 < a.Q; q0 += K) {
+#pragma unroll
+            for (int u = 0; u < K; u++) {
+                const int q = q0 + u;
+                if (q < a.Q) {
+                    const TT h = Hp[q];
+#pragma unroll
+                    for (int i = 0; i < K; i++) mac(acc[i], w[(i + u) % K], h);
+                    const int rn = l * K + K + q;                 // next row for this slot
+                    w[u] = Xp[(rn % K) * a.RSK + rn / K];
+                }
+            }
+        }
+    }
+
+    if constexpr (QUAD) {
+        // FM quadrature (demod/quadrature.h:41-56): out = arg(y[m] * conj(y[m-1])) / dev
+        __shared__ float2 lastY[256];
+        lastY[l] = acc[K - 1];
+        __syncthreads();
+        float* out = reinterpret_cast<float*>(a.out);
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            const int m = mFirst + l * K + i;
+            if (m >= 0 && m >= tile * a.TMS && m < a.M) {
+                float2 prev;
+                if (m == 0) prev = a.din[0];
+                else if (i > 0) prev = acc[i - 1];
+                else prev = lastY[l - 1];
+                const float2 y = acc[i];
+                const float br = prev.x, bi = -prev.y;
+                const float re = (y.x * br) - (y.y * bi);
+                const float im = (y.y * br) + (y.x * bi);
+                out[m] = atan2f(im, re) * a.invDev;
+                if (m == a.M - 1) a.dinNext[0] = y;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            const int m = mFirst + l * K + i;
+            if (m < a.M && m < (tile + 1) * a.TMS) {
+                if constexpr (STEREO) {
+                    reinterpret_cast<float2*>(a.out)[m] = make_float2(acc[i], acc[i]);   // LRToStereo(l = r)
+                } else {
+                    reinterpret_cast<DT*>(a.out)[m] = acc[i];
+                }
+            }
+        }
+    }
+}
+
+// history for the next call: the last H elements of hist | xl(in)
+template <typename DT, bool XL>
+__global__ void fir_hist_kernel(const DT* __restrict__ hist, const DT* __restrict__ in, DT* __restrict__ next, int H,
+                                int count, double theta0, double w) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= H) return;
+    const long long b = (long long)count + k;
+    DT v;
+    if (b < H) {
+        v = hist[b];
+    } else {
+        const long long i = b - H;
+        v = in[i];
+        if constexpr (XL) v = cmulf(v, nco(theta0, w, i));
+    }
+    next[k] = v;
+}
+
+// --------------------------------------------------------------- xlator
+__global__ void xlator_kernel(const float2* __restrict__ in, float2* __restrict__ out, long long n, double theta0,
+                              double w) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = cmulf(in[i], nco(theta0, w, i));
+}
+
+// ----------------------------------------------------------- quadrature
+__global__ void quad_kernel(const float2* __restrict__ in, float* __restrict__ out, int n, const float2* __restrict__ din,
+                            float2* __restrict__ dinNext, float invDev) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float2 y = in[i];
+    const float2 d = i ? in[i - 1] : din[0];
+    const float br = d.x, bi = -d.y;
+    const float re = (y.x * br) - (y.y * bi);
+    const float im = (y.y * br) + (y.x * bi);
+    out[i] = atan2f(im, re) * invDev;
+    if (i == n - 1) dinNext[0] = y;
+}
+
+// ------------------------------------------------ polyphase resampler
+// multirate/polyphase_resampler.h:69-99 in closed form: with pos = offset*interp + phase,
+// output m uses pos_m = pos0 + m*decim -> (offset_m, phase_m) = divmod(pos_m, interp).
+template <typename DT>
+__global__ void poly_kernel(const DT* __restrict__ hist, const DT* __restrict__ in, const float* __restrict__ bank,
+                            DT* __restrict__ out, int H, int tpp, int interp, int decim, long long pos0, int M) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= M) return;
+    const long long pos = pos0 + (long long)m * decim;
+    const long long off = pos / interp;
+    const int ph = (int)(pos % interp);
+    const float* hb = bank + (size_t)ph * tpp;
+    DT acc = zero_of<DT>();
+    for (int j = 0; j < tpp; j++) {
+        const long long b = off + j;
+        const DT x = b < H ? hist[b] : in[b - H];
+        mac(acc, x, hb[j]);
+    }
+    out[m] = acc;
+}
+
+// ------------------------------------------------------------ converters
+__global__ void convert_kernel(int kind, const void* __restrict__ in, long long n, float* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float r;
+    switch (kind) {
+    case SDRGPU_CONV_U8: r = (((const uint8_t*)in)[i] - 128 + 0.5f) / (128.0f - 0.5f); break;
+    case SDRGPU_CONV_I16: r = (((const int16_t*)in)[i] + 0.5f) / (32768.0f - 0.5f); break;
+    case SDRGPU_CONV_I24: {
+        const uint8_t* p = (const uint8_t*)in + 3 * i;
+        int32_t v = (int32_t)((uint32_t)(p[0] | (p[1] << 8) | (p[2] << 16)) << 8) >> 8;
+        r = (v + 0.5f) / (8388608.0f - 0.5f);
+        break;
+    }
+    case SDRGPU_CONV_I32: r = (float)((((const int32_t*)in)[i] + 0.5) / (2147483648.0 - 0.5)); break;
+    case SDRGPU_CONV_F64: r = (float)((const double*)in)[i]; break;
+    default: r = ((float)((const int8_t*)in)[i]) * (float)(1.0 / 128.0f); break;
+    }
+    out[i] = r;
+}
+
+// ================================================================ host blocks
+int DevBuf::ensure(size_t want) {
+    if (want <= bytes) return SDRGPU_OK;
+    release();
+    size_t sz = std::max<size_t>(want, 256);
+    if (hipMalloc(&p, sz) != hipSuccess) {
+        p = nullptr;
+        set_error("hipMalloc(%zu) failed", sz);
+        return SDRGPU_ENOMEM;
+    }
+    bytes = sz;
+    return SDRGPU_OK;
+}
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+int PinnedBuf::ensure(size_t want) {
+    if (want <= bytes) return SDRGPU_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    size_t sz = std::max<size_t>(want, 256);
+    if (hipHostMalloc(&p, sz, hipHostMallocDefault) != hipSuccess) {
+        p = nullptr;
+        set_error("hipHostMalloc(%zu) failed", sz);
+        return SDRGPU_ENOMEM;
+    }
+    bytes = sz;
+    return SDRGPU_OK;
+}
+PinnedBuf::~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+}
+
+Block::~Block() {
+    if (own) (void)hipStreamDestroy(own);
+}
+int Block::init_stream() {
+    SDRGPU_HIP(hipSetDevice(device));
+    SDRGPU_HIP(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
+    return SDRGPU_OK;
+}
+
+// ------------------------------------------------------------------ FIR block
+struct FirBlock : Block {
+    int ttype = SDRGPU_F32, ntaps = 0, D = 1, offset = 0, Q = 1;
+    bool xl = false, quad = false, stereo = false;
+    double w = 0.0;         // XL increment
+    PhaseAcc phase;         // XL: phase of the next input sample
+    float invDev = 1.0f;    // QUAD
+    DevBuf taps, hist[2], din[2];
+    int cur = 0;            // ping-pong index
+
+    int setup(int dev, int dtype_, int ttype_, const float* t, int n, int decim) {
+        device = dev;
+        in_dtype = dtype_;
+        out_dtype = quad ? SDRGPU_F32 : (stereo ? SDRGPU_C64 : dtype_);
+        ttype = ttype_;
+        if (decim < 1) { set_error("fir: decimation %d < 1", decim); return SDRGPU_EARG; }
+        D = decim;
+        SDRGPU_CHECK(init_stream());
+        SDRGPU_CHECK(set_taps(t, n));
+        return SDRGPU_OK;
+    }
+    // FIR::setTaps (fir.h:31-52): history kept aligned to the newest sample;
+    // DecimatingFIR::setTaps resets the decimation phase (decimating_fir.h:19-26)
+    int set_taps(const float* t, int n) {
+        if (!t || n < 1 || n > 64001) { set_error("fir: tap count %d out of range [1, 64001]", n); return SDRGPU_EARG; }
+        SDRGPU_HIP(hipSetDevice(device));
+        const size_t es = esize(in_dtype);
+        const int oldH = ntaps > 0 ? ntaps - 1 : 0, newH = n - 1;
+        std::vector<unsigned char> oldHist((size_t)oldH * es), newHist((size_t)std::max(newH, 1) * es, 0);
+        if (oldH > 0) SDRGPU_HIP(hipMemcpy(oldHist.data(), hist[cur].p, oldHist.size(), hipMemcpyDeviceToHost));
+        const int keep = std::min(oldH, newH);
+        if (keep > 0) std::memcpy(newHist.data() + (size_t)(newH - keep) * es, oldHist.data() + (size_t)(oldH - keep) * es, keep * es);
+        for (int k = 0; k < 2; k++) SDRGPU_CHECK(hist[k].ensure(newHist.size()));
+        SDRGPU_HIP(hipMemcpy(hist[cur].p, newHist.data(), newHist.size(), hipMemcpyHostToDevice));
+        SDRGPU_CHECK(taps.ensure(sizeof(float) * n * (ttype == SDRGPU_C64 ? 2 : 1)));
+        SDRGPU_HIP(hipMemcpy(taps.p, t, sizeof(float) * n * (ttype == SDRGPU_C64 ? 2 : 1), hipMemcpyHostToDevice));
+        ntaps = n;
+        Q = (n + D - 1) / D;
+        offset = 0;
+        if (quad) {
+            for (int k = 0; k < 2; k++) SDRGPU_CHECK(din[k].ensure(sizeof(float2)));
+        }
+        return SDRGPU_OK;
+    }
+    int set_decimation(int d) {
+        if (d < 1) { set_error("fir: decimation %d < 1", d); return SDRGPU_EARG; }
+        D = d;
+        Q = (ntaps + D - 1) / D;
+        offset = 0;
+        return SDRGPU_OK;
+    }
+    int out_count(int count) override { return count > offset ? (count - offset + D - 1) / D : 0; }
+    int reset() override {
+        SDRGPU_HIP(hipSetDevice(device));
+        SDRGPU_HIP(hipMemset(hist[cur].p, 0, (size_t)std::max(ntaps - 1, 1) * esize(in_dtype)));
+        if (quad) SDRGPU_HIP(hipMemset(din[cur].p, 0, sizeof(float2)));
+        offset = 0;
+        phase.reset();
+        return SDRGPU_OK;
+    }
+    int choose_k() const {
+        // register blocking pays when a row feeds several taps per phase (Q large)
+        if (Q >= 16) return 4;
+        if (Q >= 6) return 2;
+        return 1;
+    }
+    int NT = 256;
+    template <typename DT, typename TT, int K, bool XL, bool QD, bool ST>
+    int launch_t(FirArgs& a, int tiles, size_t lds, hipStream_t s) {
+        auto k = fir_kernel<DT, TT, K, XL, QD, ST>;
+        SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(k, dim3(tiles), dim3(NT), lds, s, a);
+        SDRGPU_HIP(hipGetLastError());
+        return SDRGPU_OK;
+    }
+    template <typename DT, typename TT, bool XL, bool QD, bool ST>
+    int launch_k(FirArgs& a, int K, int tiles, size_t lds, hipStream_t s) {
+        if (K == 4) return launch_t<DT, TT, 4, XL, QD, ST>(a, tiles, lds, s);
+        if (K == 2) return launch_t<DT, TT, 2, XL, QD, ST>(a, tiles, lds, s);
+        return launch_t<DT, TT, 1, XL, QD, ST>(a, tiles, lds, s);
+    }
+    int run(const void* in, int count, void* out, hipStream_t s) override {
+        if (count < 0) { set_error("fir: negative count"); return SDRGPU_EARG; }
+        SDRGPU_HIP(hipSetDevice(device));
+        const int M = out_count(count);
+        const int H = ntaps - 1;
+        const double theta0 = phase.value();
+        if (M > 0) {
+            int K = choose_k();
+            // LDS budget: span (TM + Q + K rows) * D elements + taps; shrink K, then the
+            // tile's thread count, until it fits (large decimations: plan_8192 stage 0)
+            size_t es = esize(in_dtype), ts = (ttype == SDRGPU_C64 ? 8 : 4);
+            size_t lds = 0;
+            int RSK = 0, RSP = 0;
+            NT = 256;
+            for (;;) {
+                const int TM = NT * K;
+                const int rows = TM + Q + K;
+                RSK = (rows + K - 1) / K;
+                RSP = K * RSK + 1;
+                lds = es * (size_t)D * RSP + ts * (size_t)D * Q;
+                if (lds <= 150 * 1024) break;
+                if (K > 1) K /= 2;
+                else if (NT > 64) NT /= 2;
+                else break;
+            }
+            if (lds > 150 * 1024) {
+                set_error("fir: tile does not fit LDS (ntaps %d, decim %d)", ntaps, D);
+                return SDRGPU_EARG;
+            }
+            const int TM = NT * K;
+            const int TMS = quad ? TM - 1 : TM;
+            const int tiles = (M + TMS - 1) / TMS;
+            FirArgs a{};
+            a.hist = hist[cur].p; a.in = in; a.taps = taps.p; a.out = out;
+            a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
+            a.theta0 = theta0; a.w = w;
+            a.ntaps = ntaps; a.H = H; a.count = count; a.D = D; a.Q = Q; a.offset0 = offset; a.M = M;
+            a.TMS = TMS; a.RSK = RSK; a.RSP = RSP; a.invDev = invDev;
+            int rc;
+            if (in_dtype == SDRGPU_F32) {
+                rc = stereo ? launch_k<float, float, false, false, true>(a, K, tiles, lds, s)
+                            : launch_k<float, float, false, false, false>(a, K, tiles, lds, s);
+            } else if (ttype == SDRGPU_C64) {
+                rc = launch_k<float2, float2, false, false, false>(a, K, tiles, lds, s);
+            } else if (xl && quad) {
+                rc = launch_k<float2, float, true, true, false>(a, K, tiles, lds, s);
+            } else if (xl) {
+                rc = launch_k<float2, float, true, false, false>(a, K, tiles, lds, s);
+            } else if (quad) {
+                rc = launch_k<float2, float, false, true, false>(a, K, tiles, lds, s);
+            } else {
+                rc = launch_k<float2, float, false, false, false>(a, K, tiles, lds, s);
+            }
+            SDRGPU_CHECK(rc);
+        }
+        if (quad && M == 0) {
+            SDRGPU_HIP(hipMemcpyAsync(din[cur ^ 1].p, din[cur].p, sizeof(float2), hipMemcpyDeviceToDevice, s));
+        }
+        if (H > 0) {
+            const int nb = (H + 255) / 256;
+            if (in_dtype == SDRGPU_F32) {
+                hipLaunchKernelGGL((fir_hist_kernel<float, false>), dim3(nb), dim3(256), 0, s, hist[cur].as<float>(),
+                                   (const float*)in, hist[cur ^ 1].as<float>(), H, count, 0.0, 0.0);
+            } else if (xl) {
+                hipLaunchKernelGGL((fir_hist_kernel<float2, true>), dim3(nb), dim3(256), 0, s, hist[cur].as<float2>(),
+                                   (const float2*)in, hist[cur ^ 1].as<float2>(), H, count, theta0, w);
+            } else {
+                hipLaunchKernelGGL((fir_hist_kernel<float2, false>), dim3(nb), dim3(256), 0, s, hist[cur].as<float2>(),
+                                   (const float2*)in, hist[cur ^ 1].as<float2>(), H, count, 0.0, 0.0);
+            }
+            SDRGPU_HIP(hipGetLastError());
+        }
+        cur ^= 1;
+        offset = offset + M * D - count;
+        if (xl) phase.advance(w, count);
+        return M;
+    }
+};
+
+// --------------------------------------------------------------- xlator block
+struct XlatorBlock : Block {
+    double w = 0.0;
+    PhaseAcc phase;
+    int out_count(int count) override { return count; }
+    int reset() override { phase.reset(); return SDRGPU_OK; }
+    int run(const void* in, int count, void* out, hipStream_t s) override {
+        SDRGPU_HIP(hipSetDevice(device));
+        if (count > 0) {
+            hipLaunchKernelGGL(xlator_kernel, dim3((count + 255) / 256), dim3(256), 0, s, (const float2*)in, (float2*)out,
+                               (long long)count, phase.value(), w);
+            SDRGPU_HIP(hipGetLastError());
+        }
+        phase.advance(w, count);
+        return count;
+    }
+};
+
+// ------------------------------------------------------------ quadrature block
+struct QuadBlock : Block {
+    float invDev = 1.0f;
+    DevBuf din[2];
+    int cur = 0;
+    int out_count(int count) override { return count; }
+    int reset() override {
+        SDRGPU_HIP(hipSetDevice(device));
+        SDRGPU_HIP(hipMemset(din[cur].p, 0, sizeof(float2)));
+        return SDRGPU_OK;
+    }
+    int run(const void* in, int count, void* out, hipStream_t s) override {
+        SDRGPU_HIP(hipSetDevice(device));
+        if (count <= 0) return 0;
+        hipLaunchKernelGGL(quad_kernel, dim3((count + 255) / 256), dim3(256), 0, s, (const float2*)in, (float*)out, count,
+                           din[cur].as<float2>(), din[cur ^ 1].as<float2>(), invDev);
+        SDRGPU_HIP(hipGetLastError());
+        cur ^= 1;
+        return count;
+    }
+};
+
+// ------------------------------------------------------------- polyphase block
+struct PolyBlock : Block {
+    int interp = 1, decim = 1, tpp = 1, phase = 0, offset = 0;
+    DevBuf bank, hist[2];
+    int cur = 0;
+    int setup(int dev, int dtype, int ip, int dc, const float* taps, int n) {
+        device = dev;
+        in_dtype = out_dtype = dtype;
+        if (ip < 1 || dc < 1 || !taps || n < 1) { set_error("polyphase: bad ratio/taps"); return SDRGPU_EARG; }
+        interp = ip; decim = dc;
+        SDRGPU_CHECK(init_stream());
+        // multirate/polyphase_bank.h:15-47: phases[P-1-(i%P)][i/P] = taps[i]
+        tpp = (n + interp - 1) / interp;
+        std::vector<float> b((size_t)interp * tpp, 0.0f);
+        for (int i = 0; i < interp * tpp; i++)
+            b[(size_t)((interp - 1) - (i % interp)) * tpp + i / interp] = (i < n) ? taps[i] : 0.0f;
+        SDRGPU_CHECK(bank.ensure(sizeof(float) * b.size()));
+        SDRGPU_HIP(hipMemcpy(bank.p, b.data(), sizeof(float) * b.size(), hipMemcpyHostToDevice));
+        for (int k = 0; k < 2; k++) SDRGPU_CHECK(hist[k].ensure(esize(dtype) * std::max(tpp - 1, 1)));
+        return reset();
+    }
+    int out_count(int count) override {
+        // while (offset < count) { out; phase += decim; offset += phase / interp; phase %= interp; }
+        long long pos = (long long)offset * interp + phase;
+        long long lim = (long long)count * interp;
+        if (pos >= lim) return 0;
+        return (int)((lim - 1 - pos) / decim + 1);
+    }
+    int reset() override {
+        SDRGPU_HIP(hipSetDevice(device));
+        SDRGPU_HIP(hipMemset(hist[cur].p, 0, esize(in_dtype) * std::max(tpp - 1, 1)));
+        phase = 0; offset = 0;
+        return SDRGPU_OK;
+    }
+    int run(const void* in, int count, void* out, hipStream_t s) override {
+        SDRGPU_HIP(hipSetDevice(device));
+        const int M = out_count(count);
+        const int H = tpp - 1;
+        const long long pos0 = (long long)offset * interp + phase;
+        if (M > 0) {
+            if (in_dtype == SDRGPU_F32)
+                hipLaunchKernelGGL((poly_kernel<float>), dim3((M + 255) / 256), dim3(256), 0, s, hist[cur].as<float>(),
+                                   (const float*)in, bank.as<float>(), (float*)out, H, tpp, interp, decim, pos0, M);
+            else
+                hipLaunchKernelGGL((poly_kernel<float2>), dim3((M + 255) / 256), dim3(256), 0, s, hist[cur].as<float2>(),
+                                   (const float2*)in, bank.as<float>(), (float2*)out, H, tpp, interp, decim, pos0, M);
+            SDRGPU_HIP(hipGetLastError());
+        }
+        if (H > 0) {
+            const int nb = (H + 255) / 256;
+            if (in_dtype == SDRGPU_F32)
+                hipLaunchKernelGGL((fir_hist_kernel<float, false>), dim3(nb), dim3(256), 0, s, hist[cur].as<float>(),
+                                   (const float*)in, hist[cur ^ 1].as<float>(), H, count, 0.0, 0.0);
+            else
+                hipLaunchKernelGGL((fir_hist_kernel<float2, false>), dim3(nb), dim3(256), 0, s, hist[cur].as<float2>(),
+                                   (const float2*)in, hist[cur ^ 1].as<float2>(), H, count, 0.0, 0.0);
+            SDRGPU_HIP(hipGetLastError());
+            cur ^= 1;
+        }
+        long long pos = pos0 + (long long)M * decim;
+        offset = (int)(pos / interp) - count;
+        phase = (int)(pos % interp);
+        return M;
+    }
+};
+
+// ---------------------------------------------------------- chains of blocks
+// Runs children back to back on one stream through device scratch buffers.
+struct ChainBlock : Block {
+    std::vector<std::unique_ptr<Block>> kids;
+    DevBuf scratch[2];
+    int out_count(int count) override {
+        for (auto& k : kids) count = k->out_count(count);   // (does not mutate state)
+        return count;
+    }
+    int reset() override {
+        for (auto& k : kids) SDRGPU_CHECK(k->reset());
+        return SDRGPU_OK;
+    }
+    int run(const void* in, int count, void* out, hipStream_t s) override {
+        if (kids.empty()) {
+            SDRGPU_HIP(hipMemcpyAsync(out, in, (size_t)count * esize(in_dtype), hipMemcpyDeviceToDevice, s));
+            return count;
+        }
+        // upper bound of intermediate sizes: each child's output never exceeds its input here
+        const void* src = in;
+        int n = count;
+        for (size_t i = 0; i < kids.size(); i++) {
+            void* dst;
+            if (i + 1 == kids.size()) {
+                dst = out;
+            } else {
+                const int m = kids[i]->out_count(n);
+                SDRGPU_CHECK(scratch[i & 1].ensure((size_t)std::max(m, 1) * esize(kids[i]->out_dtype)));
+                dst = scratch[i & 1].p;
+            }
+            n = kids[i]->run(src, n, dst, s);
+            if (n < 0) return n;
+            src = dst;
+        }
+        return n;
+    }
+};
+
+static std::unique_ptr<FirBlock> make_fir(int dev, int dtype, int ttype, const float* taps, int n, int decim, int* rc,
+                                          bool xl = false, double w = 0.0, bool quad = false, float invDev = 1.0f,
+                                          bool stereo = false) {
+    auto f = std::make_unique<FirBlock>();
+    f->xl = xl; f->w = w; f->quad = quad; f->invDev = invDev; f->stereo = stereo;
+    *rc = f->setup(dev, dtype, ttype, taps, n, decim);
+    if (*rc >= 0) *rc = f->reset();
+    return f;
+}
+
+// PowerDecimator<T> (multirate/power_decimator.h): cascade of plan stages. With
+// `xlFirst` the RxVFO's xlator is fused into the first (full-rate) stage.
+static int build_power_decim(ChainBlock* c, int dev, int dtype, int ratio, bool xlFirst, double w) {
+    if (ratio == 1) return SDRGPU_OK;
+    int d[8], n[8];
+    const float* t[8];
+    int ns = decim_plan(ratio, d, n, t);
+    if (ns < 0) return ns;
+    for (int i = 0; i < ns; i++) {
+        int rc;
+        auto f = make_fir(dev, dtype, SDRGPU_F32, t[i], n[i], d[i], &rc, xlFirst && i == 0, w);
+        if (rc < 0) return rc;
+        c->kids.push_back(std::move(f));
+    }
+    return SDRGPU_OK;
+}
+
+// RationalResampler<T>::reconfigure (multirate/rational_resampler.h:121-167)
+struct RationalPlan {
+    int mode = 3, predec = 1, interp = 1, decim = 1;
+    std::vector<float> taps;
+};
+static int plan_rational(double inSr, double outSr, RationalPlan& rp) {
+    if (!(inSr > 0) || !(outSr > 0)) { set_error("rational resampler: bad samplerates"); return SDRGPU_EARG; }
+    const int maxRatio = 8192;
+    int predecPower = std::min<int>((int)std::floor(std::log2(inSr / outSr)), maxRatio);
+    int predecRatio = std::min<int>(predecPower >= 0 && predecPower < 31 ? (1 << predecPower) : maxRatio, maxRatio);
+    double intSr = inSr;
+    bool useDecim = (inSr > outSr && predecPower > 0);
+    if (useDecim) intSr = inSr / (double)predecRatio;
+    rp.predec = useDecim ? predecRatio : 1;
+    int IntSR = (int)std::round(intSr), OutSR = (int)std::round(outSr);
+    int g = std::gcd(IntSR, OutSR);
+    rp.interp = OutSR / g;
+    rp.decim = IntSR / g;
+    if (rp.interp == rp.decim) { rp.mode = useDecim ? 1 : 3; return SDRGPU_OK; }
+    double tapSr = intSr * (double)rp.interp;
+    double tapBw = std::min<double>(inSr, outSr) / 2.0;
+    int n = taps_low_pass(tapBw, tapBw * 0.1, tapSr, 0, nullptr);
+    if (n < 1) return n < 0 ? n : SDRGPU_EARG;
+    rp.taps.resize(n);
+    taps_low_pass(tapBw, tapBw * 0.1, tapSr, 0, rp.taps.data());
+    for (auto& v : rp.taps) v *= (float)rp.interp;
+    rp.mode = useDecim ? 0 : 2;
+    return SDRGPU_OK;
+}
+
+static int build_rational(ChainBlock* c, int dev, int dtype, double inSr, double outSr, bool xlFirst, double w) {
+    RationalPlan rp;
+    SDRGPU_CHECK(plan_rational(inSr, outSr, rp));
+    bool xlDone = false;
+    if (rp.mode == 0 || rp.mode == 1) {
+        SDRGPU_CHECK(build_power_decim(c, dev, dtype, rp.predec, xlFirst, w));
+        xlDone = true;
+    }
+    if (xlFirst && !xlDone) {
+        auto x = std::make_unique<XlatorBlock>();
+        x->device = dev; x->w = w;
+        SDRGPU_CHECK(x->init_stream());
+        c->kids.insert(c->kids.begin(), std::move(x));
+    }
+    if (rp.mode == 0 || rp.mode == 2) {
+        auto p = std::make_unique<PolyBlock>();
+        SDRGPU_CHECK(p->setup(dev, dtype, rp.interp, rp.decim, rp.taps.data(), (int)rp.taps.size()));
+        c->kids.push_back(std::move(p));
+    }
+    return SDRGPU_OK;
+}
+
+// RxVFO (channel/rx_vfo.h:24-121)
+struct VfoBlock : ChainBlock {
+    double inSr = 0, outSr = 0, bw = 0, offset = 0;
+    int build() {
+        kids.clear();
+        const double w = xlator_effective_omega(hz_to_rads(-offset, inSr));
+        SDRGPU_CHECK(build_rational(this, device, SDRGPU_C64, inSr, outSr, true, w));
+        if (bw != outSr) {
+            double fw = bw / 2.0;
+            int n = taps_low_pass(fw, fw * 0.1, outSr, 0, nullptr);
+            if (n < 1) return n < 0 ? n : SDRGPU_EARG;
+            std::vector<float> t(n);
+            taps_low_pass(fw, fw * 0.1, outSr, 0, t.data());
+            int rc;
+            auto f = make_fir(device, SDRGPU_C64, SDRGPU_F32, t.data(), n, 1, &rc);
+            if (rc < 0) return rc;
+            kids.push_back(std::move(f));
+        }
+        return SDRGPU_OK;
+    }
+    // setOffset keeps the running NCO phase (frequency_xlator.h:25-29)
+    int set_offset(double off) {
+        offset = off;
+        const double w = xlator_effective_omega(hz_to_rads(-offset, inSr));
+        for (auto& k : kids) {
+            if (auto* f = dynamic_cast<FirBlock*>(k.get()); f && f->xl) {
+                f->phase.advance(0.0, 0);
+                f->w = w;
+                return SDRGPU_OK;
+            }
+            if (auto* x = dynamic_cast<XlatorBlock*>(k.get())) {
+                x->w = w;
+                return SDRGPU_OK;
+            }
+        }
+        return SDRGPU_OK;
+    }
+};
+
+}  // namespace sdrgpu
+
+using namespace sdrgpu;
+
+// ================================================================== C ABI
+static int wrap(sdrgpu_block** h, Block* b, int rc) {
+    if (rc < 0) { delete b; return rc; }
+    *h = new sdrgpu_block{b};
+    return SDRGPU_OK;
+}
+#define NEED_HANDLE(h) do { if (!(h) || !(h)->impl) { set_error("null block handle"); return SDRGPU_EARG; } } while (0)
+
+extern "C" int sdrgpu_xlator_create(sdrgpu_block** h, int device, double offsetRad) {
+    if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
+    auto* x = new XlatorBlock();
+    x->device = device;
+    x->w = xlator_effective_omega(offsetRad);
+    return wrap(h, x, x->init_stream());
+}
+extern "C" int sdrgpu_xlator_set_offset(sdrgpu_block* h, double offsetRad) {
+    NEED_HANDLE(h);
+    auto* x = dynamic_cast<XlatorBlock*>(h->impl);
+    if (!x) { set_error("not an xlator"); return SDRGPU_ESTATE; }
+    x->w = xlator_effective_omega(offsetRad);
+    return SDRGPU_OK;
+}
+
+extern "C" int sdrgpu_fir_create(sdrgpu_block** h, int device, int dtype, int ttype, const float* taps, int ntaps, int decim) {
+    if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
+    if ((dtype != SDRGPU_F32 && dtype != SDRGPU_C64) || (ttype != SDRGPU_F32 && ttype != SDRGPU_C64) ||
+        (dtype == SDRGPU_F32 && ttype == SDRGPU_C64)) {
+        set_error("fir_create: unsupported (dtype %d, ttype %d)", dtype, ttype);
+        return SDRGPU_EARG;
+    }
+    int rc;
+    auto f = make_fir(device, dtype, ttype, taps, ntaps, decim, &rc);
+    return wrap(h, f.release(), rc);
+}
+extern "C" int sdrgpu_fir_set_taps(sdrgpu_block* h, const float* taps, int ntaps) {
+    NEED_HANDLE(h);
+    auto* f = dynamic_cast<FirBlock*>(h->impl);
+    if (!f) { set_error("not a FIR"); return SDRGPU_ESTATE; }
+    return f->set_taps(taps, ntaps);
+}
+extern "C" int sdrgpu_fir_set_decimation(sdrgpu_block* h, int decim) {
+    NEED_HANDLE(h);
+    auto* f = dynamic_cast<FirBlock*>(h->impl);
+    if (!f) { set_error("not a FIR"); return SDRGPU_ESTATE; }
+    return f->set_decimation(decim);
+}
+
+extern "C" int sdrgpu_quadrature_create(sdrgpu_block** h, int device, double deviationRad) {
+    if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
+    auto* q = new QuadBlock();
+    q->device = device; q->in_dtype = SDRGPU_C64; q->out_dtype = SDRGPU_F32;
+    q->invDev = (float)(1.0 / deviationRad);
+    int rc = q->init_stream();
+    for (int k = 0; k < 2 && rc >= 0; k++) rc = q->din[k].ensure(sizeof(float2));
+    if (rc >= 0) rc = q->reset();
+    return wrap(h, q, rc);
+}
+extern "C" int sdrgpu_quadrature_set_deviation(sdrgpu_block* h, double deviationRad) {
+    NEED_HANDLE(h);
+    if (auto* q = dynamic_cast<QuadBlock*>(h->impl)) { q->invDev = (float)(1.0 / deviationRad); return SDRGPU_OK; }
+    if (auto* f = dynamic_cast<FirBlock*>(h->impl); f && f->quad) { f->invDev = (float)(1.0 / deviationRad); return SDRGPU_OK; }
+    set_error("not a quadrature demodulator");
+    return SDRGPU_ESTATE;
+}
+
+extern "C" int sdrgpu_power_decimator_create(sdrgpu_block** h, int device, int dtype, int ratio) {
+    if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
+    if (ratio < 1 || (ratio & (ratio - 1)) || ratio > (8192)) {
+        set_error("power_decimator: ratio %d must be a power of two <= 8192", ratio);   // checkRatio
+        return SDRGPU_EARG;
+    }
+    auto* c = new ChainBlock();
+    c->device = device; c->in_dtype = c->out_dtype = dtype;
+    int rc = c->init_stream();
+    if (rc >= 0) rc = build_power_decim(c, device, dtype, ratio, false, 0.0);
+    return wrap(h, c, rc);
+}
+
+extern "C" int sdrgpu_polyphase_resampler_create(sdrgpu_block** h, int device, int dtype, int interp, int decim,
+                                                 const float* taps, int ntaps) {
+    if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
+    auto* p = new PolyBlock();
+    return wrap(h, p, p->setup(device, dtype, interp, decim, taps, ntaps));
+}
+
+extern "C" int sdrgpu_rational_resampler_create(sdrgpu_block** h, int device, int dtype, double inSr, double outSr) {
+    if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
+    auto* c = new ChainBlock();
+    c->device = device; c->in_dtype = c->out_dtype = dtype;
+    int rc = c->init_stream();
+    if (rc >= 0) rc = build_rational(c, device, dtype, inSr, outSr, false, 0.0);
+    return wrap(h, c, rc);
+}
+
+extern "C" int sdrgpu_rxvfo_create(sdrgpu_block** h, int device, double inSr, double outSr, double bw, double offset) {
+    if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
+    auto* v = new VfoBlock();
+    v->device = device; v->in_dtype = v->out_dtype = SDRGPU_C64;
+    v->inSr = inSr; v->outSr = outSr; v->bw = bw; v->offset = offset;
+    int rc = v->init_stream();
+    if (rc >= 0) rc = v->build();
+    return wrap(h, v, rc);
+}
+extern "C" int sdrgpu_rxvfo_set_offset(sdrgpu_block* h, double offset) {
+    NEED_HANDLE(h);
+    auto* v = dynamic_cast<VfoBlock*>(h->impl);
+    if (!v) { set_error("not an RxVFO"); return SDRGPU_ESTATE; }
+    return v->set_offset(offset);
+}
+
+extern "C" int sdrgpu_ddc_fm_create(sdrgpu_block** h, int device, double offsetRad, const float* taps, int ntaps, int decim,
+                                    double deviationRad) {
+    if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
+    int rc;
+    auto f = make_fir(device, SDRGPU_C64, SDRGPU_F32, taps, ntaps, decim, &rc, true, xlator_effective_omega(offsetRad),
+                      true, (float)(1.0 / deviationRad));
+    return wrap(h, f.release(), rc);
+}
+
+// FM<float> (demod/fm.h:25-133): quadrature(bw/2) -> optional LPF/HPF/BPF
+extern "C" int sdrgpu_fm_create(sdrgpu_block** h, int device, double samplerate, double bandwidth, int lowPass, int highPass) {
+    if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
+    auto* c = new ChainBlock();
+    c->device = device; c->in_dtype = SDRGPU_C64; c->out_dtype = SDRGPU_F32;
+    int rc = c->init_stream();
+    sdrgpu_block* qh = nullptr;
+    if (rc >= 0) rc = sdrgpu_quadrature_create(&qh, device, hz_to_rads(bandwidth / 2.0, samplerate));
+    if (rc >= 0) { c->kids.emplace_back(qh->impl); delete qh; }
+    if (rc >= 0 && (lowPass || highPass)) {
+        int n;
+        std::vector<float> t;
+        if (lowPass && highPass) {
+            n = taps_band_pass_f(300.0, bandwidth / 2.0, 100.0, samplerate, 0, nullptr);
+            if (n > 0) { t.resize(n); taps_band_pass_f(300.0, bandwidth / 2.0, 100.0, samplerate, 0, t.data()); }
+        } else if (highPass) {
+            n = taps_high_pass(300.0, 100.0, samplerate, 0, nullptr);
+            if (n > 0) { t.resize(n); taps_high_pass(300.0, 100.0, samplerate, 0, t.data()); }
+        } else {
+            n = taps_low_pass(bandwidth / 2.0, (bandwidth / 2.0) * 0.1, samplerate, 0, nullptr);
+            if (n > 0) { t.resize(n); taps_low_pass(bandwidth / 2.0, (bandwidth / 2.0) * 0.1, samplerate, 0, t.data()); }
+        }
+        rc = n < 1 ? (n < 0 ? n : SDRGPU_EARG) : SDRGPU_OK;
+        if (rc >= 0) {
+            auto f = make_fir(device, SDRGPU_F32, SDRGPU_F32, t.data(), n, 1, &rc);
+            if (rc >= 0) c->kids.push_back(std::move(f));
+        }
+    }
+    return wrap(h, c, rc);
+}
+
+// BroadcastFM, stereo == false (demod/broadcast_fm.h:144-215): quadrature(dev) ->
+// 228-tap (at 240 kS/s) audio LPF lowPass(15 kHz, 4 kHz) -> LRToStereo(l = r)
+extern "C" int sdrgpu_wfm_create(sdrgpu_block** h, int device, double deviation, double samplerate, int lowPass) {
+    if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
+    auto* c = new ChainBlock();
+    c->device = device; c->in_dtype = SDRGPU_C64; c->out_dtype = SDRGPU_C64;
+    int rc = c->init_stream();
+    sdrgpu_block* qh = nullptr;
+    if (rc >= 0) rc = sdrgpu_quadrature_create(&qh, device, hz_to_rads(deviation, samplerate));
+    if (rc >= 0) { c->kids.emplace_back(qh->impl); delete qh; }
+    if (rc >= 0) {
+        int n = taps_low_pass(15000.0, 4000.0, samplerate, 0, nullptr);
+        std::vector<float> t(std::max(n, 1), 1.0f);
+        if (lowPass && n > 0) taps_low_pass(15000.0, 4000.0, samplerate, 0, t.data());
+        else n = 1;   // unfiltered MPX: identity tap, same stereo interleave
+        auto f = make_fir(device, SDRGPU_F32, SDRGPU_F32, t.data(), n, 1, &rc, false, 0.0, false, 1.0f, true);
+        if (rc >= 0) c->kids.push_back(std::move(f));
+    }
+    return wrap(h, c, rc);
+}
+
+extern "C" int sdrgpu_block_out_count(sdrgpu_block* h, int count) {
+    NEED_HANDLE(h);
+    return h->impl->out_count(count);
+}
+
+extern "C" int sdrgpu_block_process_dev(sdrgpu_block* h, const void* in, int count, void* out, void* stream) {
+    NEED_HANDLE(h);
+    if (count < 0 || (count > 0 && (!in || !out))) { set_error("process: bad buffers"); return SDRGPU_EARG; }
+    Block* b = h->impl;
+    return b->run(in, count, out, stream ? (hipStream_t)stream : b->own);
+}
+
+extern "C" int sdrgpu_block_process(sdrgpu_block* h, const void* in, int count, void* out) {
+    NEED_HANDLE(h);
+    if (count < 0 || (count > 0 && (!in || !out))) { set_error("process: bad buffers"); return SDRGPU_EARG; }
+    Block* b = h->impl;
+    SDRGPU_HIP(hipSetDevice(b->device));
+    const size_t inB = (size_t)std::max(count, 1) * esize(b->in_dtype);
+    const int mExp = b->out_count(count);
+    const size_t outB = (size_t)std::max(mExp, 1) * esize(b->out_dtype);
+    SDRGPU_CHECK(b->pin_in.ensure(inB));
+    SDRGPU_CHECK(b->pin_out.ensure(outB));
+    SDRGPU_CHECK(b->dev_in.ensure(inB));
+    SDRGPU_CHECK(b->dev_out.ensure(outB));
+    if (count > 0) {
+        std::memcpy(b->pin_in.p, in, (size_t)count * esize(b->in_dtype));
+        SDRGPU_HIP(hipMemcpyAsync(b->dev_in.p, b->pin_in.p, (size_t)count * esize(b->in_dtype), hipMemcpyHostToDevice, b->own));
+    }
+    int m = b->run(b->dev_in.p, count, b->dev_out.p, b->own);
+    if (m < 0) return m;
+    if (m > 0) SDRGPU_HIP(hipMemcpyAsync(b->pin_out.p, b->dev_out.p, (size_t)m * esize(b->out_dtype), hipMemcpyDeviceToHost, b->own));
+    SDRGPU_HIP(hipStreamSynchronize(b->own));
+    if (m > 0) std::memcpy(out, b->pin_out.p, (size_t)m * esize(b->out_dtype));
+    return m;
+}
+
+extern "C" int sdrgpu_block_reset(sdrgpu_block* h) {
+    NEED_HANDLE(h);
+    int rc = h->impl->reset();
+    if (rc >= 0) SDRGPU_HIP(hipDeviceSynchronize());
+    return rc;
+}
+
+extern "C" int sdrgpu_block_destroy(sdrgpu_block* h) {
+    if (!h) return SDRGPU_OK;
+    if (h->impl) {
+        (void)hipSetDevice(h->impl->device);
+        (void)hipDeviceSynchronize();
+        delete h->impl;
+    }
+    delete h;
+    return SDRGPU_OK;
+}
+
+extern "C" int sdrgpu_convert_dev(int device, int kind, const void* in, long long n, float* out, void* stream) {
+    if (kind < SDRGPU_CONV_U8 || kind > SDRGPU_CONV_I8 || n < 0 || (n > 0 && (!in || !out))) {
+        set_error("convert: bad argument");
+        return SDRGPU_EARG;
+    }
+    SDRGPU_HIP(hipSetDevice(device));
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(convert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, kind, in, n, out);
+    SDRGPU_HIP(hipGetLastError());
+    return (int)std::min<long long>(n, 0x7fffffff);
+}
+
+extern "C" int sdrgpu_convert(int device, int kind, const void* in, long long n, float* out) {
+    static const int isz[] = {1, 2, 3, 4, 8, 1};
+    if (kind < SDRGPU_CONV_U8 || kind > SDRGPU_CONV_I8 || n < 0) { set_error("convert: bad argument"); return SDRGPU_EARG; }
+    if (n == 0) return 0;
+    SDRGPU_HIP(hipSetDevice(device));
+    void* din = nullptr;
+    float* dout = nullptr;
+    SDRGPU_HIP(hipMalloc(&din, (size_t)n * isz[kind]));
+    if (hipMalloc((void**)&dout, (size_t)n * sizeof(float)) != hipSuccess) {
+        (void)hipFree(din);
+        set_error("convert: hipMalloc failed");
+        return SDRGPU_ENOMEM;
+    }
+    int rc = SDRGPU_OK;
+    if (hipMemcpy(din, in, (size_t)n * isz[kind], hipMemcpyHostToDevice) != hipSuccess) rc = SDRGPU_EHIP;
+    if (rc >= 0) rc = sdrgpu_convert_dev(device, kind, din, n, dout, nullptr);
+    if (rc >= 0 && hipMemcpy(out, dout, (size_t)n * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) rc = SDRGPU_EHIP;
+    (void)hipFree(din);
+    (void)hipFree(dout);
+    if (rc == SDRGPU_EHIP) set_error("convert: hipMemcpy failed");
+    return rc < 0 ? rc : (int)std::min<long long>(n, 0x7fffffff);
+}

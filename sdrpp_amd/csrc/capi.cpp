@@ -1,0 +1,86 @@
+// C ABI: runtime helpers and the host-side design entry points of libsdrgpu.
+#include "sdrgpu_internal.h"
+
+namespace sdrgpu { const char* last_error(); }
+using namespace sdrgpu;
+
+extern "C" int sdrgpu_version(void) { return SDRGPU_VERSION; }
+extern "C" const char* sdrgpu_last_error(void) { return last_error(); }
+
+extern "C" int sdrgpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+extern "C" int sdrgpu_malloc(int device, void** dptr, size_t bytes) {
+    if (!dptr) { set_error("malloc: null out pointer"); return SDRGPU_EARG; }
+    SDRGPU_HIP(hipSetDevice(device));
+    SDRGPU_HIP(hipMalloc(dptr, bytes));
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_free(void* dptr) {
+    SDRGPU_HIP(hipFree(dptr));
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
+    SDRGPU_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
+    SDRGPU_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    SDRGPU_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_stream_create(int device, void** stream) {
+    if (!stream) { set_error("stream_create: null out pointer"); return SDRGPU_EARG; }
+    SDRGPU_HIP(hipSetDevice(device));
+    hipStream_t s;
+    SDRGPU_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = (void*)s;
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_stream_destroy(void* stream) {
+    SDRGPU_HIP(hipStreamDestroy((hipStream_t)stream));
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_stream_synchronize(void* stream) {
+    SDRGPU_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_host_register(void* ptr, size_t bytes) {
+    SDRGPU_HIP(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_host_unregister(void* ptr) {
+    SDRGPU_HIP(hipHostUnregister(ptr));
+    return SDRGPU_OK;
+}
+
+extern "C" int sdrgpu_create_window(int type, float* buffer, int size, int centered) {
+    return create_window(type, buffer, size, centered);
+}
+extern "C" void sdrgpu_gen_reshape_params(double sampleRate, int size, double rate, int* skip, int* nz) {
+    // IQFrontEnd::genReshapeParams (signal_path/iq_frontend.h:56-60)
+    int fftInterval = (int)std::round(sampleRate / rate);
+    int n = fftInterval < size ? fftInterval : size;
+    if (nz) *nz = n;
+    if (skip) *skip = fftInterval - n;
+}
+extern "C" int sdrgpu_taps_estimate_count(double transWidth, double sampleRate) {
+    return (int)(3.8 * sampleRate / transWidth);
+}
+extern "C" int sdrgpu_taps_low_pass(double cutoff, double transWidth, double sampleRate, int odd, float* out) {
+    return taps_low_pass(cutoff, transWidth, sampleRate, odd, out);
+}
+extern "C" int sdrgpu_taps_high_pass(double cutoff, double transWidth, double sampleRate, int odd, float* out) {
+    return taps_high_pass(cutoff, transWidth, sampleRate, odd, out);
+}
+extern "C" int sdrgpu_taps_band_pass_f(double start, double stop, double transWidth, double sampleRate, int odd, float* out) {
+    return taps_band_pass_f(start, stop, transWidth, sampleRate, odd, out);
+}
+extern "C" int sdrgpu_taps_band_pass_c(double start, double stop, double transWidth, double sampleRate, int odd, float* out) {
+    return taps_band_pass_c(start, stop, transWidth, sampleRate, odd, out);
+}
+extern "C" int sdrgpu_decim_plan(int ratio, int* decims, int* ntaps, const float** taps) {
+    return decim_plan(ratio, decims, ntaps, taps);
+}

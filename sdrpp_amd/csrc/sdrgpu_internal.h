@@ -1,0 +1,93 @@
+// Internal declarations shared by the libsdrgpu translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+#include "../../include/sdrgpu.h"
+
+namespace sdrgpu {
+
+void set_error(const char* fmt, ...);
+
+#define SDRGPU_HIP(call)                                                              \
+    do {                                                                              \
+        hipError_t e_ = (call);                                                       \
+        if (e_ != hipSuccess) {                                                       \
+            ::sdrgpu::set_error("%s failed: %s (%s:%d)", #call, hipGetErrorName(e_),  \
+                                __FILE__, __LINE__);                                  \
+            return SDRGPU_EHIP;                                                       \
+        }                                                                             \
+    } while (0)
+
+#define SDRGPU_CHECK(call)                 \
+    do {                                   \
+        int r_ = (call);                   \
+        if (r_ < 0) return r_;             \
+    } while (0)
+
+// Device buffer owned by a handle; grows on demand (never inside a capture).
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t want);
+    void release();
+    ~DevBuf() { release(); }
+    template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// Pinned host staging for the host-pointer (drop-in) call style.
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t want);
+    ~PinnedBuf();
+};
+
+inline size_t esize(int dtype) { return dtype == SDRGPU_C64 ? 8 : 4; }
+
+// ---- host-side design (host_design.cpp) -----------------------------------
+double window_value(int type, double n, double N);
+int create_window(int type, float* buffer, int size, int centered);
+int taps_low_pass(double cutoff, double tw, double fs, int odd, float* out);
+int taps_high_pass(double cutoff, double tw, double fs, int odd, float* out);
+int taps_band_pass_f(double start, double stop, double tw, double fs, int odd, float* out);
+int taps_band_pass_c(double start, double stop, double tw, double fs, int odd, float* out);
+int decim_plan(int ratio, int* decims, int* ntaps, const float** taps);
+double hz_to_rads(double f, double fs);
+double xlator_effective_omega(double offsetRad);
+
+// Double-double phase accumulator: keeps (w * n) mod 2pi to ~1e-16 rad over
+// arbitrarily long streams (the NCO origin of the next call).
+struct PhaseAcc {
+    double hi = 0.0, lo = 0.0;
+    void reset() { hi = lo = 0.0; }
+    void advance(double w, long long n);
+    double value() const { return hi + lo; }
+};
+
+// ---- blocks ------------------------------------------------------------------
+struct Block {
+    int device = 0;
+    int in_dtype = SDRGPU_C64, out_dtype = SDRGPU_C64;
+    hipStream_t own = nullptr;
+    PinnedBuf pin_in, pin_out;
+    DevBuf dev_in, dev_out;
+    virtual ~Block();
+    int init_stream();
+    // exact number of outputs the next process() of `count` inputs yields
+    virtual int out_count(int count) = 0;
+    // asynchronous device-side processing on `s`; returns the output count
+    virtual int run(const void* in, int count, void* out, hipStream_t s) = 0;
+    virtual int reset() = 0;
+};
+
+// kernels (fir.hip / fft.hip)
+struct FirState;   // defined in fir.hip
+
+}  // namespace sdrgpu
+
+struct sdrgpu_block {
+    sdrgpu::Block* impl;
+};

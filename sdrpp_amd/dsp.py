@@ -1,0 +1,271 @@
+"""Python-side handles over the libsdrgpu C ABI, named after the reference blocks.
+
+Each class mirrors one ``dsp::`` block of the reference (file:line in the C
+header ``include/sdrgpu.h``): ``process(x)`` is the reference's
+``process(count, in, out) -> outCount`` on host numpy buffers (synchronous,
+staged through pinned memory), ``process_dev(in_ptr, count, out_ptr, stream)``
+runs on device-resident buffers (torch tensors' ``data_ptr()``) on a caller
+stream and returns the output count without synchronising.
+"""
+import ctypes
+
+import numpy as np
+
+from . import lib, check, F32, C64
+
+_vp = ctypes.c_void_p
+
+
+def _fptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _taps_arg(taps):
+    t = np.ascontiguousarray(taps)
+    if np.iscomplexobj(t):
+        t = t.astype(np.complex64)
+        return t, C64
+    return t.astype(np.float32), F32
+
+
+class Block:
+    """Owns one sdrgpu_block handle."""
+
+    def __init__(self, handle, in_dtype, out_dtype):
+        self._h = handle
+        self.in_dtype = in_dtype      # numpy dtype of one input element
+        self.out_dtype = out_dtype
+
+    def out_count(self, count):
+        return check(lib.sdrgpu_block_out_count(self._h, int(count)))
+
+    def process(self, x):
+        x = np.ascontiguousarray(x, dtype=self.in_dtype)
+        n = x.shape[0]
+        out = np.empty(max(self.out_count(n), 1), dtype=self.out_dtype)
+        m = check(lib.sdrgpu_block_process(self._h, _fptr(x), n, _fptr(out)))
+        return out[:m]
+
+    def process_dev(self, in_ptr, count, out_ptr, stream=None):
+        return check(lib.sdrgpu_block_process_dev(self._h, _vp(in_ptr), int(count), _vp(out_ptr), _vp(stream or 0)))
+
+    def reset(self):
+        check(lib.sdrgpu_block_reset(self._h))
+
+    def close(self):
+        if self._h:
+            lib.sdrgpu_block_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _make(fn, *args):
+    h = ctypes.c_void_p()
+    check(fn(ctypes.byref(h), *args))
+    return h
+
+
+STEREO = np.dtype([("l", np.float32), ("r", np.float32)])
+
+
+class FrequencyXlator(Block):
+    """dsp::channel::FrequencyXlator (channel/frequency_xlator.h:15-50); offset in rad/sample."""
+
+    def __init__(self, offset_rad, device=0):
+        super().__init__(_make(lib.sdrgpu_xlator_create, device, float(offset_rad)), np.complex64, np.complex64)
+
+    def set_offset(self, offset_rad):
+        check(lib.sdrgpu_xlator_set_offset(self._h, float(offset_rad)))
+
+
+class FIR(Block):
+    """dsp::filter::FIR<D,T> (filter/fir.h) / DecimatingFIR<D,T> (filter/decimating_fir.h)."""
+
+    def __init__(self, taps, decim=1, complex_data=True, device=0):
+        t, ttype = _taps_arg(taps)
+        dtype = C64 if complex_data else F32
+        self._taps = t
+        h = _make(lib.sdrgpu_fir_create, device, dtype, ttype, _fptr(t), int(t.shape[0]), int(decim))
+        npd = np.complex64 if complex_data else np.float32
+        super().__init__(h, npd, npd)
+
+    def set_taps(self, taps):
+        t, _ = _taps_arg(taps)
+        self._taps = t
+        check(lib.sdrgpu_fir_set_taps(self._h, _fptr(t), int(t.shape[0])))
+
+    def set_decimation(self, decim):
+        check(lib.sdrgpu_fir_set_decimation(self._h, int(decim)))
+
+
+def DecimatingFIR(taps, decim, complex_data=True, device=0):
+    return FIR(taps, decim, complex_data, device)
+
+
+class Quadrature(Block):
+    """dsp::demod::Quadrature (demod/quadrature.h:41-56); deviation in rad/sample."""
+
+    def __init__(self, deviation_rad, device=0):
+        super().__init__(_make(lib.sdrgpu_quadrature_create, device, float(deviation_rad)), np.complex64, np.float32)
+
+
+class PowerDecimator(Block):
+    """dsp::multirate::PowerDecimator<T> (multirate/power_decimator.h)."""
+
+    def __init__(self, ratio, complex_data=True, device=0):
+        npd = np.complex64 if complex_data else np.float32
+        super().__init__(_make(lib.sdrgpu_power_decimator_create, device, C64 if complex_data else F32, int(ratio)), npd, npd)
+
+
+class PolyphaseResampler(Block):
+    """dsp::multirate::PolyphaseResampler<T> (multirate/polyphase_resampler.h)."""
+
+    def __init__(self, interp, decim, taps, complex_data=True, device=0):
+        t = np.ascontiguousarray(taps, dtype=np.float32)
+        npd = np.complex64 if complex_data else np.float32
+        h = _make(lib.sdrgpu_polyphase_resampler_create, device, C64 if complex_data else F32, int(interp), int(decim),
+                  _fptr(t), int(t.shape[0]))
+        super().__init__(h, npd, npd)
+
+
+class RationalResampler(Block):
+    """dsp::multirate::RationalResampler<T> (multirate/rational_resampler.h)."""
+
+    def __init__(self, in_sr, out_sr, complex_data=True, device=0):
+        npd = np.complex64 if complex_data else np.float32
+        h = _make(lib.sdrgpu_rational_resampler_create, device, C64 if complex_data else F32, float(in_sr), float(out_sr))
+        super().__init__(h, npd, npd)
+
+
+class RxVFO(Block):
+    """dsp::channel::RxVFO (channel/rx_vfo.h)."""
+
+    def __init__(self, in_sr, out_sr, bandwidth, offset, device=0):
+        h = _make(lib.sdrgpu_rxvfo_create, device, float(in_sr), float(out_sr), float(bandwidth), float(offset))
+        super().__init__(h, np.complex64, np.complex64)
+
+    def set_offset(self, offset):
+        check(lib.sdrgpu_rxvfo_set_offset(self._h, float(offset)))
+
+
+class DDCFM(Block):
+    """Fused FrequencyXlator -> DecimatingFIR<complex_t,float> -> Quadrature (BASELINE config C3)."""
+
+    def __init__(self, offset_rad, taps, decim, deviation_rad, device=0):
+        t = np.ascontiguousarray(taps, dtype=np.float32)
+        self._taps = t
+        h = _make(lib.sdrgpu_ddc_fm_create, device, float(offset_rad), _fptr(t), int(t.shape[0]), int(decim),
+                  float(deviation_rad))
+        super().__init__(h, np.complex64, np.float32)
+
+
+class FM(Block):
+    """dsp::demod::FM<float> (demod/fm.h)."""
+
+    def __init__(self, samplerate, bandwidth, low_pass=True, high_pass=False, device=0):
+        h = _make(lib.sdrgpu_fm_create, device, float(samplerate), float(bandwidth), int(low_pass), int(high_pass))
+        super().__init__(h, np.complex64, np.float32)
+
+
+class BroadcastFM(Block):
+    """dsp::demod::BroadcastFM, mono path (demod/broadcast_fm.h:144-215); stereo_t out."""
+
+    def __init__(self, deviation, samplerate, low_pass=True, device=0):
+        h = _make(lib.sdrgpu_wfm_create, device, float(deviation), float(samplerate), int(low_pass))
+        super().__init__(h, np.complex64, STEREO)
+
+
+class FFTSpectrum:
+    """IQFrontEnd's FFT path (signal_path/iq_frontend.cpp:230-249, 272-296)."""
+
+    def __init__(self, fft_size, nz=None, window=6, device=0):
+        self.N = int(fft_size)
+        self.nz = int(nz if nz is not None else fft_size)
+        self._h = _make(lib.sdrgpu_fft_create, device, self.N, self.nz, int(window))
+
+    def set_window(self, w):
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        check(lib.sdrgpu_fft_set_window(self._h, _fptr(w), int(w.shape[0])))
+        self.nz = int(w.shape[0])
+
+    def logmag(self, x):
+        """Host drop-in: x = complex64[nz] -> float32[N] dB."""
+        x = np.ascontiguousarray(x, dtype=np.complex64)
+        assert x.shape[0] >= self.nz
+        out = np.empty(self.N, dtype=np.float32)
+        check(lib.sdrgpu_fft_logmag(self._h, _fptr(x), _fptr(out)))
+        return out
+
+    def execute_dev(self, in_ptr, frame_stride, frames, out_ptr, stream=None):
+        return check(lib.sdrgpu_fft_execute_dev(self._h, _vp(in_ptr), int(frame_stride), int(frames), _vp(out_ptr),
+                                                _vp(stream or 0)))
+
+    def close(self):
+        if self._h:
+            lib.sdrgpu_fft_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def convert(kind, x, device=0):
+    """file_source / rtl_sdr / hackrf ingest converters on the GPU (host buffers)."""
+    x = np.ascontiguousarray(x)
+    n = x.size if kind != 2 else x.size // 3
+    out = np.empty(n, dtype=np.float32)
+    check(lib.sdrgpu_convert(device, int(kind), _fptr(x), n, _fptr(out)))
+    return out
+
+
+# ---- host-side design functions (no GPU) ----------------------------------
+def create_window(wtype, size, centered=True):
+    w = np.empty(size, dtype=np.float32)
+    check(lib.sdrgpu_create_window(int(wtype), _fptr(w), int(size), int(centered)))
+    return w
+
+
+def _taps(fn, *args):
+    n = check(fn(*args, None))
+    t = np.empty(n, dtype=np.float32)
+    fn(*args, _fptr(t))
+    return t
+
+
+def low_pass(cutoff, trans, fs, odd=False):
+    return _taps(lib.sdrgpu_taps_low_pass, float(cutoff), float(trans), float(fs), int(odd))
+
+
+def high_pass(cutoff, trans, fs, odd=False):
+    return _taps(lib.sdrgpu_taps_high_pass, float(cutoff), float(trans), float(fs), int(odd))
+
+
+def band_pass(start, stop, trans, fs, odd=False, complex_taps=False):
+    if complex_taps:
+        n = check(lib.sdrgpu_taps_band_pass_c(float(start), float(stop), float(trans), float(fs), int(odd), None))
+        t = np.empty(n, dtype=np.complex64)
+        lib.sdrgpu_taps_band_pass_c(float(start), float(stop), float(trans), float(fs), int(odd), _fptr(t))
+        return t
+    return _taps(lib.sdrgpu_taps_band_pass_f, float(start), float(stop), float(trans), float(fs), int(odd))
+
+
+def gen_reshape_params(fs, size, rate):
+    skip, nz = ctypes.c_int(), ctypes.c_int()
+    lib.sdrgpu_gen_reshape_params(float(fs), int(size), float(rate), ctypes.byref(skip), ctypes.byref(nz))
+    return skip.value, nz.value
+
+
+def decim_plan(ratio):
+    d = (ctypes.c_int * 8)()
+    n = (ctypes.c_int * 8)()
+    t = (ctypes.POINTER(ctypes.c_float) * 8)()
+    ns = check(lib.sdrgpu_decim_plan(int(ratio), d, n, t))
+    return [(d[i], np.ctypeslib.as_array(t[i], shape=(n[i],)).copy()) for i in range(ns)]

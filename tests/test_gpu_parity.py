@@ -1,0 +1,284 @@
+"""GPU parity: libsdrgpu (HIP, gfx950) vs the CPU restatement (oracle/) on the same
+seeded inputs. Every call goes through the C ABI (ctypes). Tolerances: tests/_util.py."""
+import numpy as np
+import pytest
+
+import oracle
+import sdrpp_amd
+from sdrpp_amd import dsp
+from _util import GOLDEN, assert_close_c, db_check, fir_atol, iq, ref32_fft_db
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    n = sdrpp_amd.lib.sdrgpu_device_count()
+    assert n > 0, "no HIP device visible: gpu tests need an MI355X"
+
+
+# ------------------------------------------------------------------ spectrum
+@pytest.mark.parametrize("N", [64, 256, 1024, 4096, 8192, 65536, 262144])
+def test_fft_logmag_random(N, rng):
+    x = iq(rng, N)
+    w = oracle.create_window(6, N)
+    f = dsp.FFTSpectrum(N, N, 6)
+    db = f.logmag(x)
+    truth = oracle.fft_truth_power(x, N, N, w)
+    db_check(db, truth, N, ref32_fft_db(x, N, N, w))
+
+
+def test_fft_logmag_1M_zero_pad(rng):
+    # C2: fs 10 MS/s, fftRate 10 -> nz = 1,000,000, zero-padded to 2^20
+    skip, nz = dsp.gen_reshape_params(10e6, 1 << 20, 10.0)
+    assert (skip, nz) == (0, 1000000)
+    N = 1 << 20
+    x = iq(rng, nz)
+    w = oracle.create_window(6, nz)
+    f = dsp.FFTSpectrum(N, nz, 6)
+    db = f.logmag(x)
+    truth = oracle.fft_truth_power(x, nz, N, w)
+    db_check(db, truth, N, ref32_fft_db(x, nz, N, w))
+
+
+@pytest.mark.parametrize("N,k0,A", [(65536, 1000, 0.5), (4096, -77, 1.0), (1 << 20, 12345, 0.25)])
+def test_fft_tone_unity_gain_centred(N, k0, A):
+    # a bin-centred tone of amplitude A reads 20 log10 A at bin N/2 + k0 (unity coherent gain, centred)
+    n = np.arange(N)
+    x = (A * np.exp(2j * np.pi * k0 * n / N)).astype(np.complex64)
+    f = dsp.FFTSpectrum(N, N, 6)
+    db = f.logmag(x)
+    k = N // 2 + k0
+    assert int(np.argmax(db)) == k
+    assert abs(db[k] - 20 * np.log10(A)) < 0.01
+
+
+@pytest.mark.parametrize("wtype", range(7))
+def test_fft_all_windows(wtype, rng):
+    N = 16384
+    x = iq(rng, N)
+    w = oracle.create_window(wtype, N)
+    f = dsp.FFTSpectrum(N, N, wtype)
+    db = f.logmag(x)
+    db_check(db, oracle.fft_truth_power(x, N, N, w), N, ref32_fft_db(x, N, N, w))
+
+
+def test_fft_batch_dev_matches_host(rng):
+    import torch
+    N, frames, stride = 65536, 5, 70000       # skip = stride - N (reshaper keep/skip framing)
+    x = iq(rng, stride * frames)
+    f = dsp.FFTSpectrum(N, N, 6)
+    xd = torch.from_numpy(x.view(np.float32)).cuda()
+    out = torch.empty(frames * N, dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    f.execute_dev(xd.data_ptr(), stride, frames, out.data_ptr(), s)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().reshape(frames, N)
+    for i in range(frames):
+        np.testing.assert_array_equal(o[i], f.logmag(x[i * stride:i * stride + N]))
+
+
+def test_fft_aes17_fixture():
+    # test_source AES17 14-bit table (source_modules/test_source/src/main.cpp:41-48), 16 samples/period
+    g = np.load(GOLDEN + "/fft_aes17.npz")
+    f = dsp.FFTSpectrum(int(g["N"]), int(g["N"]), 6)
+    db = f.logmag(g["x"])
+    truth = g["power_f64"]
+    db_check(db, truth, int(g["N"]), g["db_ref32"])
+
+
+# ----------------------------------------------------------------------- FIR
+@pytest.mark.parametrize("ntaps,decim,cplx", [(1, 1, True), (91, 1, True), (228, 1, False), (256, 8, True),
+                                                (143, 32, True), (27, 4, True), (69, 2, False), (726, 128, True),
+                                                (5, 3, True)])
+def test_fir_vs_oracle(ntaps, decim, cplx, rng):
+    taps = rng.standard_normal(ntaps).astype(np.float32) / ntaps
+    g = dsp.FIR(taps, decim, cplx)
+    o = oracle.FIR(taps, decim, cplx)
+    for n in [1000, 7, 50000, 0, 123457]:
+        x = iq(rng, n) if cplx else rng.uniform(-1, 1, n).astype(np.float32)
+        yo = o.process(x)
+        yg = g.process(x)
+        assert len(yg) == len(yo), (n, len(yg), len(yo))
+        assert_close_c(yg, yo, fir_atol(taps, x) if n else 0, f"fir {ntaps}/{decim}")
+
+
+def test_fir_complex_taps(rng):
+    taps = dsp.band_pass(18750.0, 19250.0, 3000.0, 240000.0, True, True)   # WFM stereo pilot BPF, 305 taps
+    assert len(taps) == 305
+    g = dsp.FIR(taps, 1, True)
+    o = oracle.FIR(taps, 1, True)
+    for n in [4000, 1, 30001]:
+        x = iq(rng, n)
+        assert_close_c(g.process(x), o.process(x), fir_atol(taps, x), "complex-tap FIR")
+
+
+def test_fir_block_split_invariance(rng):
+    # splitting the stream into arbitrary counts yields the identical output stream (bit-exact)
+    taps = dsp.low_pass(3.0e6, 912000.0, 61.44e6)
+    x = iq(rng, 200000)
+    a = dsp.FIR(taps, 8).process(x)
+    g = dsp.FIR(taps, 8)
+    cuts = np.sort(rng.choice(np.arange(1, len(x)), 40, replace=False))
+    parts = [g.process(p) for p in np.split(x, cuts)]
+    np.testing.assert_array_equal(np.concatenate(parts).view(np.uint32), a.view(np.uint32))
+
+
+def test_fir_impulse_is_taps_correlation_order(rng):
+    taps = rng.standard_normal(33).astype(np.float32)
+    x = np.zeros(100, dtype=np.complex64)
+    x[0] = 1
+    y = dsp.FIR(taps, 1).process(x)
+    # correlation (no tap reversal): y[i] = sum_j buf[i+j] h[j], buf = [32 zeros | x] -> y[i] = h[32 - i]
+    np.testing.assert_array_equal(y[:33].real, taps[::-1])
+
+
+def test_fir_set_taps_keeps_history(rng):
+    t1 = rng.standard_normal(40).astype(np.float32)
+    t2 = rng.standard_normal(17).astype(np.float32)
+    g, o = dsp.FIR(t1, 3), oracle.FIR(t1, 3)
+    x = iq(rng, 1000)
+    assert_close_c(g.process(x), o.process(x), fir_atol(t1, x))
+    g.set_taps(t2); o.set_taps(t2)
+    x = iq(rng, 999)
+    assert_close_c(g.process(x), o.process(x), fir_atol(t2, x))
+    g.set_taps(t1); o.set_taps(t1)
+    x = iq(rng, 555)
+    assert_close_c(g.process(x), o.process(x), fir_atol(t1, x))
+
+
+# ---------------------------------------------------------------- xlator/quad
+def test_xlator_vs_fp64_nco(rng):
+    w = 2 * np.pi * (-1.5e6 / 61.44e6)
+    g, o = dsp.FrequencyXlator(w), oracle.Xlator(w)
+    for n in [100000, 3, 777777]:
+        x = iq(rng, n)
+        assert_close_c(g.process(x), o.process(x), 2e-6, "xlator")
+
+
+def test_xlator_long_run_phase_drift():
+    # phase drift vs the fp64 NCO after 1e7 samples <= 1e-5 rad
+    w = 2 * np.pi * (2.5e6 / 61.44e6)
+    g = dsp.FrequencyXlator(w)
+    x = np.ones(1_000_000, dtype=np.complex64)
+    for _ in range(10):
+        y = g.process(x)
+    weff = oracle.lib.orc_xlator_effective_omega(w)
+    n = 10_000_000 - 1
+    ph_true = np.angle(np.exp(1j * np.fmod(weff * n, 2 * np.pi)))
+    assert abs(np.angle(y[-1] * np.exp(-1j * ph_true))) < 1e-5
+
+
+def test_quadrature_vs_oracle(rng):
+    dev = 2 * np.pi * 100e3 / 7.68e6
+    g, o = dsp.Quadrature(dev), oracle.Quadrature(dev)
+    for n in [5000, 1, 77777]:
+        x = iq(rng, n)
+        assert_close_c(g.process(x), o.process(x), 1e-5 * (1 / dev), "quadrature")
+
+
+# ------------------------------------------------------------ multirate
+@pytest.mark.parametrize("ratio", [1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 8192])
+def test_power_decimator(ratio, rng):
+    g, o = dsp.PowerDecimator(ratio), oracle.PowerDecimator(ratio)
+    for n in [ratio * 50 + 3, 100000, 17]:
+        x = iq(rng, n)
+        yo, yg = o.process(x), g.process(x)
+        assert len(yg) == len(yo)
+        assert_close_c(yg, yo, 2e-5, f"power decim {ratio}")
+
+
+@pytest.mark.parametrize("interp,decim", [(4, 5), (3, 2), (1, 7), (5, 4)])
+def test_polyphase(interp, decim, rng):
+    taps = dsp.low_pass(0.4 / max(interp, decim), 0.05 / max(interp, decim), 1.0) * interp
+    g, o = dsp.PolyphaseResampler(interp, decim, taps), oracle.PolyphaseResampler(interp, decim, taps)
+    for n in [1000, 13, 40000]:
+        x = iq(rng, n)
+        yo, yg = o.process(x), g.process(x)
+        assert len(yg) == len(yo)
+        assert_close_c(yg, yo, fir_atol(taps, x), "polyphase")
+
+
+@pytest.mark.parametrize("ins,outs,cplx", [(240000, 48000, False), (61.44e6, 240000, True), (2.4e6, 48000, True),
+                                           (48000, 44100, False), (8e6, 200000, True)])
+def test_rational_resampler(ins, outs, cplx, rng):
+    g, o = dsp.RationalResampler(ins, outs, cplx), oracle.RationalResampler(ins, outs, cplx)
+    for n in [int(ins / 200), 5000, 123]:
+        x = iq(rng, n) if cplx else rng.uniform(-1, 1, n).astype(np.float32)
+        yo, yg = o.process(x), g.process(x)
+        assert len(yg) == len(yo)
+        assert_close_c(yg, yo, 5e-5, "rational")
+
+
+# ------------------------------------------------------------ VFO / demods
+def test_rxvfo_c5(rng):
+    g = dsp.RxVFO(61.44e6, 240000, 200000, 2.5e6)
+    o = oracle.RxVFO(61.44e6, 240000, 200000, 2.5e6)
+    for n in [307200, 307200, 1000, 999999]:
+        x = iq(rng, n)
+        yo, yg = o.process(x), g.process(x)
+        assert len(yg) == len(yo)
+        assert_close_c(yg, yo, 5e-5, "rxvfo")
+
+
+def test_ddc_fm_c3(rng):
+    fs = 61.44e6
+    taps = dsp.low_pass(3.0e6, 912000.0, fs)
+    w = 2 * np.pi * (-1.5e6 / fs)
+    dev = 2 * np.pi * 100e3 / (fs / 8)
+    g = dsp.DDCFM(w, taps, 8, dev)
+    ox, of, oq = oracle.Xlator(w), oracle.FIR(taps, 8), oracle.Quadrature(dev)
+    for n in [307200, 12345, 8, 500000]:
+        x = iq(rng, n)
+        yo = oq.process(of.process(ox.process(x)))
+        yg = g.process(x)
+        assert len(yg) == len(yo)
+        # atan2 of an fp32 FIR output: the phase error scales with 1/|y|; bound it on samples
+        # whose |y| is not tiny and check the global fraction
+        assert np.mean(np.abs(yg - yo) < 1e-3) > 0.999
+
+
+def test_fm_tone_demod_amplitude():
+    # 1 kHz tone FM-modulated at 75 kHz deviation, demodulated with dev 100 kHz -> amplitude 0.75
+    fs = 240000.0
+    t = np.arange(240000) / fs
+    phase = 2 * np.pi * 75e3 * np.cumsum(np.sin(2 * np.pi * 1e3 * t)) / fs
+    x = np.exp(1j * phase).astype(np.complex64)
+    y = dsp.Quadrature(2 * np.pi * 100e3 / fs).process(x)
+    assert abs(np.max(y[1000:]) - 0.75) < 2e-3
+
+
+def test_wfm_mono_vs_oracle(rng):
+    g = dsp.BroadcastFM(100000, 240000)
+    o = oracle.BroadcastFM(100000, 240000)
+    for n in [1200, 4800, 1]:
+        x = iq(rng, n)
+        yo, yg = o.process(x), g.process(x)
+        assert len(yg) == len(yo)
+        assert np.abs(yg["l"] - yo["l"]).max() < 1e-3
+        np.testing.assert_array_equal(yg["l"], yg["r"])
+
+
+def test_fm_nfm_vs_oracle(rng):
+    for lp, hp in [(True, False), (False, True), (True, True), (False, False)]:
+        g = dsp.FM(48000, 12500, lp, hp)
+        o = oracle.FM(48000, 12500, lp, hp)
+        x = iq(rng, 9600)
+        assert np.abs(g.process(x) - o.process(x)).max() < 1e-3
+
+
+# -------------------------------------------------------------- converters
+def test_converters_bit_exact():
+    u8 = np.arange(256, dtype=np.uint8)
+    i16 = np.arange(-32768, 32768, dtype=np.int16)
+    i8 = np.arange(-128, 128, dtype=np.int8)
+    rng = np.random.default_rng(7)
+    i32 = np.concatenate([rng.integers(-2**31, 2**31, 200000, dtype=np.int64).astype(np.int32),
+                          np.array([-2**31, 2**31 - 1, 0, -1], dtype=np.int32)])
+    f64 = rng.standard_normal(100000)
+    i24v = np.arange(-(1 << 23), 1 << 23, 37, dtype=np.int32)
+    i24 = np.stack([(i24v & 0xff), (i24v >> 8) & 0xff, (i24v >> 16) & 0xff], axis=1).astype(np.uint8).ravel()
+    for kind, x in [(0, u8), (1, i16), (2, i24), (3, i32), (4, f64), (5, i8)]:
+        a = dsp.convert(kind, x)
+        b = oracle.convert(kind, x)
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32), err_msg=f"kind {kind}")
