@@ -151,6 +151,9 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
+    # one explicit non-default stream for every kernel of the step (libsdrgpu treats a NULL
+    # stream as "the handle's own stream", which would split the chain over several queues)
+    torch.cuda.set_stream(torch.cuda.Stream())
     B = 1 << a.log2_batch
     if a.config == "c2":
         B = 256 * 1000000

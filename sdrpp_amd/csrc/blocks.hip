@@ -17,16 +17,26 @@ __device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
     return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
-// NCO phasor for stream sample `idx` of a call whose first sample has phase theta0:
-// angle = theta0 + w*idx in double, reduced to [-pi, pi], then an accurate float sincos.
-__device__ __forceinline__ float2 nco(double theta0, double w, long long idx) {
+// Two-level NCO table: phasor(i) = Phi[i >> 12] * Plo[i & 4095], with
+// Plo[k] = exp(i w k) (fixed per configuration, fp64 -> float on the host) and
+// Phi[j] = exp(i (theta0 + w 4096 j)) (per call, fp64 on the device). Two cached
+// loads + one complex multiply per sample instead of an fp64 argument reduction
+// and a sincos; error <= ~2 ulp of the phasor, no drift (theta0 is carried in
+// double-double on the host).
+constexpr int NCO_LO_BITS = 12;
+constexpr int NCO_LO = 1 << NCO_LO_BITS;
+__device__ __forceinline__ float2 nco_tab(const float2* __restrict__ phi, const float2* __restrict__ plo, long long i) {
+    return cmulf(phi[i >> NCO_LO_BITS], plo[i & (NCO_LO - 1)]);
+}
+__global__ void nco_hi_kernel(float2* __restrict__ phi, int n, double theta0, double w) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
     const double TWO_PI = 6.283185307179586476925286766559;
-    const double INV_TWO_PI = 0.15915494309189533576888376337251;
-    double a = fma(w, (double)idx, theta0);
-    a = fma(-rint(a * INV_TWO_PI), TWO_PI, a);
-    float s, c;
-    sincosf((float)a, &s, &c);
-    return make_float2(c, s);
+    double a = fma(w * (double)NCO_LO, (double)j, theta0);
+    a = fma(-rint(a / TWO_PI), TWO_PI, a);
+    double sn, cs;
+    sincos(a, &sn, &cs);
+    phi[j] = make_float2((float)cs, (float)sn);
 }
 
 template <typename T> __device__ __forceinline__ T zero_of();
@@ -52,12 +62,14 @@ __device__ __forceinline__ void mac(float2& acc, float2 x, float2 h) {
 struct FirArgs {
     const void* hist;
     const void* in;
-    const void* taps;   // ntaps elements of TT
+    const void* taps;   // [D][Q] (phase-major, zero-padded) elements of TT
     void* out;
     const float2* din;  // QUAD: y[-1] (carried)
     float2* dinNext;    // QUAD: y[M-1]
-    double theta0, w;   // XL: phase of in[0], increment
+    const float2* phi;  // XL: per-call coarse phasors
+    const float2* plo;  // XL: fine phasors
     int ntaps, H, count, D, Q, offset0, M, TMS, RSK, RSP;
+    int dshift;         // log2(D) when D is a power of two, else -1
     float invDev;
 };
 
@@ -68,7 +80,6 @@ __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
     constexpr int QOFF = QUAD ? 1 : 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     DT* X = reinterpret_cast<DT*>(smem);
-    TT* Hs = reinterpret_cast<TT*>(smem + sizeof(DT) * (size_t)a.D * a.RSP);
 
     const int tid = threadIdx.x;
     const int tile = blockIdx.x;
@@ -78,29 +89,55 @@ __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
     const int span = rows * a.D;
     const DT* hist = reinterpret_cast<const DT*>(a.hist);
     const DT* in = reinterpret_cast<const DT*>(a.in);
-    const TT* taps = reinterpret_cast<const TT*>(a.taps);
+    const TT* __restrict__ taps = reinterpret_cast<const TT*>(a.taps);   // wave-uniform reads -> scalar loads
 
-    // taps -> LDS as [p][q] = taps[q*D + p] (zero past ntaps)
-    for (int e = tid; e < a.D * a.Q; e += NT) {
-        const int p = e / a.Q, q = e % a.Q;
-        const int j = q * a.D + p;
-        Hs[e] = j < a.ntaps ? taps[j] : zero_of<TT>();
-    }
-    // input span -> LDS (phase-major, row-swizzled)
-    for (int s = tid; s < span; s += NT) {
-        const long long b = b0 + s;
-        DT v = zero_of<DT>();
-        if (b >= 0) {
-            if (b < a.H) {
-                v = hist[b];
-            } else if (b - a.H < a.count) {
-                const long long i = b - a.H;
-                v = in[i];
-                if constexpr (XL) v = cmulf(v, nco(a.theta0, a.w, i));
+    // input span -> LDS (phase-major, row-swizzled). Loads are issued UNR at a time into
+    // registers before any LDS store so HBM latency overlaps; interior tiles (span fully
+    // inside `in`) take a branch-free path.
+    const bool interior = (b0 >= a.H) && (b0 + span <= (long long)a.H + a.count);
+    constexpr int UNR = 8;
+    for (int s0 = tid; s0 < span; s0 += UNR * NT) {
+        DT v[UNR];
+        if (interior) {
+#pragma unroll
+            for (int u = 0; u < UNR; u++) {
+                const int sc = min(s0 + u * NT, span - 1);        // clamp keeps the load in bounds
+                const long long i = b0 + sc - a.H;
+                v[u] = in[i];
+                if constexpr (XL) v[u] = cmulf(v[u], nco_tab(a.phi, a.plo, i));
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < UNR; u++) {
+                const long long b = b0 + s0 + u * NT;
+                DT x = zero_of<DT>();
+                if (s0 + u * NT < span && b >= 0) {
+                    if (b < a.H) {
+                        x = hist[b];
+                    } else if (b - a.H < a.count) {
+                        const long long i = b - a.H;
+                        x = in[i];
+                        if constexpr (XL) x = cmulf(x, nco_tab(a.phi, a.plo, i));
+                    }
+                }
+                v[u] = x;
             }
         }
-        const int p = s % a.D, r = s / a.D;
-        X[p * a.RSP + (r % K) * a.RSK + r / K] = v;
+#pragma unroll
+        for (int u = 0; u < UNR; u++) {
+            const int sx = s0 + u * NT;
+            if (sx < span) {
+                int p, r;
+                if (a.dshift >= 0) {
+                    p = sx & (a.D - 1);
+                    r = sx >> a.dshift;
+                } else {
+                    r = sx / a.D;
+                    p = sx - r * a.D;
+                }
+                X[p * a.RSP + (r % K) * a.RSK + r / K] = v[u];
+            }
+        }
     }
     __syncthreads();
 
@@ -110,7 +147,7 @@ __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
     const int l = tid;
     for (int p = 0; p < a.D; p++) {
         const DT* Xp = X + p * a.RSP;
-        const TT* Hp = Hs + p * a.Q;
+        const TT* __restrict__ Hp = taps + p * a.Q;
         DT w[K];
 #pragma unroll
         for (int i = 0; i < K; i++) w[i] = Xp[i * a.RSK + l];   // rows l*K + i
@@ -169,7 +206,7 @@ __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
 // history for the next call: the last H elements of hist | xl(in)
 template <typename DT, bool XL>
 __global__ void fir_hist_kernel(const DT* __restrict__ hist, const DT* __restrict__ in, DT* __restrict__ next, int H,
-                                int count, double theta0, double w) {
+                                int count, const float2* __restrict__ phi, const float2* __restrict__ plo) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= H) return;
     const long long b = (long long)count + k;
@@ -179,17 +216,44 @@ __global__ void fir_hist_kernel(const DT* __restrict__ hist, const DT* __restric
     } else {
         const long long i = b - H;
         v = in[i];
-        if constexpr (XL) v = cmulf(v, nco(theta0, w, i));
+        if constexpr (XL) v = cmulf(v, nco_tab(phi, plo, i));
     }
     next[k] = v;
 }
 
 // --------------------------------------------------------------- xlator
-__global__ void xlator_kernel(const float2* __restrict__ in, float2* __restrict__ out, long long n, double theta0,
-                              double w) {
+__global__ void xlator_kernel(const float2* __restrict__ in, float2* __restrict__ out, long long n,
+                              const float2* __restrict__ phi, const float2* __restrict__ plo) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = cmulf(in[i], nco(theta0, w, i));
+    if (i < n) out[i] = cmulf(in[i], nco_tab(phi, plo, i));
 }
+
+// host side of the NCO tables
+struct Nco {
+    double w = 0.0;
+    PhaseAcc phase;     // phase of the next input sample
+    DevBuf plo, phi;
+    int set_w(double w_) {
+        w = w_;
+        std::vector<float2> t(NCO_LO);
+        for (int k = 0; k < NCO_LO; k++) {
+            const double a = std::fmod(w * (double)k, 2.0 * M_PI);
+            t[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+        }
+        SDRGPU_CHECK(plo.ensure(sizeof(float2) * NCO_LO));
+        SDRGPU_HIP(hipMemcpy(plo.p, t.data(), sizeof(float2) * NCO_LO, hipMemcpyHostToDevice));
+        return SDRGPU_OK;
+    }
+    // coarse table for a call of `count` samples starting at the current phase
+    int prepare(int count, hipStream_t s) {
+        const int nhi = (count >> NCO_LO_BITS) + 2;
+        SDRGPU_CHECK(phi.ensure(sizeof(float2) * nhi));
+        hipLaunchKernelGGL(nco_hi_kernel, dim3((nhi + 255) / 256), dim3(256), 0, s, phi.as<float2>(), nhi,
+                           phase.value(), w);
+        SDRGPU_HIP(hipGetLastError());
+        return SDRGPU_OK;
+    }
+};
 
 // ----------------------------------------------------------- quadrature
 __global__ void quad_kernel(const float2* __restrict__ in, float* __restrict__ out, int n, const float2* __restrict__ din,
@@ -296,8 +360,7 @@ int Block::init_stream() {
 struct FirBlock : Block {
     int ttype = SDRGPU_F32, ntaps = 0, D = 1, offset = 0, Q = 1;
     bool xl = false, quad = false, stereo = false;
-    double w = 0.0;         // XL increment
-    PhaseAcc phase;         // XL: phase of the next input sample
+    Nco nco;                // XL: fused frequency xlator
     float invDev = 1.0f;    // QUAD
     DevBuf taps, hist[2], din[2];
     int cur = 0;            // ping-pong index
@@ -326,11 +389,10 @@ struct FirBlock : Block {
         if (keep > 0) std::memcpy(newHist.data() + (size_t)(newH - keep) * es, oldHist.data() + (size_t)(oldH - keep) * es, keep * es);
         for (int k = 0; k < 2; k++) SDRGPU_CHECK(hist[k].ensure(newHist.size()));
         SDRGPU_HIP(hipMemcpy(hist[cur].p, newHist.data(), newHist.size(), hipMemcpyHostToDevice));
-        SDRGPU_CHECK(taps.ensure(sizeof(float) * n * (ttype == SDRGPU_C64 ? 2 : 1)));
-        SDRGPU_HIP(hipMemcpy(taps.p, t, sizeof(float) * n * (ttype == SDRGPU_C64 ? 2 : 1), hipMemcpyHostToDevice));
+        host_taps.assign(t, t + (size_t)n * (ttype == SDRGPU_C64 ? 2 : 1));
         ntaps = n;
-        Q = (n + D - 1) / D;
         offset = 0;
+        SDRGPU_CHECK(upload_taps());
         if (quad) {
             for (int k = 0; k < 2; k++) SDRGPU_CHECK(din[k].ensure(sizeof(float2)));
         }
@@ -339,8 +401,24 @@ struct FirBlock : Block {
     int set_decimation(int d) {
         if (d < 1) { set_error("fir: decimation %d < 1", d); return SDRGPU_EARG; }
         D = d;
-        Q = (ntaps + D - 1) / D;
         offset = 0;
+        return upload_taps();
+    }
+    // device taps in [p][q] = h[q*D + p] order, zero past ntaps (phase-major like the LDS span)
+    std::vector<float> host_taps;
+    int upload_taps() {
+        SDRGPU_HIP(hipSetDevice(device));
+        Q = (ntaps + D - 1) / D;
+        const int e = ttype == SDRGPU_C64 ? 2 : 1;
+        std::vector<float> pq((size_t)D * Q * e, 0.0f);
+        for (int p = 0; p < D; p++)
+            for (int q = 0; q < Q; q++) {
+                const int j = q * D + p;
+                if (j < ntaps)
+                    for (int k = 0; k < e; k++) pq[((size_t)p * Q + q) * e + k] = host_taps[(size_t)j * e + k];
+            }
+        SDRGPU_CHECK(taps.ensure(sizeof(float) * pq.size()));
+        SDRGPU_HIP(hipMemcpy(taps.p, pq.data(), sizeof(float) * pq.size(), hipMemcpyHostToDevice));
         return SDRGPU_OK;
     }
     int out_count(int count) override { return count > offset ? (count - offset + D - 1) / D : 0; }
@@ -349,7 +427,7 @@ struct FirBlock : Block {
         SDRGPU_HIP(hipMemset(hist[cur].p, 0, (size_t)std::max(ntaps - 1, 1) * esize(in_dtype)));
         if (quad) SDRGPU_HIP(hipMemset(din[cur].p, 0, sizeof(float2)));
         offset = 0;
-        phase.reset();
+        nco.phase.reset();
         return SDRGPU_OK;
     }
     int choose_k() const {
@@ -378,12 +456,12 @@ struct FirBlock : Block {
         SDRGPU_HIP(hipSetDevice(device));
         const int M = out_count(count);
         const int H = ntaps - 1;
-        const double theta0 = phase.value();
+        if (xl && count > 0) SDRGPU_CHECK(nco.prepare(count, s));
         if (M > 0) {
             int K = choose_k();
             // LDS budget: span (TM + Q + K rows) * D elements + taps; shrink K, then the
             // tile's thread count, until it fits (large decimations: plan_8192 stage 0)
-            size_t es = esize(in_dtype), ts = (ttype == SDRGPU_C64 ? 8 : 4);
+            size_t es = esize(in_dtype);
             size_t lds = 0;
             int RSK = 0, RSP = 0;
             NT = 256;
@@ -392,7 +470,7 @@ struct FirBlock : Block {
                 const int rows = TM + Q + K;
                 RSK = (rows + K - 1) / K;
                 RSP = K * RSK + 1;
-                lds = es * (size_t)D * RSP + ts * (size_t)D * Q;
+                lds = es * (size_t)D * RSP;
                 if (lds <= 150 * 1024) break;
                 if (K > 1) K /= 2;
                 else if (NT > 64) NT /= 2;
@@ -408,9 +486,10 @@ struct FirBlock : Block {
             FirArgs a{};
             a.hist = hist[cur].p; a.in = in; a.taps = taps.p; a.out = out;
             a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
-            a.theta0 = theta0; a.w = w;
+            a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>();
             a.ntaps = ntaps; a.H = H; a.count = count; a.D = D; a.Q = Q; a.offset0 = offset; a.M = M;
             a.TMS = TMS; a.RSK = RSK; a.RSP = RSP; a.invDev = invDev;
+            a.dshift = (D & (D - 1)) ? -1 : __builtin_ctz((unsigned)D);
             int rc;
             if (in_dtype == SDRGPU_F32) {
                 rc = stereo ? launch_k<float, float, false, false, true>(a, K, tiles, lds, s)
@@ -435,37 +514,38 @@ struct FirBlock : Block {
             const int nb = (H + 255) / 256;
             if (in_dtype == SDRGPU_F32) {
                 hipLaunchKernelGGL((fir_hist_kernel<float, false>), dim3(nb), dim3(256), 0, s, hist[cur].as<float>(),
-                                   (const float*)in, hist[cur ^ 1].as<float>(), H, count, 0.0, 0.0);
+                                   (const float*)in, hist[cur ^ 1].as<float>(), H, count, nullptr, nullptr);
             } else if (xl) {
                 hipLaunchKernelGGL((fir_hist_kernel<float2, true>), dim3(nb), dim3(256), 0, s, hist[cur].as<float2>(),
-                                   (const float2*)in, hist[cur ^ 1].as<float2>(), H, count, theta0, w);
+                                   (const float2*)in, hist[cur ^ 1].as<float2>(), H, count, nco.phi.as<float2>(),
+                                   nco.plo.as<float2>());
             } else {
                 hipLaunchKernelGGL((fir_hist_kernel<float2, false>), dim3(nb), dim3(256), 0, s, hist[cur].as<float2>(),
-                                   (const float2*)in, hist[cur ^ 1].as<float2>(), H, count, 0.0, 0.0);
+                                   (const float2*)in, hist[cur ^ 1].as<float2>(), H, count, nullptr, nullptr);
             }
             SDRGPU_HIP(hipGetLastError());
         }
         cur ^= 1;
         offset = offset + M * D - count;
-        if (xl) phase.advance(w, count);
+        if (xl) nco.phase.advance(nco.w, count);
         return M;
     }
 };
 
 // --------------------------------------------------------------- xlator block
 struct XlatorBlock : Block {
-    double w = 0.0;
-    PhaseAcc phase;
+    Nco nco;
     int out_count(int count) override { return count; }
-    int reset() override { phase.reset(); return SDRGPU_OK; }
+    int reset() override { nco.phase.reset(); return SDRGPU_OK; }
     int run(const void* in, int count, void* out, hipStream_t s) override {
         SDRGPU_HIP(hipSetDevice(device));
         if (count > 0) {
+            SDRGPU_CHECK(nco.prepare(count, s));
             hipLaunchKernelGGL(xlator_kernel, dim3((count + 255) / 256), dim3(256), 0, s, (const float2*)in, (float2*)out,
-                               (long long)count, phase.value(), w);
+                               (long long)count, nco.phi.as<float2>(), nco.plo.as<float2>());
             SDRGPU_HIP(hipGetLastError());
         }
-        phase.advance(w, count);
+        nco.phase.advance(nco.w, count);
         return count;
     }
 };
@@ -544,10 +624,10 @@ struct PolyBlock : Block {
             const int nb = (H + 255) / 256;
             if (in_dtype == SDRGPU_F32)
                 hipLaunchKernelGGL((fir_hist_kernel<float, false>), dim3(nb), dim3(256), 0, s, hist[cur].as<float>(),
-                                   (const float*)in, hist[cur ^ 1].as<float>(), H, count, 0.0, 0.0);
+                                   (const float*)in, hist[cur ^ 1].as<float>(), H, count, nullptr, nullptr);
             else
                 hipLaunchKernelGGL((fir_hist_kernel<float2, false>), dim3(nb), dim3(256), 0, s, hist[cur].as<float2>(),
-                                   (const float2*)in, hist[cur ^ 1].as<float2>(), H, count, 0.0, 0.0);
+                                   (const float2*)in, hist[cur ^ 1].as<float2>(), H, count, nullptr, nullptr);
             SDRGPU_HIP(hipGetLastError());
             cur ^= 1;
         }
@@ -600,8 +680,9 @@ static std::unique_ptr<FirBlock> make_fir(int dev, int dtype, int ttype, const f
                                           bool xl = false, double w = 0.0, bool quad = false, float invDev = 1.0f,
                                           bool stereo = false) {
     auto f = std::make_unique<FirBlock>();
-    f->xl = xl; f->w = w; f->quad = quad; f->invDev = invDev; f->stereo = stereo;
+    f->xl = xl; f->quad = quad; f->invDev = invDev; f->stereo = stereo;
     *rc = f->setup(dev, dtype, ttype, taps, n, decim);
+    if (*rc >= 0 && xl) *rc = f->nco.set_w(w);
     if (*rc >= 0) *rc = f->reset();
     return f;
 }
@@ -663,8 +744,9 @@ static int build_rational(ChainBlock* c, int dev, int dtype, double inSr, double
     }
     if (xlFirst && !xlDone) {
         auto x = std::make_unique<XlatorBlock>();
-        x->device = dev; x->w = w;
+        x->device = dev;
         SDRGPU_CHECK(x->init_stream());
+        SDRGPU_CHECK(x->nco.set_w(w));
         c->kids.insert(c->kids.begin(), std::move(x));
     }
     if (rp.mode == 0 || rp.mode == 2) {
@@ -700,15 +782,8 @@ struct VfoBlock : ChainBlock {
         offset = off;
         const double w = xlator_effective_omega(hz_to_rads(-offset, inSr));
         for (auto& k : kids) {
-            if (auto* f = dynamic_cast<FirBlock*>(k.get()); f && f->xl) {
-                f->phase.advance(0.0, 0);
-                f->w = w;
-                return SDRGPU_OK;
-            }
-            if (auto* x = dynamic_cast<XlatorBlock*>(k.get())) {
-                x->w = w;
-                return SDRGPU_OK;
-            }
+            if (auto* f = dynamic_cast<FirBlock*>(k.get()); f && f->xl) return f->nco.set_w(w);
+            if (auto* x = dynamic_cast<XlatorBlock*>(k.get())) return x->nco.set_w(w);
         }
         return SDRGPU_OK;
     }
@@ -730,15 +805,15 @@ extern "C" int sdrgpu_xlator_create(sdrgpu_block** h, int device, double offsetR
     if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
     auto* x = new XlatorBlock();
     x->device = device;
-    x->w = xlator_effective_omega(offsetRad);
-    return wrap(h, x, x->init_stream());
+    int rc = x->init_stream();
+    if (rc >= 0) rc = x->nco.set_w(xlator_effective_omega(offsetRad));
+    return wrap(h, x, rc);
 }
 extern "C" int sdrgpu_xlator_set_offset(sdrgpu_block* h, double offsetRad) {
     NEED_HANDLE(h);
     auto* x = dynamic_cast<XlatorBlock*>(h->impl);
     if (!x) { set_error("not an xlator"); return SDRGPU_ESTATE; }
-    x->w = xlator_effective_omega(offsetRad);
-    return SDRGPU_OK;
+    return x->nco.set_w(xlator_effective_omega(offsetRad));
 }
 
 extern "C" int sdrgpu_fir_create(sdrgpu_block** h, int device, int dtype, int ttype, const float* taps, int ntaps, int decim) {

@@ -14,6 +14,7 @@
 //    conflicts, twiddles from an fp64-generated table.
 #include <cmath>
 #include <cstring>
+#include <cstdlib>
 #include <algorithm>
 #include "sdrgpu_internal.h"
 
@@ -92,26 +93,21 @@ template <> __device__ __forceinline__ void dft<16>(float2* v) { dft16(v); }
 __device__ __forceinline__ int pad16(int i) { return i + (i >> 4); }
 template <int L> struct Lds { static constexpr int LS = L + L / 16 + 1; };   // sequence stride (odd)
 
-// One Stockham radix-R stage over S sequences of length L held in LDS.
-// Thread (s, t) owns butterflies j = t + b*T, T = L/16, b < 16/R.
-template <int L, int S, int R, int NS>
-__device__ __forceinline__ void stockham_stage(float2* lds, const float2* __restrict__ tw, int tid) {
+// One Stockham radix-R stage, LDS -> LDS, for sequence s, thread t (T = L/16 threads per
+// sequence, each owning butterflies j = t + b*T, b < 16/R). Caller provides the barriers.
+template <int L, int R, int NS>
+__device__ __forceinline__ void stage_lds(float2* seq, const float2* __restrict__ tw, int t) {
     constexpr int T = L / 16;
     constexpr int BPT = 16 / R;
-    constexpr int LS = Lds<L>::LS;
-    const int s = tid / T, t = tid % T;
-    float2* seq = lds + s * LS;
     float2 v[BPT][R];
 #pragma unroll
     for (int b = 0; b < BPT; b++) {
         const int j = t + b * T;
 #pragma unroll
         for (int r = 0; r < R; r++) v[b][r] = seq[pad16(j + r * (L / R))];
-        if (NS > 1) {
-            const int jm = j % NS;
+        const int jm = j % NS;
 #pragma unroll
-            for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw[r * jm * (L / (NS * R))]);
-        }
+        for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw[r * jm * (L / (NS * R))]);
         dft<R>(v[b]);
     }
     __syncthreads();
@@ -125,28 +121,58 @@ __device__ __forceinline__ void stockham_stage(float2* lds, const float2* __rest
     __syncthreads();
 }
 
-// Full in-LDS FFT of S sequences of length L (L = 16^a * r).
-template <int L, int S>
-__device__ __forceinline__ void fft_lds(float2* lds, const float2* __restrict__ tw, int tid) {
-    static_assert(L >= 64 && L <= 4096, "fft length");
+// Last stage: LDS -> registers -> store functor (output index k, value).
+template <int L, int R, int NS, class Store>
+__device__ __forceinline__ void stage_last(const float2* seq, const float2* __restrict__ tw, int t, Store&& st) {
+    constexpr int T = L / 16;
+    constexpr int BPT = 16 / R;
+    float2 v[BPT][R];
+#pragma unroll
+    for (int b = 0; b < BPT; b++) {
+        const int j = t + b * T;
+#pragma unroll
+        for (int r = 0; r < R; r++) v[b][r] = seq[pad16(j + r * (L / R))];
+        const int jm = j % NS;
+#pragma unroll
+        for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw[r * jm * (L / (NS * R))]);
+        dft<R>(v[b]);
+    }
+#pragma unroll
+    for (int b = 0; b < BPT; b++) {
+        const int j = t + b * T;
+        const int idxD = (j / NS) * NS * R + (j % NS);
+#pragma unroll
+        for (int r = 0; r < R; r++) st(idxD + r * NS, v[b][r]);
+    }
+}
+
+// Stage 1 of a length-L Stockham FFT on a thread's 16 register values (radix 16, NS = 1,
+// no twiddles), written to the sequence's LDS image.
+template <int L>
+__device__ __forceinline__ void stage_first(float2* seq, float2 (&v)[16], int t) {
+    dft16(v);
+#pragma unroll
+    for (int r = 0; r < 16; r++) seq[pad16(t * 16 + r)] = v[r];
+}
+
+// Stages after the first: LDS -> ... -> store functor. Expects stage_first's LDS writes
+// to be complete (caller's barrier); leaves the LDS free for reuse on return.
+template <int L, class Store>
+__device__ __forceinline__ void stages_rest(float2* lds, const float2* __restrict__ tw, int sL, int tL, Store&& st) {
+    constexpr int LS = Lds<L>::LS;
+    const float2* seqL = lds + sL * LS;
     if constexpr (L == 64) {
-        stockham_stage<L, S, 16, 1>(lds, tw, tid); stockham_stage<L, S, 4, 16>(lds, tw, tid);
+        stage_last<L, 4, 16>(seqL, tw, tL, st);
     } else if constexpr (L == 128) {
-        stockham_stage<L, S, 16, 1>(lds, tw, tid); stockham_stage<L, S, 8, 16>(lds, tw, tid);
+        stage_last<L, 8, 16>(seqL, tw, tL, st);
     } else if constexpr (L == 256) {
-        stockham_stage<L, S, 16, 1>(lds, tw, tid); stockham_stage<L, S, 16, 16>(lds, tw, tid);
-    } else if constexpr (L == 512) {
-        stockham_stage<L, S, 16, 1>(lds, tw, tid); stockham_stage<L, S, 16, 16>(lds, tw, tid);
-        stockham_stage<L, S, 2, 256>(lds, tw, tid);
-    } else if constexpr (L == 1024) {
-        stockham_stage<L, S, 16, 1>(lds, tw, tid); stockham_stage<L, S, 16, 16>(lds, tw, tid);
-        stockham_stage<L, S, 4, 256>(lds, tw, tid);
-    } else if constexpr (L == 2048) {
-        stockham_stage<L, S, 16, 1>(lds, tw, tid); stockham_stage<L, S, 16, 16>(lds, tw, tid);
-        stockham_stage<L, S, 8, 256>(lds, tw, tid);
+        stage_last<L, 16, 16>(seqL, tw, tL, st);
     } else {
-        stockham_stage<L, S, 16, 1>(lds, tw, tid); stockham_stage<L, S, 16, 16>(lds, tw, tid);
-        stockham_stage<L, S, 16, 256>(lds, tw, tid);
+        stage_lds<L, 16, 16>(lds + sL * LS, tw, tL);   // middle stage (radix 16, NS = 16)
+        if constexpr (L == 512) stage_last<L, 2, 256>(seqL, tw, tL, st);
+        else if constexpr (L == 1024) stage_last<L, 4, 256>(seqL, tw, tL, st);
+        else if constexpr (L == 2048) stage_last<L, 8, 256>(seqL, tw, tL, st);
+        else stage_last<L, 16, 256>(seqL, tw, tL, st);
     }
 }
 
@@ -155,118 +181,173 @@ __device__ __forceinline__ float db_of(float2 X) {
     return 10.0f * log10f(X.x * X.x + X.y * X.y);
 }
 
-// ---- single pass (N <= 4096): S frames per workgroup -------------------------
+// Persistent tile loop shared by the three spectrum kernels. Each workgroup walks tiles
+// blockIdx.x, +gridDim.x, ...; the 16 raw loads of tile i+1 (Frag) are issued before tile i
+// is transformed and stored, so HBM latency overlaps the LDS exchange, the math and the
+// stores of the previous tile (one register fragment in flight per thread).
+template <int L, class Frag, class Issue, class Finish, class Store>
+__device__ __forceinline__ void tile_loop(float2* lds, const float2* __restrict__ tw, int ntiles, int sF, int tF, int sL,
+                                          int tL, Issue&& issue, Finish&& finish, Store&& store) {
+    // One tile per workgroup (grid = tiles). A persistent variant with a ping-pong register
+    // prefetch of the next tile was measured at the same 64k throughput with a quarter of the
+    // occupancy (and spills at N1 = 1024), so the simple form is kept.
+    constexpr int LS = Lds<L>::LS;
+    const int tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    Frag fr;
+    issue(fr, tile);
+    float2 v[16];
+    finish(fr, v);
+    stage_first<L>(lds + sF * LS, v, tF);
+    __syncthreads();
+    stages_rest<L>(lds, tw, sL, tL, [&](int k, float2 y) { store(tile, k, y); });
+}
+
+struct FragW {   // raw input + window values for 16 samples
+    float2 x[16];
+    float w[16];
+};
+struct FragC {
+    float2 x[16];
+};
+
+// ---- single pass (N <= 4096): S frames per tile -------------------------------
 template <int L, int S>
 __global__ __launch_bounds__(S * L / 16) void fft_single_kernel(
     const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz,
     const float2* __restrict__ tw, float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    constexpr int NT = S * L / 16;
-    constexpr int LS = Lds<L>::LS;
+    constexpr int T = L / 16;
     const int tid = threadIdx.x;
-    const int f0 = blockIdx.x * S;
-    for (int e = tid; e < S * L; e += NT) {
-        const int s = e / L, n = e % L;
-        const int f = f0 + s;
-        float2 v = make_float2(0.f, 0.f);
-        if (f < frames && n < nz) {
-            const float2 x = in[(long long)f * frameStride + n];
-            const float w = win[n];
-            v = make_float2(x.x * w, x.y * w);
-        }
-        lds[s * LS + pad16(n)] = v;
-    }
-    __syncthreads();
-    fft_lds<L, S>(lds, tw, tid);
-    for (int e = tid; e < S * L; e += NT) {
-        const int s = e / L, k = e % L;
-        const int f = f0 + s;
-        if (f < frames) out[(long long)f * L + k] = db_of(lds[s * LS + pad16(k)]);
-    }
+    const int s = tid / T, t = tid % T;           // frame-contiguous mapping for load and store
+    const int ntiles = (frames + S - 1) / S;
+    tile_loop<L, FragW>(
+        lds, tw, ntiles, s, t, s, t,
+        [&](FragW& fr, int tile) {
+            const int f = min(tile * S + s, frames - 1);
+            const float2* x = in + (long long)f * frameStride;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int n = t + r * T;
+                const int nc = n < nz ? n : nz - 1;
+                fr.x[r] = x[nc];
+                fr.w[r] = n < nz ? win[nc] : 0.0f;
+            }
+        },
+        [&](const FragW& fr, float2 (&v)[16]) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) v[r] = make_float2(fr.x[r].x * fr.w[r], fr.x[r].y * fr.w[r]);
+        },
+        [&](int tile, int k, float2 y) {
+            const int f = tile * S + s;
+            if (f < frames) out[(long long)f * L + k] = db_of(y);
+        });
 }
 
-// ---- pass A: S columns x N1 rows per workgroup ---------------------------------
+// ---- pass A: S columns x N1 rows per tile ---------------------------------------
+// Column c of the frame viewed as N1 x N2: x[n1*N2 + c0 + c]. The column index is the
+// fastest-varying thread coordinate in both the load and the store, so each wave reads
+// and writes whole 128-B row segments (S = 16 columns x 8 B).
+// Four-step twiddle W_N^(n2 k1), n2 = c0 + c = S*b + c:
+//   W_N^(S b k1) from Tbase[b][k1] (one value per 16 lanes) x W_N^(c k1) from Tcol[k1][c]
+// (contiguous per 16 lanes); both fp64-generated, one complex product.
 template <int L, int S>
 __global__ __launch_bounds__(S * L / 16) void fft_passA_kernel(
-    const float2* __restrict__ in, long long frameStride, const float* __restrict__ win, int nz, int N2, int logN,
-    const float2* __restrict__ tw, float2* __restrict__ scratch) {
+    const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
+    int logN, const float2* __restrict__ tw, const float2* __restrict__ tbase, const float2* __restrict__ tcol,
+    float2* __restrict__ scratch) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    constexpr int NT = S * L / 16;
-    constexpr int LS = Lds<L>::LS;
     const int tid = threadIdx.x;
-    const int c0 = blockIdx.x * S;
-    const long long f = blockIdx.y;
-    const float2* x = in + f * frameStride;
-    for (int e = tid; e < S * L; e += NT) {
-        const int c = e % S, n1 = e / S;
-        const int n = n1 * N2 + c0 + c;
-        float2 v = make_float2(0.f, 0.f);
-        if (n < nz) {
-            const float2 xv = x[n];
-            const float w = win[n];
-            v = make_float2(xv.x * w, xv.y * w);
-        }
-        lds[c * LS + pad16(n1)] = v;
-    }
-    __syncthreads();
-    fft_lds<L, S>(lds, tw, tid);
-    const long long N = 1LL << logN;
-    float2* dst = scratch + f * N;
-    const float inv = 2.0f / (float)N;
-    for (int e = tid; e < S * L; e += NT) {
-        const int c = e % S, k1 = e / S;
-        const int n2 = c0 + c;
-        const int m = n2 * k1;                  // < N: exact twiddle index
-        float sn, cs;
-        sincospif(-(float)m * inv, &sn, &cs);   // W_N^(n2 k1)
-        dst[(long long)k1 * N2 + n2] = cmul(lds[c * LS + pad16(k1)], make_float2(cs, sn));
-    }
+    const int c = tid % S, t = tid / S;
+    constexpr int T = L / 16;
+    const int nb = N2 / S;                        // column blocks per frame
+    const int ntiles = nb * frames;
+    tile_loop<L, FragW>(
+        lds, tw, ntiles, c, t, c, t,
+        [&](FragW& fr, int tile) {
+            const int b = tile % nb;
+            const long long f = tile / nb;
+            const int col = b * S + c;
+            const float2* x = in + f * frameStride;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const long long n = (long long)(t + r * T) * N2 + col;
+                const bool live = n < nz;
+                const long long nc = live ? n : 0;   // frame[0]: always in bounds
+                fr.x[r] = x[nc];
+                fr.w[r] = live ? win[nc] : 0.0f;
+            }
+        },
+        [&](const FragW& fr, float2 (&v)[16]) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) v[r] = make_float2(fr.x[r].x * fr.w[r], fr.x[r].y * fr.w[r]);
+        },
+        [&](int tile, int k1, float2 y) {
+            const int b = tile % nb;
+            const long long f = tile / nb;
+            const float2 t0 = cmul(tbase[(long long)b * L + k1], tcol[k1 * S + c]);
+            scratch[(f << logN) + (long long)k1 * N2 + b * S + c] = cmul(y, t0);
+        });
 }
 
-// ---- pass B: S rows of length N2 per workgroup, dB out, transposed store ------------
+// ---- pass B: S rows of length N2 per tile, dB out, transposed store -----------------
+// Stage 1 maps threads row-contiguous (coalesced row reads); the last stage maps the row
+// index fastest so the transposed dB store writes S consecutive floats per k2.
 template <int L, int S>
 __global__ __launch_bounds__(S * L / 16) void fft_passB_kernel(
-    const float2* __restrict__ scratch, int N1, int logN, const float2* __restrict__ tw, float* __restrict__ out) {
+    const float2* __restrict__ scratch, int frames, int N1, int logN, const float2* __restrict__ tw,
+    float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    constexpr int NT = S * L / 16;
-    constexpr int LS = Lds<L>::LS;
+    constexpr int T = L / 16;
     const int tid = threadIdx.x;
-    const int r0 = blockIdx.x * S;
-    const long long f = blockIdx.y;
-    const long long N = 1LL << logN;
-    const float2* src = scratch + f * N + (long long)r0 * L;
-    for (int e = tid; e < S * L; e += NT) {
-        const int kk = e / L, n2 = e % L;
-        lds[kk * LS + pad16(n2)] = src[e];
-    }
-    __syncthreads();
-    fft_lds<L, S>(lds, tw, tid);
-    float* dst = out + f * N;
-    for (int e = tid; e < S * L; e += NT) {
-        const int kk = e % S, k2 = e / S;
-        dst[(long long)(r0 + kk) + (long long)N1 * k2] = db_of(lds[kk * LS + pad16(k2)]);
-    }
+    const int sF = tid / T, tF = tid % T;
+    const int sL = tid % S, tL = tid / S;
+    const int nb = N1 / S;
+    const int ntiles = nb * frames;
+    tile_loop<L, FragC>(
+        lds, tw, ntiles, sF, tF, sL, tL,
+        [&](FragC& fr, int tile) {
+            const int b = tile % nb;
+            const long long f = tile / nb;
+            const float2* src = scratch + (f << logN) + (long long)(b * S + sF) * L + tF;
+#pragma unroll
+            for (int r = 0; r < 16; r++) fr.x[r] = src[r * T];
+        },
+        [&](const FragC& fr, float2 (&v)[16]) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) v[r] = fr.x[r];
+        },
+        [&](int tile, int k2, float2 y) {
+            const int b = tile % nb;
+            const long long f = tile / nb;
+            out[(f << logN) + b * S + sL + (long long)N1 * k2] = db_of(y);
+        });
 }
 
 // ---------------------------------------------------------------- host side
 struct FftPlan {
     int device = 0, N = 0, logN = 0, nz = 0;
     int N1 = 0, N2 = 0;               // two-pass split (N1 * N2 = N); N1 = 0 -> single pass
-    DevBuf win, tw1, tw2, scratch;
+    DevBuf win, tw1, tw2, tbase, tcol, scratch;
     int chunkFrames = 1;
+    int sa = 16, sb = 32;             // pass-A columns / pass-B rows per workgroup (tuning)
+    int dbg = 0;                      // timing-only ablations (SDRGPU_FFT_DEBUG; wrong results)
+    int tcolS = 0;                    // columns of the [k1][c] twiddle table
     hipStream_t own = nullptr;
     PinnedBuf pin_in, pin_out;
     DevBuf dev_in, dev_out;
 };
 
-static int make_twiddles(DevBuf& b, int L) {
-    std::vector<float2> t(L);
-    for (int m = 0; m < L; m++) {
-        double a = -2.0 * M_PI * (double)m / (double)L;
+// t[m] = exp(-2 pi i (m * step) / L) for m < count (fp64 -> float)
+static int make_twiddles(DevBuf& b, int L, int count = -1, int step = 1) {
+    if (count < 0) count = L;
+    std::vector<float2> t(count);
+    for (int m = 0; m < count; m++) {
+        double a = -2.0 * M_PI * (double)((long long)m * step % L) / (double)L;
         t[m] = make_float2((float)std::cos(a), (float)std::sin(a));
     }
-    SDRGPU_CHECK(b.ensure(sizeof(float2) * L));
-    SDRGPU_HIP(hipMemcpy(b.p, t.data(), sizeof(float2) * L, hipMemcpyHostToDevice));
+    SDRGPU_CHECK(b.ensure(sizeof(float2) * count));
+    SDRGPU_HIP(hipMemcpy(b.p, t.data(), sizeof(float2) * count, hipMemcpyHostToDevice));
     return SDRGPU_OK;
 }
 
@@ -290,12 +371,13 @@ static int launch_single(const FftPlan& p, const float2* in, long long stride, i
 
 template <int L, int S>
 static int launch_passA(const FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
+    if (p.tcolS != S) { set_error("fft: column twiddle table built for %d columns, kernel uses %d", p.tcolS, S); return SDRGPU_ESTATE; }
     auto k = fft_passA_kernel<L, S>;
     size_t lds = sizeof(float2) * S * Lds<L>::LS;
     SDRGPU_CHECK(set_lds(k, lds));
-    dim3 grid(p.N2 / S, frames);
-    hipLaunchKernelGGL(k, grid, dim3(S * L / 16), lds, s, in, stride, p.win.as<float>(), p.nz, p.N2, p.logN,
-                       p.tw1.as<float2>(), p.scratch.as<float2>());
+    const int g = (p.N2 / S) * frames;
+    hipLaunchKernelGGL(k, dim3(g), dim3(S * L / 16), lds, s, in, stride, frames, p.win.as<float>(), p.nz, p.N2,
+                       p.logN, p.tw1.as<float2>(), p.tbase.as<float2>(), p.tcol.as<float2>(), p.scratch.as<float2>());
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
@@ -305,8 +387,8 @@ static int launch_passB(const FftPlan& p, int frames, float* out, hipStream_t s)
     auto k = fft_passB_kernel<L, S>;
     size_t lds = sizeof(float2) * S * Lds<L>::LS;
     SDRGPU_CHECK(set_lds(k, lds));
-    dim3 grid(p.N1 / S, frames);
-    hipLaunchKernelGGL(k, grid, dim3(S * L / 16), lds, s, p.scratch.as<float2>(), p.N1, p.logN,
+    const int g = (p.N1 / S) * frames;
+    hipLaunchKernelGGL(k, dim3(g), dim3(S * L / 16), lds, s, p.scratch.as<float2>(), frames, p.N1, p.logN,
                        p.tw2.as<float2>(), out);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
@@ -326,14 +408,19 @@ static int dispatch_single(const FftPlan& p, const float2* in, long long stride,
     return SDRGPU_EARG;
 }
 
-// pass-A column FFT length N1 with 16 columns per workgroup (128-B row segments)
+// pass-A column FFT length N1 with SA columns per workgroup (8*SA-byte row segments)
 static int dispatch_passA(const FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
     switch (p.N1) {
     case 64: return launch_passA<64, 16>(p, in, stride, frames, s);
     case 128: return launch_passA<128, 16>(p, in, stride, frames, s);
-    case 256: return launch_passA<256, 16>(p, in, stride, frames, s);
-    case 512: return launch_passA<512, 16>(p, in, stride, frames, s);
-    case 1024: return launch_passA<1024, 16>(p, in, stride, frames, s);
+    case 256:
+        if (p.sa == 64) return launch_passA<256, 64>(p, in, stride, frames, s);
+        if (p.sa == 32) return launch_passA<256, 32>(p, in, stride, frames, s);
+        return launch_passA<256, 16>(p, in, stride, frames, s);
+    case 512: return launch_passA<512, 8>(p, in, stride, frames, s);
+    case 1024:
+        if (p.sa == 16) return launch_passA<1024, 16>(p, in, stride, frames, s);
+        return launch_passA<1024, 8>(p, in, stride, frames, s);   // (sa 8 only on request)
     }
     set_error("fft: unsupported N1 %d", p.N1);
     return SDRGPU_EARG;
@@ -343,7 +430,10 @@ static int dispatch_passB(const FftPlan& p, int frames, float* out, hipStream_t 
     switch (p.N2) {
     case 64: return launch_passB<64, 32>(p, frames, out, s);
     case 128: return launch_passB<128, 32>(p, frames, out, s);
-    case 256: return launch_passB<256, 32>(p, frames, out, s);
+    case 256:
+        if (p.sb == 64) return launch_passB<256, 64>(p, frames, out, s);
+        if (p.sb == 16) return launch_passB<256, 16>(p, frames, out, s);
+        return launch_passB<256, 32>(p, frames, out, s);
     case 512: return launch_passB<512, 16>(p, frames, out, s);
     case 1024: return launch_passB<1024, 16>(p, frames, out, s);
     }
@@ -390,9 +480,46 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         p.N2 = fftSize / p.N1;
         rc = make_twiddles(p.tw1, p.N1);
         if (rc >= 0) rc = make_twiddles(p.tw2, p.N2);
+
         // chunk so the pass-A -> pass-B intermediate (+ the input it came from) stays
         // resident in the Infinity Cache: 64 MB of intermediate per chunk
-        p.chunkFrames = std::max(1, (int)((64ll << 20) / ((long long)fftSize * 8)));
+        long long chunkMB = 64;
+        if (const char* e = getenv("SDRGPU_FFT_CHUNK_MB")) chunkMB = std::max(1, atoi(e));
+        if (const char* e = getenv("SDRGPU_FFT_SA")) p.sa = atoi(e);
+        if (const char* e = getenv("SDRGPU_FFT_SB")) p.sb = atoi(e);
+        if (const char* e = getenv("SDRGPU_FFT_DEBUG")) p.dbg = atoi(e);
+        p.chunkFrames = std::max(1, (int)((chunkMB << 20) / ((long long)fftSize * 8)));
+        // pass-A columns per workgroup actually dispatched for this N1 (see dispatch_passA)
+        p.tcolS = (p.N1 == 256) ? (p.sa == 64 ? 64 : p.sa == 32 ? 32 : 16)
+                : (p.N1 == 512) ? 8 : (p.N1 == 1024) ? (p.sa == 16 ? 16 : 8) : 16;
+        if (rc >= 0) {   // Tbase[b][k1] = W_N^(S b k1) for the N2/S column blocks
+            const int nb = p.N2 / p.tcolS;
+            std::vector<float2> t((size_t)nb * p.N1);
+            for (int b = 0; b < nb; b++)
+                for (int k1 = 0; k1 < p.N1; k1++) {
+                    const long long m = ((long long)b * p.tcolS * k1) % fftSize;
+                    const double a = -2.0 * M_PI * (double)m / (double)fftSize;
+                    t[(size_t)b * p.N1 + k1] = make_float2((float)std::cos(a), (float)std::sin(a));
+                }
+            rc = p.tbase.ensure(sizeof(float2) * t.size());
+            if (rc >= 0 && hipMemcpy(p.tbase.p, t.data(), sizeof(float2) * t.size(), hipMemcpyHostToDevice) != hipSuccess) {
+                set_error("fft: twiddle upload failed");
+                rc = SDRGPU_EHIP;
+            }
+        }
+        if (rc >= 0) {
+            std::vector<float2> t((size_t)p.N1 * p.tcolS);
+            for (int k1 = 0; k1 < p.N1; k1++)
+                for (int c = 0; c < p.tcolS; c++) {
+                    const double a = -2.0 * M_PI * (double)((long long)c * k1) / (double)fftSize;
+                    t[(size_t)k1 * p.tcolS + c] = make_float2((float)std::cos(a), (float)std::sin(a));
+                }
+            rc = p.tcol.ensure(sizeof(float2) * t.size());
+            if (rc >= 0 && hipMemcpy(p.tcol.p, t.data(), sizeof(float2) * t.size(), hipMemcpyHostToDevice) != hipSuccess) {
+                set_error("fft: twiddle upload failed");
+                rc = SDRGPU_EHIP;
+            }
+        }
         if (rc >= 0) rc = p.scratch.ensure((size_t)p.chunkFrames * fftSize * sizeof(float2));
     }
     if (rc >= 0 && hipStreamCreateWithFlags(&p.own, hipStreamNonBlocking) != hipSuccess) {

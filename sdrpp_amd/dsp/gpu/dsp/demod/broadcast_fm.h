@@ -1,0 +1,80 @@
+// GPU-backed dsp::demod::BroadcastFM -- drop-in for core/src/dsp/demod/broadcast_fm.h,
+// mono path (stereo == false, no RDS; broadcast_fm.h:144-215 else-branch): quadrature(dev)
+// -> 15 kHz audio low-pass (lowPass(15e3, 4e3, fs)) -> LRToStereo(l = r).
+// Stereo decoding (pilot PLL) and RDS are not on the GPU yet: init()/setStereo(true)
+// report an error instead of silently producing mono (DESIGN.md, section 8 "next").
+#pragma once
+#include "../processor.h"
+#include "../sdrgpu_handle.h"
+
+namespace dsp::demod {
+class BroadcastFM : public Processor<complex_t, stereo_t> {
+    using base_type = Processor<complex_t, stereo_t>;
+public:
+    BroadcastFM() {}
+    BroadcastFM(stream<complex_t>* in, double deviation, double samplerate, bool stereo = true, bool lowPass = true,
+                bool rdsOut = false) {
+        init(in, deviation, samplerate, stereo, lowPass, rdsOut);
+    }
+    virtual void init(stream<complex_t>* in, double deviation, double samplerate, bool stereo = true, bool lowPass = true,
+                      bool rdsOut = false) {
+        _deviation = deviation;
+        _samplerate = samplerate;
+        _stereo = stereo;
+        _lowPass = lowPass;
+        _rdsOut = rdsOut;
+        rebuild();
+        base_type::init(in);
+    }
+    void setDeviation(double deviation) {
+        std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx);
+        _deviation = deviation;
+        rebuild();
+    }
+    void setSamplerate(double samplerate) { set(samplerate, _stereo, _lowPass, _rdsOut); }
+    void setStereo(bool stereo) { set(_samplerate, stereo, _lowPass, _rdsOut); }
+    void setLowPass(bool lowPass) { set(_samplerate, _stereo, lowPass, _rdsOut); }
+    void setRDSOut(bool rdsOut) { set(_samplerate, _stereo, _lowPass, rdsOut); }
+    void reset() {
+        std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx);
+        base_type::tempStop();
+        gpu::ok(sdrgpu_block_reset(_h.h), "wfm_reset");
+        base_type::tempStart();
+    }
+    inline int process(int count, complex_t* in, stereo_t* out, int& rdsOutCount, complex_t* rdsout = nullptr) {
+        rdsOutCount = 0;
+        if (_stereo || _rdsOut) return -1;
+        return _h.process(in, count, out, "wfm");
+    }
+    int run() override {
+        int count = base_type::_in->read();
+        if (count < 0) return -1;
+        int rds = 0;
+        int n = process(count, base_type::_in->readBuf, base_type::out.writeBuf, rds);
+        base_type::_in->flush();
+        if (n < 0 || !base_type::out.swap(count)) return -1;
+        return count;
+    }
+    stream<complex_t> rdsOut;
+
+protected:
+    void set(double sr, bool stereo, bool lp, bool rds) {
+        std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx);
+        base_type::tempStop();
+        _samplerate = sr; _stereo = stereo; _lowPass = lp; _rdsOut = rds;
+        rebuild();
+        base_type::tempStart();
+    }
+    void rebuild() {
+        if (_stereo || _rdsOut) {
+            std::fprintf(stderr, "[sdrgpu] BroadcastFM: stereo/RDS decoding is not available on the GPU path yet\n");
+        }
+        sdrgpu_block* h = nullptr;
+        gpu::ok(sdrgpu_wfm_create(&h, gpu::device(), _deviation, _samplerate, _lowPass), "wfm_create");
+        _h.reset(h);
+    }
+    double _deviation = 0, _samplerate = 0;
+    bool _stereo = false, _lowPass = true, _rdsOut = false;
+    gpu::Handle _h;
+};
+}  // namespace dsp::demod

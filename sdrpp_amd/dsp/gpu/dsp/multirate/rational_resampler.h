@@ -1,0 +1,59 @@
+// GPU-backed dsp::multirate::RationalResampler<T> -- drop-in for
+// core/src/dsp/multirate/rational_resampler.h: power-of-two pre-decimation + polyphase
+// interp/decim planned exactly like reconfigure() (rational_resampler.h:121-167).
+#pragma once
+#include <type_traits>
+#include "../processor.h"
+#include "../sdrgpu_handle.h"
+
+namespace dsp::multirate {
+template <class T>
+class RationalResampler : public Processor<T, T> {
+    using base_type = Processor<T, T>;
+public:
+    RationalResampler() {}
+    RationalResampler(stream<T>* in, double inSamplerate, double outSamplerate) { init(in, inSamplerate, outSamplerate); }
+    void init(stream<T>* in, double inSamplerate, double outSamplerate) {
+        _inSamplerate = inSamplerate;
+        _outSamplerate = outSamplerate;
+        reconfigure();
+        base_type::init(in);
+    }
+    void reset() {
+        std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx);
+        base_type::tempStop();
+        gpu::ok(sdrgpu_block_reset(_h.h), "rational_reset");
+        base_type::tempStart();
+    }
+    void setInSamplerate(double inSamplerate) { setRates(inSamplerate, _outSamplerate); }
+    void setOutSamplerate(double outSamplerate) { setRates(_inSamplerate, outSamplerate); }
+    void setRates(double inSamplerate, double outSamplerate) {
+        std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx);
+        base_type::tempStop();
+        _inSamplerate = inSamplerate;
+        _outSamplerate = outSamplerate;
+        reconfigure();
+        base_type::tempStart();
+    }
+    inline int process(int count, const T* in, T* out) { return _h.process(in, count, out, "rational_resampler"); }
+    int run() override {
+        int count = base_type::_in->read();
+        if (count < 0) return -1;
+        int n = process(count, base_type::_in->readBuf, base_type::out.writeBuf);
+        base_type::_in->flush();
+        if (n < 0) return -1;
+        if (n && !base_type::out.swap(n)) return -1;
+        return n;
+    }
+
+protected:
+    void reconfigure() {
+        sdrgpu_block* h = nullptr;
+        gpu::ok(sdrgpu_rational_resampler_create(&h, gpu::device(), std::is_same_v<T, float> ? SDRGPU_F32 : SDRGPU_C64,
+                                                 _inSamplerate, _outSamplerate), "rational_create");
+        _h.reset(h);
+    }
+    double _inSamplerate = 0, _outSamplerate = 0;
+    gpu::Handle _h;
+};
+}  // namespace dsp::multirate

@@ -1,0 +1,116 @@
+// C++ drop-in test: the GPU-backed dsp:: blocks run inside the reference's threaded
+// stream/block model (runtime mirror) and match the CPU restatement (oracle) sample for
+// sample within the stated tolerances. Built and run by tests/test_cpp_dropin.py.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include <dsp/stream.h>
+#include <dsp/sink/handler_sink.h>
+#include "dsp/channel/rx_vfo.h"
+#include "dsp/demod/broadcast_fm.h"
+#include "dsp/demod/quadrature.h"
+#include "dsp/filter/decimating_fir.h"
+#include "dsp/signal_path/gpu_spectrum.h"
+#include "sdr_oracle.h"
+
+static int failures = 0;
+#define CHECK(c, ...) do { if (!(c)) { std::printf("FAIL %s:%d ", __FILE__, __LINE__); std::printf(__VA_ARGS__); std::printf("\n"); failures++; } } while (0)
+
+// feeds `blocks` of IQ into a stream from a writer thread (SpeedTester-style)
+struct Feeder {
+    dsp::stream<dsp::complex_t> out;
+};
+
+int main() {
+    std::mt19937 gen(0xACE1);
+    std::uniform_real_distribution<float> U(-1.f, 1.f);
+    const int blk = 307200, nblk = 6;
+    std::vector<dsp::complex_t> x((size_t)blk * nblk);
+    for (auto& v : x) v = {U(gen), U(gen)};
+
+    // 1. threaded pipeline: stream -> RxVFO(61.44M -> 240k) -> BroadcastFM mono -> collector
+    {
+        dsp::stream<dsp::complex_t> src;
+        dsp::channel::RxVFO vfo(&src, 61.44e6, 240000, 200000, 2.5e6);
+        dsp::demod::BroadcastFM wfm(&vfo.out, 100000, 240000, false, true, false);
+        std::vector<dsp::stereo_t> got;
+        dsp::sink::Handler<dsp::stereo_t> sink(&wfm.out, [](dsp::stereo_t* d, int n, void* ctx) {
+            auto* g = (std::vector<dsp::stereo_t>*)ctx;
+            g->insert(g->end(), d, d + n);
+        }, &got);
+        vfo.start(); wfm.start(); sink.start();
+        for (int b = 0; b < nblk; b++) {
+            std::memcpy(src.writeBuf, x.data() + (size_t)b * blk, sizeof(dsp::complex_t) * blk);
+            CHECK(src.swap(blk), "swap");
+        }
+        // wait for the last batch to drain
+        for (int i = 0; i < 200 && (int)got.size() < nblk * blk / 256; i++) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+        sink.stop(); wfm.stop(); vfo.stop();
+
+        orc_vfo* ov = orc_vfo_create(61.44e6, 240000, 200000, 2.5e6, 1);
+        orc_wfm* ow = orc_wfm_create(100000, 240000, 1, 1);
+        std::vector<float> ifb(2 * blk), aud(2 * blk);
+        std::vector<float> want;
+        for (int b = 0; b < nblk; b++) {
+            int m = orc_vfo_process(ov, (const float*)(x.data() + (size_t)b * blk), blk, ifb.data());
+            orc_wfm_process(ow, ifb.data(), m, aud.data());
+            want.insert(want.end(), aud.begin(), aud.begin() + 2 * m);
+        }
+        CHECK(got.size() * 2 == want.size(), "pipeline output count %zu vs %zu", got.size() * 2, want.size());
+        double err = 0;
+        for (size_t i = 0; i < got.size() && 2 * i + 1 < want.size(); i++) {
+            err = std::fmax(err, std::fabs(got[i].l - want[2 * i]));
+            CHECK(got[i].l == got[i].r, "mono l != r at %zu", i);
+            if (failures > 5) break;
+        }
+        CHECK(err < 1e-3, "pipeline audio max err %g", err);
+        std::printf("pipeline RxVFO->WFM: %zu stereo samples, max err %.3g\n", got.size(), err);
+        orc_vfo_destroy(ov); orc_wfm_destroy(ow);
+    }
+
+    // 2. direct process() calls (the reference's synchronous call style)
+    {
+        std::vector<float> taps(256);
+        int n = sdrgpu_taps_low_pass(3.0e6, 912000.0, 61.44e6, 0, taps.data());
+        CHECK(n == 256, "tap count %d", n);
+        dsp::tap<float> t{taps.data(), (unsigned)n};
+        dsp::stream<dsp::complex_t> dummy;
+        dsp::filter::DecimatingFIR<dsp::complex_t, float> fir(&dummy, t, 8);
+        orc_fir* of = orc_fir_create(1, 0, taps.data(), n, 8, 1);
+        std::vector<dsp::complex_t> y(blk);
+        std::vector<float> yo(2 * blk);
+        double err = 0;
+        for (int b = 0; b < 3; b++) {
+            int m = fir.process(blk, x.data() + (size_t)b * blk, y.data());
+            int mo = orc_fir_process(of, (const float*)(x.data() + (size_t)b * blk), blk, yo.data());
+            CHECK(m == mo, "decim fir count %d vs %d", m, mo);
+            for (int i = 0; i < m; i++) err = std::fmax(err, std::fmax(std::fabs(y[i].re - yo[2 * i]), std::fabs(y[i].im - yo[2 * i + 1])));
+        }
+        CHECK(err < 1e-5, "decim fir err %g", err);
+        std::printf("DecimatingFIR<complex_t,float> 256/8: max err %.3g\n", err);
+        orc_fir_destroy(of);
+    }
+
+    // 3. spectrum handler with acquire/release (including the NULL-buffer case)
+    {
+        dsp::gpu::Spectrum sp;
+        CHECK(sp.update(65536, 65536, 6), "spectrum update");
+        std::vector<float> row(65536), work(4 * 65536), ref(65536), win(65536);
+        int acquired = 0, released = 0;
+        sp.handler(x.data(), 65536, [&]() { acquired++; return row.data(); }, [&]() { released++; });
+        sp.handler(x.data(), 65536, [&]() { acquired++; return (float*)nullptr; }, [&]() { released++; });
+        CHECK(acquired == 2 && released == 2, "acquire/release %d/%d", acquired, released);
+        orc_create_window(6, win.data(), 65536, 1);
+        orc_fft_logmag((const float*)x.data(), 65536, 65536, win.data(), work.data(), ref.data());
+        double err = 0, peak = -1e30;
+        for (float v : ref) peak = std::fmax(peak, v);
+        for (int k = 0; k < 65536; k++) if (ref[k] > peak - 60) err = std::fmax(err, std::fabs(row[k] - ref[k]));
+        CHECK(err < 2e-3, "spectrum err %g dB", err);
+        std::printf("Spectrum 64k BH7 via handler: max |dB err| within 60 dB of peak %.3g\n", err);
+    }
+    std::printf(failures ? "FAILED (%d)\n" : "ALL OK\n", failures);
+    return failures ? 1 : 0;
+}

@@ -1,0 +1,236 @@
+"""CPU suite: pin the oracle (CPU restatement) against the committed golden fixtures and
+independent fp64 evaluations of the reference formulas; check the product's host-side
+design code (windows, taps, plans) is bit-identical to the oracle's."""
+import hashlib
+import math
+
+import numpy as np
+import pytest
+
+import oracle
+from sdrpp_amd import dsp
+from _util import GOLDEN, EPS32
+
+
+def _bits(a):
+    return np.asarray(a, dtype=np.float32).view(np.uint32)
+
+
+# -------------------------------------------------------------------- windows
+@pytest.mark.parametrize("wtype", range(7))
+def test_window_oracle_vs_golden(wtype):
+    g = np.load(GOLDEN + "/windows.npz")
+    np.testing.assert_array_equal(_bits(oracle.create_window(wtype, 4096)), _bits(g[f"w{wtype}_4096"]))
+
+
+def test_window_bh7_64k_and_sha():
+    g = np.load(GOLDEN + "/windows.npz")
+    np.testing.assert_array_equal(_bits(oracle.create_window(6, 65536)), _bits(g["w6_65536"]))
+    want = dict(line.split() for line in open(GOLDEN + "/windows_sha256.txt"))
+    for n, h in want.items():
+        assert hashlib.sha256(oracle.create_window(6, int(n)).tobytes()).hexdigest() == h
+
+
+@pytest.mark.parametrize("wtype,size,centered", [(6, 65536, True), (6, 1000000, True), (4, 1024, False),
+                                                 (2, 4097, True), (0, 100, True), (5, 2048, False)])
+def test_product_window_bit_exact(wtype, size, centered):
+    # libsdrgpu host design code == oracle restatement, bit for bit (no GPU needed)
+    np.testing.assert_array_equal(_bits(dsp.create_window(wtype, size, centered)),
+                                  _bits(oracle.create_window(wtype, size, centered)))
+
+
+def test_window_properties():
+    # unity coherent gain and the centred sign flip (window.h:53-62)
+    w = oracle.create_window(6, 4096)
+    assert abs(float(np.abs(w.astype(np.float64)).sum()) - 1.0) < 1e-6
+    assert np.all(w[0::2] <= 0) and np.all(w[1::2] >= 0)
+
+
+# -------------------------------------------------------------------- framing
+@pytest.mark.parametrize("fs,size,rate,skip,nz", [(2.4e6, 65536, 15, 94464, 65536), (10e6, 1 << 20, 10, 0, 1000000),
+                                                  (61.44e6, 65536, 937.5, 0, 65536), (10e6, 1 << 20, 15, 0, 666667)])
+def test_reshape_params(fs, size, rate, skip, nz):
+    assert oracle.gen_reshape_params(fs, size, rate) == (skip, nz)
+    assert dsp.gen_reshape_params(fs, size, rate) == (skip, nz)
+
+
+# ----------------------------------------------------------------------- taps
+def test_taps_vs_golden_and_counts():
+    g = np.load(GOLDEN + "/taps.npz")
+    cases = {"vfo_lpf_91": (100000.0, 10000.0, 240000.0), "wfm_audio_228": (15000.0, 4000.0, 240000.0),
+             "c3_256": (3.0e6, 912000.0, 61.44e6)}
+    for k, args in cases.items():
+        o = oracle.low_pass(*args)
+        assert len(o) == int(k.split("_")[-1])
+        np.testing.assert_array_equal(_bits(o), _bits(g[k]))
+        np.testing.assert_array_equal(_bits(dsp.low_pass(*args)), _bits(o))
+    r = oracle.RationalResampler(240000, 48000, False).info()
+    assert (r["predec"], r["interp"], r["decim"], r["ntaps"]) == (4, 4, 5, 380)
+
+
+@pytest.mark.parametrize("fn,args", [("high_pass", (300.0, 100.0, 48000.0)), ("band_pass", (300.0, 6250.0, 100.0, 48000.0)),
+                                     ("low_pass", (12500.0, 1250.0, 48000.0, True))])
+def test_product_taps_bit_exact(fn, args):
+    np.testing.assert_array_equal(_bits(getattr(dsp, fn)(*args)), _bits(getattr(oracle, fn)(*args)))
+
+
+def test_complex_band_pass_pilot():
+    a = dsp.band_pass(18750.0, 19250.0, 3000.0, 240000.0, True, True)
+    b = oracle.band_pass(18750.0, 19250.0, 3000.0, 240000.0, True, True)
+    assert len(a) == 305   # 304 -> odd forced (broadcast_fm.h:34)
+    np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_decim_plans():
+    # multirate/decim/plans.h: plan_256 = {32:143, 4:27, 2:69}; both sides read the same data
+    assert [(d, len(t)) for d, t in oracle.decim_plan(256)] == [(32, 143), (4, 27), (2, 69)]
+    for ratio in [2 << i for i in range(13)]:
+        a, b = oracle.decim_plan(ratio), dsp.decim_plan(ratio)
+        assert [d for d, _ in a] == [d for d, _ in b]
+        prod = 1
+        for (d, t1), (_, t2) in zip(a, b):
+            np.testing.assert_array_equal(t1, t2)
+            prod *= d
+        assert prod == ratio
+        # every stage is a lowpass with ~unity DC gain (the generated tables are within a few %)
+        for _, t in a:
+            assert abs(float(t.astype(np.float64).sum()) - 1.0) < 0.05
+
+
+# ----------------------------------------------------------------- converters
+def test_converters_oracle_vs_golden():
+    g = np.load(GOLDEN + "/converters.npz")
+    np.testing.assert_array_equal(_bits(oracle.convert(0, np.arange(256, dtype=np.uint8))), _bits(g["u8"]))
+    np.testing.assert_array_equal(_bits(oracle.convert(1, np.arange(-32768, 32768, dtype=np.int16))), _bits(g["i16"]))
+
+
+def test_u8_division_is_not_reciprocal_multiply():
+    # 126 of 256 u8 codes differ between x/127.5f and x*(1/127.5f): bit-exact means true division
+    x = (np.arange(256, dtype=np.int32) - 128).astype(np.float32) + np.float32(0.5)
+    div = x / np.float32(127.5)
+    mul = x * np.float32(1.0 / 127.5)
+    assert int(np.sum(div.view(np.uint32) != mul.view(np.uint32))) == 126
+    np.testing.assert_array_equal(_bits(oracle.convert(0, np.arange(256, dtype=np.uint8))), _bits(div))
+
+
+def test_u8_roundtrip_recorder_encoder():
+    # recorder u8 encoder (utils/wav.cpp:301) maps every decoded u8 back to its code
+    f = oracle.convert(0, np.arange(256, dtype=np.uint8)).astype(np.float64)
+    back = np.clip(np.round(f * 127.5 + 127.5 - 0.5), 0, 255).astype(np.int64)
+    np.testing.assert_array_equal(back, np.arange(256))
+
+
+def test_i24_sign_extension():
+    v = np.array([-(1 << 23), -1, 0, 1, (1 << 23) - 1], dtype=np.int64)
+    b = np.stack([v & 0xff, (v >> 8) & 0xff, (v >> 16) & 0xff], axis=1).astype(np.uint8).ravel()
+    want = ((v.astype(np.float32) + np.float32(0.5)) / np.float32(8388607.5)).astype(np.float32)
+    np.testing.assert_array_equal(_bits(oracle.convert(2, b)), _bits(want))
+
+
+# ----------------------------------------------------------------- spectrum
+def test_oracle_fft_fp32_vs_fp64():
+    rng = np.random.default_rng(1)
+    N = 4096
+    x = (rng.uniform(-1, 1, N) + 1j * rng.uniform(-1, 1, N)).astype(np.complex64)
+    out = np.empty(2 * N, dtype=np.float32)
+    oracle.lib.orc_fft_c2c(oracle._p(x.view(np.float32)), oracle._p(out), N)
+    X = out.view(np.complex64)
+    ref = np.fft.fft(x.astype(np.complex128))
+    assert np.linalg.norm(X - ref) / np.linalg.norm(ref) < 2 * EPS32 * np.log2(N)
+
+
+def test_oracle_spectrum_aes17_fixture():
+    g = np.load(GOLDEN + "/fft_aes17.npz")
+    N = int(g["N"])
+    db = oracle.fft_logmag(g["x"], N, N, oracle.create_window(6, N))
+    truth = 10 * np.log10(np.maximum(g["power_f64"], 1e-300))
+    sel = truth > truth.max() - 60
+    assert np.abs(db[sel] - truth[sel]).max() < 1e-3
+    # the AES17 0 dBFS tone at fs/16 lands at bin N/2 + N/16 (centred spectrum)
+    assert int(np.argmax(db)) == N // 2 + N // 16
+
+
+# --------------------------------------------------------------------- FIR
+def test_oracle_fir_vs_numpy_correlation():
+    rng = np.random.default_rng(2)
+    taps = rng.standard_normal(57).astype(np.float32)
+    x = (rng.standard_normal(5000) + 1j * rng.standard_normal(5000)).astype(np.complex64)
+    y = oracle.FIR(taps, 3).process(x)
+    buf = np.concatenate([np.zeros(56, np.complex128), x.astype(np.complex128)])
+    full = np.correlate(buf, taps.astype(np.float64), mode="valid")[:len(x)]
+    np.testing.assert_allclose(y, full[::3].astype(np.complex64), rtol=0, atol=1e-5)
+
+
+def test_oracle_fir_c3_fixture():
+    g = np.load(GOLDEN + "/fir_c3.npz")
+    taps = np.load(GOLDEN + "/taps.npz")["c3_256"]
+    y = oracle.FIR(taps, 8).process(g["x"])
+    np.testing.assert_array_equal(y.view(np.uint32), g["y"].view(np.uint32))
+
+
+def test_oracle_fir_block_split_invariance():
+    rng = np.random.default_rng(3)
+    taps = rng.standard_normal(143).astype(np.float32)
+    x = (rng.standard_normal(20000) + 1j * rng.standard_normal(20000)).astype(np.complex64)
+    a = oracle.FIR(taps, 32).process(x)
+    f = oracle.FIR(taps, 32)
+    parts = [f.process(p) for p in np.split(x, [7, 100, 5000, 5001, 12345])]
+    np.testing.assert_array_equal(np.concatenate(parts).view(np.uint32), a.view(np.uint32))
+
+
+def test_oracle_polyphase_matches_upsample_filter_decimate():
+    rng = np.random.default_rng(4)
+    interp, decim = 4, 5
+    taps = oracle.low_pass(0.1, 0.02, 1.0) * np.float32(interp)
+    x = rng.standard_normal(3000).astype(np.float32)
+    y = oracle.PolyphaseResampler(interp, decim, taps, complex_data=False).process(x)
+    # reference model: zero-stuff, convolve (bank reversal == convolution), keep every decim-th
+    up = np.zeros(len(x) * interp)
+    up[::interp] = x
+    full = np.convolve(up, taps.astype(np.float64))[:len(up)]
+    tpp = (len(taps) + interp - 1) // interp
+    shift = (interp - 1) - (tpp * interp - 1)   # bank alignment of polyphase_bank.h
+    want = np.array([full[m * decim - shift] if 0 <= m * decim - shift < len(full) else 0.0 for m in range(len(y))])
+    assert np.abs(y[50:] - want[50:]).max() < 1e-4
+
+
+def test_oracle_quadrature_tone():
+    fs = 240000.0
+    t = np.arange(48000) / fs
+    ph = 2 * np.pi * 75e3 * np.cumsum(np.sin(2 * np.pi * 1e3 * t)) / fs
+    y = oracle.Quadrature(2 * np.pi * 100e3 / fs).process(np.exp(1j * ph).astype(np.complex64))
+    assert abs(y[100:].max() - 0.75) < 2e-3
+
+
+def test_oracle_xlator_shifts_tone_to_dc():
+    fs, f0 = 1e6, 123456.0
+    n = np.arange(10000)
+    x = np.exp(2j * np.pi * f0 * n / fs).astype(np.complex64)
+    y = oracle.Xlator(2 * np.pi * (-f0 / fs)).process(x)
+    assert np.abs(y - y[0]).max() < 1e-4 and abs(y[0] - 1) < 1e-6
+
+
+def test_oracle_vfo_output_rate():
+    v = oracle.RxVFO(61.44e6, 240000, 200000, 2.5e6)
+    x = np.zeros(307200, np.complex64)
+    assert len(v.process(x)) == 1200
+
+
+def test_oracle_compression_roundtrip():
+    rng = np.random.default_rng(5)
+    x = (rng.uniform(-1, 1, 4096) + 1j * rng.uniform(-1, 1, 4096)).astype(np.complex64)
+    buf = np.zeros(8 + 8 * 4096, np.uint8)
+    for t, tol in [(2, 0.0), (1, 1.0 / 32768 * 2), (0, 1.0 / 128 * 2)]:
+        nb = oracle.lib.orc_compress(t, oracle._p(x.view(np.float32)), 4096, oracle._p(buf))
+        y = np.zeros(4096, np.complex64)
+        m = oracle.lib.orc_decompress(oracle._p(buf), nb, oracle._p(y.view(np.float32)))
+        assert m == 4096
+        assert np.abs(y - x).max() <= tol + 1e-7
+
+
+def test_oracle_agc_and_am_ssb_run():
+    rng = np.random.default_rng(6)
+    x = (rng.uniform(-1, 1, 4800) + 1j * rng.uniform(-1, 1, 4800)).astype(np.complex64) * np.float32(0.01)
+    assert len(oracle.AM(1, 10000, 50.0 / 48000, 5.0 / 48000, 10.0 / 48000, 48000).process(x)) == 4800
+    y = oracle.SSB(0, 2800, 48000, True, 50.0 / 48000, 5.0 / 48000).process(x)
+    assert len(y) == 4800 and np.isfinite(y).all()

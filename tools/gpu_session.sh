@@ -23,3 +23,13 @@ if [ "${PROFILE:-1}" == "1" ]; then
   done
 fi
 echo "done $(date)" >> "$OUT/${TAG}_status.txt"
+# PMC passes (separate runs, kernel-trace only): HBM traffic per kernel
+if [ "${PMC:-0}" == "1" ]; then
+  for cfg in ${PROF_CFGS:-c5}; do
+    for ctr in FETCH_SIZE WRITE_SIZE; do
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$OUT/${TAG}_pmc_${cfg}_$ctr" -o run -- python3 "$R/bench.py" --config $cfg --steps 3 --warmup 1 --no-cpu > "$OUT/${TAG}_pmc_${cfg}_$ctr.log" 2>&1)
+      rc=$?; echo "pmc $cfg $ctr rc=$rc" >> "$OUT/${TAG}_status.txt"; fatal $rc pmc_$cfg
+    done
+  done
+fi
+echo "all done $(date)" >> "$OUT/${TAG}_status.txt"
