@@ -170,16 +170,26 @@ def main():
         gather_bufs = [torch.empty_like(src) for _ in range(world)] if rank == 0 else None
 
     ev = []
+    # The spectrum path and the VFO chain are independent consumers of the same IQ (the
+    # reference runs them on separate block threads, iq_frontend.cpp:49,115): run them on two
+    # HIP streams forked from / joined to the step stream so their kernels overlap.
+    s_fft, s_vfo = torch.cuda.Stream(), torch.cuda.Stream()
 
     def step(timed):
+        fork = torch.cuda.Event()
+        fork.record(stream)
+        s_fft.wait_event(fork)
+        s_vfo.wait_event(fork)
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        wl.dominant(x, s)
+            e0.record(s_fft)
+        wl.dominant(x, s_fft.cuda_stream)
         if timed:
-            e1.record(stream)
+            e1.record(s_fft)
             ev.append((e0, e1))
-        wl.rest(x, s)
+        wl.rest(x, s_vfo.cuda_stream)
+        stream.wait_stream(s_fft)
+        stream.wait_stream(s_vfo)
         if world > 1:
             dist.gather(wl.gather_src(), gather_bufs, dst=0)
 

@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
     const int tile = blockIdx.x;
     const int mFirst = tile * a.TMS - QOFF;                    // output of local index 0
     const long long b0 = (long long)a.offset0 + (long long)mFirst * a.D;
-    const int rows = TM + a.Q;                                   // + 1 prefetch row
+    const int rows = TM + a.Q + K;                               // padded taps + prefetch rows
     const int span = rows * a.D;
     const DT* hist = reinterpret_cast<const DT*>(a.hist);
     const DT* in = reinterpret_cast<const DT*>(a.in);
@@ -145,23 +145,31 @@ __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
 #pragma unroll
     for (int i = 0; i < K; i++) acc[i] = zero_of<DT>();
     const int l = tid;
+    // a.Q is padded to a multiple of QC with zero taps: each chunk loads QC taps with one
+    // wave-uniform (scalar) load and issues its QC row reads before the first FMA, so the
+    // loop waits once per chunk instead of once per tap.
+    constexpr int QC = 8;
     for (int p = 0; p < a.D; p++) {
         const DT* Xp = X + p * a.RSP;
         const TT* __restrict__ Hp = taps + p * a.Q;
         DT w[K];
 #pragma unroll
         for (int i = 0; i < K; i++) w[i] = Xp[i * a.RSK + l];   // rows l*K + i
-        for (int q0 = 0; q0 < a.Q; q0 += K) {
+        for (int q0 = 0; q0 < a.Q; q0 += QC) {
+            TT hv[QC];
+            DT nx[QC];
 #pragma unroll
-            for (int u = 0; u < K; u++) {
-                const int q = q0 + u;
-                if (q < a.Q) {
-                    const TT h = Hp[q];
+            for (int u = 0; u < QC; u++) hv[u] = Hp[q0 + u];
 #pragma unroll
-                    for (int i = 0; i < K; i++) mac(acc[i], w[(i + u) % K], h);
-                    const int rn = l * K + K + q;                 // next row for this slot
-                    w[u] = Xp[(rn % K) * a.RSK + rn / K];
-                }
+            for (int u = 0; u < QC; u++) {
+                const int rn = l * K + K + q0 + u;                // row entering slot (q0 + u) % K
+                nx[u] = Xp[(rn % K) * a.RSK + rn / K];
+            }
+#pragma unroll
+            for (int u = 0; u < QC; u++) {
+#pragma unroll
+                for (int i = 0; i < K; i++) mac(acc[i], w[(i + u) % K], hv[u]);
+                w[u % K] = nx[u];
             }
         }
     }
@@ -409,6 +417,7 @@ struct FirBlock : Block {
     int upload_taps() {
         SDRGPU_HIP(hipSetDevice(device));
         Q = (ntaps + D - 1) / D;
+        Q = (Q + 7) / 8 * 8;      // kernel chunk QC = 8 (zero taps past ntaps)
         const int e = ttype == SDRGPU_C64 ? 2 : 1;
         std::vector<float> pq((size_t)D * Q * e, 0.0f);
         for (int p = 0; p < D; p++)
@@ -431,9 +440,10 @@ struct FirBlock : Block {
         return SDRGPU_OK;
     }
     int choose_k() const {
-        // register blocking pays when a row feeds several taps per phase (Q large)
-        if (Q >= 16) return 4;
-        if (Q >= 6) return 2;
+        // register blocking pays when a row feeds several taps per phase (unpadded Q large)
+        const int Qr = (ntaps + D - 1) / D;
+        if (Qr >= 16) return 4;
+        if (Qr >= 6) return 2;
         return 1;
     }
     int NT = 256;
@@ -464,17 +474,23 @@ struct FirBlock : Block {
             size_t es = esize(in_dtype);
             size_t lds = 0;
             int RSK = 0, RSP = 0;
-            NT = 256;
-            for (;;) {
-                const int TM = NT * K;
-                const int rows = TM + Q + K;
-                RSK = (rows + K - 1) / K;
-                RSP = K * RSK + 1;
-                lds = es * (size_t)D * RSP;
-                if (lds <= 150 * 1024) break;
-                if (K > 1) K /= 2;
-                else if (NT > 64) NT /= 2;
-                else break;
+            // prefer a tile that leaves room for two workgroups per CU (<= 76 KB), else <= 150 KB
+            const int K0 = K;
+            for (size_t cap : {(size_t)76 * 1024, (size_t)150 * 1024}) {
+                K = K0;
+                NT = 256;
+                for (;;) {
+                    const int TM = NT * K;
+                    const int rows = TM + Q + 2 * K;
+                    RSK = (rows + K - 1) / K;
+                    RSP = K * RSK + 1;
+                    lds = es * (size_t)D * RSP;
+                    if (lds <= cap) break;
+                    if (K > 1) K /= 2;
+                    else if (NT > 64) NT /= 2;
+                    else break;
+                }
+                if (lds <= cap) break;
             }
             if (lds > 150 * 1024) {
                 set_error("fir: tile does not fit LDS (ntaps %d, decim %d)", ntaps, D);
