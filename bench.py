@@ -28,6 +28,7 @@ import torch.distributed as dist  # noqa: E402
 
 import sdrpp_amd  # noqa: E402
 from sdrpp_amd import dsp  # noqa: E402
+from sdrpp_amd.multistream import StreamShard  # noqa: E402
 
 METRIC = "IQ Msamples/s through FFT+FIR+demod chain; % HBM roofline at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
@@ -50,11 +51,11 @@ class C5:
     N = 65536
     FS = 61.44e6
 
-    def __init__(self, B, rank, dev):
+    def __init__(self, B, shard, dev):
         self.B = (B // self.N) * self.N
         self.frames = self.B // self.N
         self.fft = dsp.FFTSpectrum(self.N, self.N, 6, device=dev)
-        self.vfo = dsp.RxVFO(self.FS, 240000, 200000, 2.5e6 + 1e5 * rank, device=dev)
+        self.vfo = dsp.RxVFO(self.FS, 240000, 200000, shard.vfo_offset(), device=dev)
         self.wfm = dsp.BroadcastFM(100000, 240000, True, device=dev)
         self.spectra = torch.empty(self.frames * self.N, dtype=torch.float32, device="cuda")
         self.ifbuf = torch.empty(2 * (self.B // 256 + 64), dtype=torch.float32, device="cuda")
@@ -79,7 +80,7 @@ class C2:
     N = 1 << 20
     NZ = 1000000
 
-    def __init__(self, B, rank, dev):
+    def __init__(self, B, shard, dev):
         self.frames = max(1, B // self.NZ)
         self.B = self.frames * self.NZ
         self.fft = dsp.FFTSpectrum(self.N, self.NZ, 6, device=dev)
@@ -102,7 +103,7 @@ class C3:
     """FrequencyXlator(-1.5 MHz) -> 256-tap DecimatingFIR /8 -> Quadrature(100 kHz), fused kernel."""
     FS = 61.44e6
 
-    def __init__(self, B, rank, dev):
+    def __init__(self, B, shard, dev):
         self.B = B
         taps = dsp.low_pass(3.0e6, 912000.0, self.FS)
         w = 2 * np.pi * (-1.5e6 / self.FS)
@@ -140,15 +141,22 @@ def cpu_baseline(seconds):
     return n / dt / 1e6, n, dt
 
 
+def traffic_per_sample(config):
+    """HBM bytes per input sample of the dominant launch group, from the committed rocprofv3
+    PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/pmc_traffic.py)."""
+    path = os.path.join(ROOT, "profiles", "r1", f"{config}_pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        return float(d["bytes_per_sample"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
+    shard = StreamShard(backend="nccl")
+    world, rank = shard.world, shard.rank
+    if world == 1:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
     # one explicit non-default stream for every kernel of the step (libsdrgpu treats a NULL
@@ -157,22 +165,20 @@ def main():
     B = 1 << a.log2_batch
     if a.config == "c2":
         B = 256 * 1000000
-    wl = {"c5": C5, "c2": C2, "c3": C3}[a.config](B, rank, dev)
+    wl = {"c5": C5, "c2": C2, "c3": C3}[a.config](B, shard, dev)
     B = wl.B
     g = torch.Generator(device="cuda")
-    g.manual_seed(0xACE1 + rank)
+    g.manual_seed(shard.seed())
     x = (torch.rand(2 * B, device="cuda", generator=g) * 2 - 1).contiguous()   # complex_t interleaved
     stream = torch.cuda.current_stream()
-    s = stream.cuda_stream
     gather_bufs = None
-    if world > 1:
-        src = wl.gather_src()
-        gather_bufs = [torch.empty_like(src) for _ in range(world)] if rank == 0 else None
+    if world > 1 and rank == 0:
+        gather_bufs = [torch.empty_like(wl.gather_src()) for _ in range(world)]
 
     ev = []
     # The spectrum path and the VFO chain are independent consumers of the same IQ (the
     # reference runs them on separate block threads, iq_frontend.cpp:49,115): run them on two
-    # HIP streams forked from / joined to the step stream so their kernels overlap.
+    # HIP streams forked from / joined to the step stream so their kernels may overlap.
     s_fft, s_vfo = torch.cuda.Stream(), torch.cuda.Stream()
 
     def step(timed):
@@ -191,30 +197,26 @@ def main():
         stream.wait_stream(s_fft)
         stream.wait_stream(s_vfo)
         if world > 1:
-            dist.gather(wl.gather_src(), gather_bufs, dst=0)
+            shard.gather_spectra(wl.gather_src(), gather_bufs)
 
     for _ in range(a.warmup):
         step(False)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    shard.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step(True)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    shard.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / max(len(ev), 1)
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms = shard.max_over_ranks([elapsed, kern_ms], device="cuda")
 
     if rank == 0:
         total = world * B * a.steps
         value = total / elapsed / 1e6
         achieved = wl.kernel_bytes / (kern_ms * 1e-3) / 1e9
+        tps = traffic_per_sample(a.config)
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "MS/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
@@ -226,7 +228,8 @@ def main():
                        "samples_per_gpu_per_step": B, "parallelism": f"replica-streams x{world}",
                        "bytes_per_sample": round(wl.bytes_per_sample, 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": round(tps * B) if tps else None,
                          "kernel": wl.kernel_name, "kernel_ms": round(kern_ms, 4)},
             "chain_hbm_GBs": round(wl.bytes_per_sample * value * 1e6 / world / 1e9, 1),
         }
@@ -236,8 +239,7 @@ def main():
                                    "sample": f"oracle C port of the same C5 chain (fp32, VOLK-style rotator/dots), "
                                              f"{n} samples in 1M blocks, {dt:.1f} s on 1 host core"}
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    shard.close()
 
 
 if __name__ == "__main__":

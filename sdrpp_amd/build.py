@@ -60,8 +60,12 @@ def build_lib(force=False):
 
 
 def build_oracle():
+    """The checker (test infrastructure): the C restatement, and -- where the reference tree is
+    mounted (dev container only) -- oracle/_ref/ref_probe built from the reference's own headers."""
     odir = os.path.join(ROOT, "oracle")
     _run(["make", "-C", odir, "-s"])
+    if os.path.isdir("/root/reference/core/src/dsp"):
+        _run(["make", "-C", odir, "-s", "ref"])
     return os.path.join(odir, "libsdr_oracle.so")
 
 

@@ -1,0 +1,57 @@
+"""Multi-GPU layer of the streaming-DSP path: one independent IQ stream per GPU.
+
+SDR++ has no multi-device code; independent IQ streams (one SDR per
+GPU) shard with no per-sample exchange. The only collective is a rank-0 gather of the
+latest spectra for display (RCCL over xGMI via torch.distributed "nccl"; "gloo" on CPU for
+tests). Timing is the max over ranks.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class StreamShard:
+    """Rank/world bookkeeping for stream-per-GPU sharding."""
+
+    def __init__(self, backend=None):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.backend = backend
+        if self.world > 1 and not dist.is_initialized():
+            if backend == "nccl":
+                torch.cuda.set_device(self.local)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            else:
+                dist.init_process_group(backend or "gloo")
+
+    # stream parameters of this rank's SDR: a distinct seed and VFO offset per stream
+    def seed(self, base=0xACE1):
+        return base + self.rank
+
+    def vfo_offset(self, base=2.5e6, step=1e5):
+        return base + step * self.rank
+
+    def gather_spectra(self, local_rows, out_list=None):
+        """Gather every rank's latest spectra rows to rank 0 (list indexed by rank there)."""
+        if self.world == 1:
+            return [local_rows]
+        if self.rank == 0 and out_list is None:
+            out_list = [torch.empty_like(local_rows) for _ in range(self.world)]
+        dist.gather(local_rows, out_list if self.rank == 0 else None, dst=0)
+        return out_list if self.rank == 0 else None
+
+    def max_over_ranks(self, values, device=None):
+        t = torch.tensor(values, dtype=torch.float64, device=device)
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(v) for v in t]
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def close(self):
+        if self.world > 1 and dist.is_initialized():
+            dist.destroy_process_group()
