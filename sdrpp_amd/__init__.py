@@ -12,7 +12,8 @@ import os
 __all__ = ["lib", "LIB_PATH", "check", "SdrGpuError"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsdrgpu.so")
+# SDRGPU_LIB_PATH: load another build of the same ABI (A/B timing of two builds on one box)
+LIB_PATH = os.environ.get("SDRGPU_LIB_PATH") or os.path.join(_HERE, "lib", "libsdrgpu.so")
 
 F32, C64 = 0, 1
 WIN_RECTANGULAR, WIN_HAMMING, WIN_HANN, WIN_BLACKMAN, WIN_NUTTALL, WIN_BH4, WIN_BH7 = range(7)

@@ -70,144 +70,209 @@ struct FirArgs {
     const float2* plo;  // XL: fine phasors
     int ntaps, H, count, D, Q, offset0, M, TMS, RSK, RSP;
     int dshift;         // log2(D) when D is a power of two, else -1
+    int ntiles;         // tiles of TMS outputs (persistent grid walks them)
+    int tapsLdsOff;     // TL: byte offset of the [D][Q] taps in dynamic LDS
     float invDev;
 };
 
-template <typename DT, typename TT, int K, bool XL, bool QUAD, bool STEREO>
+// Persistent, software-pipelined FIR tile loop. Workgroup g walks tiles g, g + G, ...; the
+// input span of its next tile is loaded into registers (PF elements per thread) while the
+// current tile is computed from LDS, so HBM latency hides behind the dot products instead
+// of serialising load -> barrier -> compute per tile. Spans longer than
+// PF * NT (very large decimations) load their remainder synchronously at commit time.
+template <typename DT, bool XL>
+__device__ __forceinline__ DT fir_fetch(const FirArgs& a, long long b) {
+    // element b of [hist (H) || in (count)] with zero outside; hist is stored translated
+    const DT* hist = reinterpret_cast<const DT*>(a.hist);
+    const DT* in = reinterpret_cast<const DT*>(a.in);
+    DT x = zero_of<DT>();
+    if (b >= 0) {
+        if (b < a.H) x = hist[b];
+        else if (b - a.H < a.count) x = in[b - a.H];
+    }
+    return x;
+}
+
+template <typename DT, typename TT, int K, bool XL, bool QUAD, bool STEREO, bool TL>
 __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
+    constexpr int PF = sizeof(DT) == 8 ? 36 : 40;   // prefetch slots per thread
     const int NT = blockDim.x;       // 64, 128 or 256 (host picks the largest tile that fits LDS)
     const int TM = NT * K;
     constexpr int QOFF = QUAD ? 1 : 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     DT* X = reinterpret_cast<DT*>(smem);
+    __shared__ float2 lastY[QUAD ? 256 : 1];
 
-    const int tid = threadIdx.x;
-    const int tile = blockIdx.x;
-    const int mFirst = tile * a.TMS - QOFF;                    // output of local index 0
-    const long long b0 = (long long)a.offset0 + (long long)mFirst * a.D;
+    int tid = threadIdx.x;
     const int rows = TM + a.Q + K;                               // padded taps + prefetch rows
     const int span = rows * a.D;
-    const DT* hist = reinterpret_cast<const DT*>(a.hist);
     const DT* in = reinterpret_cast<const DT*>(a.in);
-    const TT* __restrict__ taps = reinterpret_cast<const TT*>(a.taps);   // wave-uniform reads -> scalar loads
+    // Taps: TL -> copied once per (persistent) workgroup behind the span in LDS and read with
+    // wave-uniform (broadcast) LDS loads; else wave-uniform global reads (tap sets too large
+    // for LDS). Global reads inside the tile loop cannot become scalar loads -- the loop's
+    // output stores may alias them -- and a vector load there would wait on the prefetch.
+    const TT* __restrict__ taps = reinterpret_cast<const TT*>(a.taps);
+    if constexpr (TL) {
+        TT* tl = reinterpret_cast<TT*>(smem + a.tapsLdsOff);
+        for (int i = threadIdx.x; i < a.D * a.Q; i += NT) tl[i] = taps[i];
+        taps = tl;                                                // (barrier: first commit's)
+    }
+    int tile = blockIdx.x;
+    if (tile >= a.ntiles) return;
 
-    // input span -> LDS (phase-major, row-swizzled). Loads are issued UNR at a time into
-    // registers before any LDS store so HBM latency overlaps; interior tiles (span fully
-    // inside `in`) take a branch-free path.
-    const bool interior = (b0 >= a.H) && (b0 + span <= (long long)a.H + a.count);
-    constexpr int UNR = 8;
-    for (int s0 = tid; s0 < span; s0 += UNR * NT) {
-        DT v[UNR];
-        if (interior) {
+    auto base = [&](int t) { return (long long)a.offset0 + (long long)(t * a.TMS - QOFF) * a.D; };
+    auto is_interior = [&](long long b0) { return (b0 >= a.H) && (b0 + span <= (long long)a.H + a.count); };
+    auto lds_put = [&](int sx, DT v) {
+        int p, r;
+        if (a.dshift >= 0) {
+            p = sx & (a.D - 1);
+            r = sx >> a.dshift;
+        } else {
+            r = sx / a.D;
+            p = sx - r * a.D;
+        }
+        X[p * a.RSP + (r % K) * a.RSK + r / K] = v;   // phase-major, row-swizzled
+    };
+
+    // Interior tiles (span entirely inside `in`) are prefetched; the few boundary tiles of a
+    // call (history / tail) are fetched synchronously at commit.
+    DT pf[PF];
+    bool pfValid = false;
+    auto issue = [&](int t) {
+        const long long b0 = base(t);
+        pfValid = is_interior(b0);
+        if (pfValid) {
+            const DT* __restrict__ src = in + (b0 - a.H);
 #pragma unroll
-            for (int u = 0; u < UNR; u++) {
-                const int sc = min(s0 + u * NT, span - 1);        // clamp keeps the load in bounds
-                const long long i = b0 + sc - a.H;
-                v[u] = in[i];
-                if constexpr (XL) v[u] = cmulf(v[u], nco_tab(a.phi, a.plo, i));
+            for (int u = 0; u < PF; u++) {
+                const int sx = tid + u * NT;
+                if (sx < span) pf[u] = src[sx];
+            }
+        }
+    };
+    auto xl_apply = [&](DT v, long long b) {
+        if constexpr (XL) {
+            if (b >= a.H && b - a.H < a.count) v = cmulf(v, nco_tab(a.phi, a.plo, b - a.H));
+        }
+        return v;
+    };
+    auto commit = [&](int t) {
+        const long long b0 = base(t);
+        int sx0 = tid;
+        if (pfValid) {
+            if constexpr (XL) {
+                // interior: every element is from `in`. NCO table reads in groups of 8 so
+                // the table latency is paid once per group, not once per element
+                const long long i0 = b0 - a.H;
+#pragma unroll
+                for (int g = 0; g < PF; g += 8) {
+                    float2 ph[8];
+#pragma unroll
+                    for (int u = 0; u < 8 && g + u < PF; u++) {
+                        const int sx = min(tid + (g + u) * NT, span - 1);
+                        ph[u] = nco_tab(a.phi, a.plo, i0 + sx);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8 && g + u < PF; u++) {
+                        const int sx = tid + (g + u) * NT;
+                        if (sx < span) lds_put(sx, cmulf(pf[g + u], ph[u]));
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < PF; u++) {
+                    const int sx = tid + u * NT;
+                    if (sx < span) lds_put(sx, pf[u]);
+                }
+            }
+            sx0 = tid + PF * NT;                                   // remainder (rare: huge decimations)
+        }
+        for (int sx = sx0; sx < span; sx += NT) lds_put(sx, xl_apply(fir_fetch<DT, XL>(a, b0 + sx), b0 + sx));
+    };
+
+    const int l = tid;
+    float2 din0 = make_float2(0.f, 0.f);
+    if constexpr (QUAD) din0 = a.din[0];
+    issue(tile);
+    for (;;) {
+        // re-materialise the thread index each tile: keeps the compiler from hoisting the PF
+        // per-slot global/LDS addresses out of the loop (that costs ~2 PF live registers)
+        asm volatile("" : "+v"(tid));
+        commit(tile);
+        __syncthreads();
+        const int next = tile + gridDim.x;
+        if (next < a.ntiles) issue(next);                      // in flight during the dot products
+
+        DT acc[K];
+#pragma unroll
+        for (int i = 0; i < K; i++) acc[i] = zero_of<DT>();
+        // a.Q is padded to a multiple of QC with zero taps: each chunk loads QC taps with one
+        // wave-uniform (scalar) load and issues its QC row reads before the first FMA, so the
+        // loop waits once per chunk instead of once per tap.
+        constexpr int QC = 8;
+        for (int p = 0; p < a.D; p++) {
+            const DT* Xp = X + p * a.RSP;
+            const TT* __restrict__ Hp = taps + p * a.Q;
+            DT w[K];
+#pragma unroll
+            for (int i = 0; i < K; i++) w[i] = Xp[i * a.RSK + l];   // rows l*K + i
+            for (int q0 = 0; q0 < a.Q; q0 += QC) {
+                TT hv[QC];
+                DT nx[QC];
+#pragma unroll
+                for (int u = 0; u < QC; u++) hv[u] = Hp[q0 + u];
+#pragma unroll
+                for (int u = 0; u < QC; u++) {
+                    const int rn = l * K + K + q0 + u;                // row entering slot (q0 + u) % K
+                    nx[u] = Xp[(rn % K) * a.RSK + rn / K];
+                }
+#pragma unroll
+                for (int u = 0; u < QC; u++) {
+#pragma unroll
+                    for (int i = 0; i < K; i++) mac(acc[i], w[(i + u) % K], hv[u]);
+                    w[u % K] = nx[u];
+                }
+            }
+        }
+
+        const int mFirst = tile * a.TMS - QOFF;                    // output of local index 0
+        if constexpr (QUAD) {
+            // FM quadrature (demod/quadrature.h:41-56): out = arg(y[m] * conj(y[m-1])) / dev
+            lastY[l] = acc[K - 1];
+            __syncthreads();
+            float* out = reinterpret_cast<float*>(a.out);
+#pragma unroll
+            for (int i = 0; i < K; i++) {
+                const int m = mFirst + l * K + i;
+                if (m >= 0 && m >= tile * a.TMS && m < a.M) {
+                    float2 prev;
+                    if (m == 0) prev = din0;
+                    else if (i > 0) prev = acc[i - 1];
+                    else prev = lastY[l - 1];
+                    const float2 y = acc[i];
+                    const float br = prev.x, bi = -prev.y;
+                    const float re = (y.x * br) - (y.y * bi);
+                    const float im = (y.y * br) + (y.x * bi);
+                    out[m] = atan2f(im, re) * a.invDev;
+                    if (m == a.M - 1) a.dinNext[0] = y;
+                }
             }
         } else {
 #pragma unroll
-            for (int u = 0; u < UNR; u++) {
-                const long long b = b0 + s0 + u * NT;
-                DT x = zero_of<DT>();
-                if (s0 + u * NT < span && b >= 0) {
-                    if (b < a.H) {
-                        x = hist[b];
-                    } else if (b - a.H < a.count) {
-                        const long long i = b - a.H;
-                        x = in[i];
-                        if constexpr (XL) x = cmulf(x, nco_tab(a.phi, a.plo, i));
+            for (int i = 0; i < K; i++) {
+                const int m = mFirst + l * K + i;
+                if (m < a.M && m < (tile + 1) * a.TMS) {
+                    if constexpr (STEREO) {
+                        reinterpret_cast<float2*>(a.out)[m] = make_float2(acc[i], acc[i]);   // LRToStereo(l = r)
+                    } else {
+                        reinterpret_cast<DT*>(a.out)[m] = acc[i];
                     }
                 }
-                v[u] = x;
             }
         }
-#pragma unroll
-        for (int u = 0; u < UNR; u++) {
-            const int sx = s0 + u * NT;
-            if (sx < span) {
-                int p, r;
-                if (a.dshift >= 0) {
-                    p = sx & (a.D - 1);
-                    r = sx >> a.dshift;
-                } else {
-                    r = sx / a.D;
-                    p = sx - r * a.D;
-                }
-                X[p * a.RSP + (r % K) * a.RSK + r / K] = v[u];
-            }
-        }
-    }
-    __syncthreads();
-
-    DT acc[K];
-#pragma unroll
-    for (int i = 0; i < K; i++) acc[i] = zero_of<DT>();
-    const int l = tid;
-    // a.Q is padded to a multiple of QC with zero taps: each chunk loads QC taps with one
-    // wave-uniform (scalar) load and issues its QC row reads before the first FMA, so the
-    // loop waits once per chunk instead of once per tap.
-    constexpr int QC = 8;
-    for (int p = 0; p < a.D; p++) {
-        const DT* Xp = X + p * a.RSP;
-        const TT* __restrict__ Hp = taps + p * a.Q;
-        DT w[K];
-#pragma unroll
-        for (int i = 0; i < K; i++) w[i] = Xp[i * a.RSK + l];   // rows l*K + i
-        for (int q0 = 0; q0 < a.Q; q0 += QC) {
-            TT hv[QC];
-            DT nx[QC];
-#pragma unroll
-            for (int u = 0; u < QC; u++) hv[u] = Hp[q0 + u];
-#pragma unroll
-            for (int u = 0; u < QC; u++) {
-                const int rn = l * K + K + q0 + u;                // row entering slot (q0 + u) % K
-                nx[u] = Xp[(rn % K) * a.RSK + rn / K];
-            }
-#pragma unroll
-            for (int u = 0; u < QC; u++) {
-#pragma unroll
-                for (int i = 0; i < K; i++) mac(acc[i], w[(i + u) % K], hv[u]);
-                w[u % K] = nx[u];
-            }
-        }
-    }
-
-    if constexpr (QUAD) {
-        // FM quadrature (demod/quadrature.h:41-56): out = arg(y[m] * conj(y[m-1])) / dev
-        __shared__ float2 lastY[256];
-        lastY[l] = acc[K - 1];
-        __syncthreads();
-        float* out = reinterpret_cast<float*>(a.out);
-#pragma unroll
-        for (int i = 0; i < K; i++) {
-            const int m = mFirst + l * K + i;
-            if (m >= 0 && m >= tile * a.TMS && m < a.M) {
-                float2 prev;
-                if (m == 0) prev = a.din[0];
-                else if (i > 0) prev = acc[i - 1];
-                else prev = lastY[l - 1];
-                const float2 y = acc[i];
-                const float br = prev.x, bi = -prev.y;
-                const float re = (y.x * br) - (y.y * bi);
-                const float im = (y.y * br) + (y.x * bi);
-                out[m] = atan2f(im, re) * a.invDev;
-                if (m == a.M - 1) a.dinNext[0] = y;
-            }
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < K; i++) {
-            const int m = mFirst + l * K + i;
-            if (m < a.M && m < (tile + 1) * a.TMS) {
-                if constexpr (STEREO) {
-                    reinterpret_cast<float2*>(a.out)[m] = make_float2(acc[i], acc[i]);   // LRToStereo(l = r)
-                } else {
-                    reinterpret_cast<DT*>(a.out)[m] = acc[i];
-                }
-            }
-        }
+        __syncthreads();                                            // LDS span free for the next commit
+        if (next >= a.ntiles) break;
+        tile = next;
     }
 }
 
@@ -359,7 +424,7 @@ Block::~Block() {
     if (own) (void)hipStreamDestroy(own);
 }
 int Block::init_stream() {
-    SDRGPU_HIP(hipSetDevice(device));
+    SDRGPU_SET_DEVICE(device);
     SDRGPU_HIP(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
     return SDRGPU_OK;
 }
@@ -380,6 +445,9 @@ struct FirBlock : Block {
         ttype = ttype_;
         if (decim < 1) { set_error("fir: decimation %d < 1", decim); return SDRGPU_EARG; }
         D = decim;
+        if (const char* e = getenv("SDRGPU_FIR_TPW")) tilesPerWG = std::max(1, atoi(e));
+        if (const char* e = getenv("SDRGPU_FIR_NT")) forceNT = atoi(e);
+        if (const char* e = getenv("SDRGPU_FIR_LDS_KB")) ldsCap = std::max(8, atoi(e));
         SDRGPU_CHECK(init_stream());
         SDRGPU_CHECK(set_taps(t, n));
         return SDRGPU_OK;
@@ -388,7 +456,7 @@ struct FirBlock : Block {
     // DecimatingFIR::setTaps resets the decimation phase (decimating_fir.h:19-26)
     int set_taps(const float* t, int n) {
         if (!t || n < 1 || n > 64001) { set_error("fir: tap count %d out of range [1, 64001]", n); return SDRGPU_EARG; }
-        SDRGPU_HIP(hipSetDevice(device));
+        SDRGPU_SET_DEVICE(device);
         const size_t es = esize(in_dtype);
         const int oldH = ntaps > 0 ? ntaps - 1 : 0, newH = n - 1;
         std::vector<unsigned char> oldHist((size_t)oldH * es), newHist((size_t)std::max(newH, 1) * es, 0);
@@ -415,7 +483,7 @@ struct FirBlock : Block {
     // device taps in [p][q] = h[q*D + p] order, zero past ntaps (phase-major like the LDS span)
     std::vector<float> host_taps;
     int upload_taps() {
-        SDRGPU_HIP(hipSetDevice(device));
+        SDRGPU_SET_DEVICE(device);
         Q = (ntaps + D - 1) / D;
         Q = (Q + 7) / 8 * 8;      // kernel chunk QC = 8 (zero taps past ntaps)
         const int e = ttype == SDRGPU_C64 ? 2 : 1;
@@ -432,7 +500,7 @@ struct FirBlock : Block {
     }
     int out_count(int count) override { return count > offset ? (count - offset + D - 1) / D : 0; }
     int reset() override {
-        SDRGPU_HIP(hipSetDevice(device));
+        SDRGPU_SET_DEVICE(device);
         SDRGPU_HIP(hipMemset(hist[cur].p, 0, (size_t)std::max(ntaps - 1, 1) * esize(in_dtype)));
         if (quad) SDRGPU_HIP(hipMemset(din[cur].p, 0, sizeof(float2)));
         offset = 0;
@@ -447,11 +515,25 @@ struct FirBlock : Block {
         return 1;
     }
     int NT = 256;
+    int tilesPerWG = 1;     // SDRGPU_FIR_TPW (tuning)
+    int forceNT = 0;        // SDRGPU_FIR_NT (tuning): threads per tile
+    int ldsCap = 76;        // SDRGPU_FIR_LDS_KB (tuning): preferred LDS per tile
     template <typename DT, typename TT, int K, bool XL, bool QD, bool ST>
     int launch_t(FirArgs& a, int tiles, size_t lds, hipStream_t s) {
-        auto k = fir_kernel<DT, TT, K, XL, QD, ST>;
+        // taps behind the span in LDS when they fit (<= 16 KB)
+        const size_t tb = (size_t)D * Q * sizeof(TT);
+        const bool tl = tb <= 16 * 1024 && lds + tb <= 160 * 1024;
+        a.tapsLdsOff = (int)((lds + 15) / 16 * 16);
+        if (tl) lds = a.tapsLdsOff + tb;
+        auto k = tl ? fir_kernel<DT, TT, K, XL, QD, ST, true> : fir_kernel<DT, TT, K, XL, QD, ST, false>;
         SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(k, dim3(tiles), dim3(NT), lds, s, a);
+        a.ntiles = tiles;
+        // tilesPerWG consecutive-in-stride tiles per workgroup. A co-resident persistent grid
+        // (tilesPerWG ~ tiles / (2 * CUs)) with the register prefetch was measured 1.5x SLOWER
+        // than one tile per workgroup on C3 (the hardware's own workgroup turnover staggers the
+        // load/compute phases of the workgroups sharing a CU better), so the default is 1.
+        const int grid = (tiles + tilesPerWG - 1) / tilesPerWG;
+        hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, s, a);
         SDRGPU_HIP(hipGetLastError());
         return SDRGPU_OK;
     }
@@ -463,7 +545,7 @@ struct FirBlock : Block {
     }
     int run(const void* in, int count, void* out, hipStream_t s) override {
         if (count < 0) { set_error("fir: negative count"); return SDRGPU_EARG; }
-        SDRGPU_HIP(hipSetDevice(device));
+        SDRGPU_SET_DEVICE(device);
         const int M = out_count(count);
         const int H = ntaps - 1;
         if (xl && count > 0) SDRGPU_CHECK(nco.prepare(count, s));
@@ -476,9 +558,9 @@ struct FirBlock : Block {
             int RSK = 0, RSP = 0;
             // prefer a tile that leaves room for two workgroups per CU (<= 76 KB), else <= 150 KB
             const int K0 = K;
-            for (size_t cap : {(size_t)76 * 1024, (size_t)150 * 1024}) {
+            for (size_t cap : {(size_t)ldsCap * 1024, (size_t)150 * 1024}) {
                 K = K0;
-                NT = 256;
+                NT = (forceNT == 64 || forceNT == 128) ? forceNT : 256;
                 for (;;) {
                     const int TM = NT * K;
                     const int rows = TM + Q + 2 * K;
@@ -554,7 +636,7 @@ struct XlatorBlock : Block {
     int out_count(int count) override { return count; }
     int reset() override { nco.phase.reset(); return SDRGPU_OK; }
     int run(const void* in, int count, void* out, hipStream_t s) override {
-        SDRGPU_HIP(hipSetDevice(device));
+        SDRGPU_SET_DEVICE(device);
         if (count > 0) {
             SDRGPU_CHECK(nco.prepare(count, s));
             hipLaunchKernelGGL(xlator_kernel, dim3((count + 255) / 256), dim3(256), 0, s, (const float2*)in, (float2*)out,
@@ -573,12 +655,12 @@ struct QuadBlock : Block {
     int cur = 0;
     int out_count(int count) override { return count; }
     int reset() override {
-        SDRGPU_HIP(hipSetDevice(device));
+        SDRGPU_SET_DEVICE(device);
         SDRGPU_HIP(hipMemset(din[cur].p, 0, sizeof(float2)));
         return SDRGPU_OK;
     }
     int run(const void* in, int count, void* out, hipStream_t s) override {
-        SDRGPU_HIP(hipSetDevice(device));
+        SDRGPU_SET_DEVICE(device);
         if (count <= 0) return 0;
         hipLaunchKernelGGL(quad_kernel, dim3((count + 255) / 256), dim3(256), 0, s, (const float2*)in, (float*)out, count,
                            din[cur].as<float2>(), din[cur ^ 1].as<float2>(), invDev);
@@ -617,13 +699,13 @@ struct PolyBlock : Block {
         return (int)((lim - 1 - pos) / decim + 1);
     }
     int reset() override {
-        SDRGPU_HIP(hipSetDevice(device));
+        SDRGPU_SET_DEVICE(device);
         SDRGPU_HIP(hipMemset(hist[cur].p, 0, esize(in_dtype) * std::max(tpp - 1, 1)));
         phase = 0; offset = 0;
         return SDRGPU_OK;
     }
     int run(const void* in, int count, void* out, hipStream_t s) override {
-        SDRGPU_HIP(hipSetDevice(device));
+        SDRGPU_SET_DEVICE(device);
         const int M = out_count(count);
         const int H = tpp - 1;
         const long long pos0 = (long long)offset * interp + phase;
@@ -996,7 +1078,7 @@ extern "C" int sdrgpu_block_process(sdrgpu_block* h, const void* in, int count, 
     NEED_HANDLE(h);
     if (count < 0 || (count > 0 && (!in || !out))) { set_error("process: bad buffers"); return SDRGPU_EARG; }
     Block* b = h->impl;
-    SDRGPU_HIP(hipSetDevice(b->device));
+    SDRGPU_SET_DEVICE(b->device);
     const size_t inB = (size_t)std::max(count, 1) * esize(b->in_dtype);
     const int mExp = b->out_count(count);
     const size_t outB = (size_t)std::max(mExp, 1) * esize(b->out_dtype);
@@ -1039,7 +1121,7 @@ extern "C" int sdrgpu_convert_dev(int device, int kind, const void* in, long lon
         set_error("convert: bad argument");
         return SDRGPU_EARG;
     }
-    SDRGPU_HIP(hipSetDevice(device));
+    SDRGPU_SET_DEVICE(device);
     if (n == 0) return 0;
     hipLaunchKernelGGL(convert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, kind, in, n, out);
     SDRGPU_HIP(hipGetLastError());
@@ -1050,7 +1132,7 @@ extern "C" int sdrgpu_convert(int device, int kind, const void* in, long long n,
     static const int isz[] = {1, 2, 3, 4, 8, 1};
     if (kind < SDRGPU_CONV_U8 || kind > SDRGPU_CONV_I8 || n < 0) { set_error("convert: bad argument"); return SDRGPU_EARG; }
     if (n == 0) return 0;
-    SDRGPU_HIP(hipSetDevice(device));
+    SDRGPU_SET_DEVICE(device);
     void* din = nullptr;
     float* dout = nullptr;
     SDRGPU_HIP(hipMalloc(&din, (size_t)n * isz[kind]));

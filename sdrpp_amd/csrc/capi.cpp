@@ -14,7 +14,7 @@ extern "C" int sdrgpu_device_count(void) {
 }
 extern "C" int sdrgpu_malloc(int device, void** dptr, size_t bytes) {
     if (!dptr) { set_error("malloc: null out pointer"); return SDRGPU_EARG; }
-    SDRGPU_HIP(hipSetDevice(device));
+    SDRGPU_SET_DEVICE(device);
     SDRGPU_HIP(hipMalloc(dptr, bytes));
     return SDRGPU_OK;
 }
@@ -33,7 +33,7 @@ extern "C" int sdrgpu_memcpy_d2h(void* dst, const void* src, size_t bytes, void*
 }
 extern "C" int sdrgpu_stream_create(int device, void** stream) {
     if (!stream) { set_error("stream_create: null out pointer"); return SDRGPU_EARG; }
-    SDRGPU_HIP(hipSetDevice(device));
+    SDRGPU_SET_DEVICE(device);
     hipStream_t s;
     SDRGPU_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     *stream = (void*)s;

@@ -290,6 +290,143 @@ __global__ __launch_bounds__(S * L / 16) void fft_passA_kernel(
         });
 }
 
+// ---- pass A, paired columns: S columns x N1 rows per tile, two adjacent columns per lane --
+// Same transform as fft_passA_kernel with a third of its vector-memory instructions per
+// element (the 64k pass A was issue-bound on them): 16-B loads of two
+// adjacent columns (and an 8-B window pair), stage twiddles staged once per workgroup in
+// LDS, and one 16-B load of the exact four-step twiddle pair W_N^(n2 k1) from an N-entry
+// [k1][n2] table (L2-resident) instead of a product of two table values. Requires an even
+// frame stride and a 16-B aligned input (checked on the host).
+template <int L, int R, int NS, int V>
+__device__ __forceinline__ void stage_lds_v(float2* seq0, const float2* twl, int t) {
+    constexpr int T = L / 16, BPT = 16 / R, LS = Lds<L>::LS;
+    float2 v[V][BPT][R];
+#pragma unroll
+    for (int q = 0; q < V; q++)
+#pragma unroll
+        for (int b = 0; b < BPT; b++) {
+            const int j = t + b * T, jm = j % NS;
+#pragma unroll
+            for (int r = 0; r < R; r++) v[q][b][r] = seq0[q * LS + pad16(j + r * (L / R))];
+#pragma unroll
+            for (int r = 1; r < R; r++) v[q][b][r] = cmul(v[q][b][r], twl[r * jm * (L / (NS * R))]);
+            dft<R>(v[q][b]);
+        }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < V; q++)
+#pragma unroll
+        for (int b = 0; b < BPT; b++) {
+            const int j = t + b * T, idxD = (j / NS) * NS * R + (j % NS);
+#pragma unroll
+            for (int r = 0; r < R; r++) seq0[q * LS + pad16(idxD + r * NS)] = v[q][b][r];
+        }
+    __syncthreads();
+}
+
+template <int L, int R, int NS, int V, class Store>
+__device__ __forceinline__ void stage_last_v(const float2* seq0, const float2* twl, int t, Store&& st) {
+    constexpr int T = L / 16, BPT = 16 / R, LS = Lds<L>::LS;
+    float2 v[V][BPT][R];
+#pragma unroll
+    for (int q = 0; q < V; q++)
+#pragma unroll
+        for (int b = 0; b < BPT; b++) {
+            const int j = t + b * T, jm = j % NS;
+#pragma unroll
+            for (int r = 0; r < R; r++) v[q][b][r] = seq0[q * LS + pad16(j + r * (L / R))];
+#pragma unroll
+            for (int r = 1; r < R; r++) v[q][b][r] = cmul(v[q][b][r], twl[r * jm * (L / (NS * R))]);
+            dft<R>(v[q][b]);
+        }
+#pragma unroll
+    for (int b = 0; b < BPT; b++) {
+        const int j = t + b * T, idxD = (j / NS) * NS * R + (j % NS);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            float2 y[V];
+#pragma unroll
+            for (int q = 0; q < V; q++) y[q] = v[q][b][r];
+            st(idxD + r * NS, y);
+        }
+    }
+}
+
+// stages 2.. of V length-L sequences (seq q at seq0 + q*LS) with LDS twiddles
+template <int L, int V, class Store>
+__device__ __forceinline__ void stages_rest_v(float2* seq0, const float2* twl, int t, Store&& st) {
+    if constexpr (L == 64) {
+        stage_last_v<L, 4, 16, V>(seq0, twl, t, st);
+    } else if constexpr (L == 128) {
+        stage_last_v<L, 8, 16, V>(seq0, twl, t, st);
+    } else if constexpr (L == 256) {
+        stage_last_v<L, 16, 16, V>(seq0, twl, t, st);
+    } else {
+        stage_lds_v<L, 16, 16, V>(seq0, twl, t);
+        if constexpr (L == 512) stage_last_v<L, 2, 256, V>(seq0, twl, t, st);
+        else if constexpr (L == 1024) stage_last_v<L, 4, 256, V>(seq0, twl, t, st);
+        else if constexpr (L == 2048) stage_last_v<L, 8, 256, V>(seq0, twl, t, st);
+        else stage_last_v<L, 16, 256, V>(seq0, twl, t, st);
+    }
+}
+
+template <int L, int S>
+__global__ __launch_bounds__(S / 2 * L / 16) void fft_passA2_kernel(
+    const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
+    int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull, float2* __restrict__ scratch, int dbg) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    constexpr int P = S / 2, T = L / 16, NT = P * T, LS = Lds<L>::LS;
+    float2* twl = lds + S * LS;
+    const int tid = threadIdx.x;
+    const int cp = tid % P, t = tid / P;
+    for (int i = tid; i < L; i += NT) twl[i] = tw[i];
+    const int nb = N2 / S;
+    const int b = blockIdx.x % nb;
+    const long long f = blockIdx.x / nb;
+    const int col = b * S + 2 * cp;
+    const float2* x = in + f * frameStride;
+    float4 q[16];
+    float2 w[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const long long n = (long long)(t + r * T) * N2 + col;
+        if (n + 1 < nz) {
+            q[r] = *reinterpret_cast<const float4*>(x + ((dbg & 4) ? (long long)b * S * L + (long long)(r * NT + tid) * 2 : n));
+            w[r] = (dbg & 1) ? make_float2(1.0f, 1.0f) : *reinterpret_cast<const float2*>(win + n);
+        } else {   // zero-padded tail (n >= nz) or the one pair straddling nz
+            const bool live = n < nz;
+            const float2 e = x[live ? n : 0];
+            const float we = live ? win[n] : 0.0f;
+            q[r] = make_float4(e.x, e.y, 0.0f, 0.0f);
+            w[r] = make_float2(we, 0.0f);
+        }
+    }
+    float2 v0[16], v1[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        v0[r] = make_float2(q[r].x * w[r].x, q[r].y * w[r].x);
+        v1[r] = make_float2(q[r].z * w[r].y, q[r].w * w[r].y);
+    }
+    dft16(v0);
+    dft16(v1);
+    float2* seq0 = lds + 2 * cp * LS;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        seq0[pad16(t * 16 + r)] = v0[r];
+        seq0[LS + pad16(t * 16 + r)] = v1[r];
+    }
+    __syncthreads();
+    float2* dst = scratch + (f << logN);
+    stages_rest_v<L, 2>(seq0, twl, t, [&](int k1, float2 (&y)[2]) {
+        const long long o = (long long)k1 * N2 + col;
+        const float4 tt = (dbg & 2) ? make_float4(1.f, 0.f, 1.f, 0.f) : *reinterpret_cast<const float4*>(tfull + o);
+        const float2 a = cmul(y[0], make_float2(tt.x, tt.y)), c = cmul(y[1], make_float2(tt.z, tt.w));
+        // (dbg & 8: tile-contiguous store, timing ablation only)
+        const long long od = (dbg & 8) ? (long long)b * S * L + (long long)k1 * S + 2 * cp : o;
+        *reinterpret_cast<float4*>(dst + od) = make_float4(a.x, a.y, c.x, c.y);
+    });
+}
+
 // ---- pass B: S rows of length N2 per tile, dB out, transposed store -----------------
 // Stage 1 maps threads row-contiguous (coalesced row reads); the last stage maps the row
 // index fastest so the transposed dB store writes S consecutive floats per k2.
@@ -328,11 +465,12 @@ __global__ __launch_bounds__(S * L / 16) void fft_passB_kernel(
 struct FftPlan {
     int device = 0, N = 0, logN = 0, nz = 0;
     int N1 = 0, N2 = 0;               // two-pass split (N1 * N2 = N); N1 = 0 -> single pass
-    DevBuf win, tw1, tw2, tbase, tcol, scratch;
+    DevBuf win, tw1, tw2, tbase, tcol, tfull, scratch;
     int chunkFrames = 1;
     int sa = 16, sb = 32;             // pass-A columns / pass-B rows per workgroup (tuning)
     int dbg = 0;                      // timing-only ablations (SDRGPU_FFT_DEBUG; wrong results)
     int tcolS = 0;                    // columns of the [k1][c] twiddle table
+    int sa2 = 0;                      // paired pass-A columns per workgroup (0: paired kernel off)
     hipStream_t own = nullptr;
     PinnedBuf pin_in, pin_out;
     DevBuf dev_in, dev_out;
@@ -383,6 +521,19 @@ static int launch_passA(const FftPlan& p, const float2* in, long long stride, in
 }
 
 template <int L, int S>
+static int launch_passA2(const FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
+    if (p.N2 % S) { set_error("fft: N2 %d not a multiple of %d columns", p.N2, S); return SDRGPU_ESTATE; }
+    auto k = fft_passA2_kernel<L, S>;
+    size_t lds = sizeof(float2) * (S * Lds<L>::LS + L);
+    SDRGPU_CHECK(set_lds(k, lds));
+    const int g = (p.N2 / S) * frames;
+    hipLaunchKernelGGL(k, dim3(g), dim3(S / 2 * L / 16), lds, s, in, stride, frames, p.win.as<float>(), p.nz, p.N2,
+                       p.logN, p.tw1.as<float2>(), p.tfull.as<float2>(), p.scratch.as<float2>(), p.dbg);
+    SDRGPU_HIP(hipGetLastError());
+    return SDRGPU_OK;
+}
+
+template <int L, int S>
 static int launch_passB(const FftPlan& p, int frames, float* out, hipStream_t s) {
     auto k = fft_passB_kernel<L, S>;
     size_t lds = sizeof(float2) * S * Lds<L>::LS;
@@ -426,6 +577,22 @@ static int dispatch_passA(const FftPlan& p, const float2* in, long long stride, 
     return SDRGPU_EARG;
 }
 
+// paired-column pass A (16-B accesses); used when the input allows 16-B loads
+static int dispatch_passA2(const FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
+    switch (p.N1) {
+    case 64: return launch_passA2<64, 32>(p, in, stride, frames, s);
+    case 128: return launch_passA2<128, 32>(p, in, stride, frames, s);
+    case 256:
+        if (p.sa2 == 64) return launch_passA2<256, 64>(p, in, stride, frames, s);
+        if (p.sa2 == 16) return launch_passA2<256, 16>(p, in, stride, frames, s);
+        return launch_passA2<256, 32>(p, in, stride, frames, s);
+    case 512: return launch_passA2<512, 16>(p, in, stride, frames, s);
+    case 1024: return launch_passA2<1024, 16>(p, in, stride, frames, s);
+    }
+    set_error("fft: unsupported N1 %d", p.N1);
+    return SDRGPU_EARG;
+}
+
 static int dispatch_passB(const FftPlan& p, int frames, float* out, hipStream_t s) {
     switch (p.N2) {
     case 64: return launch_passB<64, 32>(p, frames, out, s);
@@ -451,7 +618,7 @@ struct sdrgpu_fft {
 
 static int fft_upload_window(sdrgpu_fft* h, const float* window, int nz) {
     if (nz <= 0 || nz > h->p.N) { set_error("fft: nz %d out of range (N %d)", nz, h->p.N); return SDRGPU_EARG; }
-    SDRGPU_HIP(hipSetDevice(h->p.device));
+    SDRGPU_SET_DEVICE(h->p.device);
     SDRGPU_CHECK(h->p.win.ensure(sizeof(float) * nz));
     SDRGPU_HIP(hipMemcpy(h->p.win.p, window, sizeof(float) * nz, hipMemcpyHostToDevice));
     h->p.nz = nz;
@@ -467,7 +634,7 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         set_error("fft_create: size %d must be a power of two in [64, 2^20]", fftSize);
         return SDRGPU_EARG;
     }
-    SDRGPU_HIP(hipSetDevice(device));
+    SDRGPU_SET_DEVICE(device);
     sdrgpu_fft* h = new sdrgpu_fft();
     FftPlan& p = h->p;
     p.device = device; p.N = fftSize; p.logN = logN;
@@ -520,6 +687,25 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
                 rc = SDRGPU_EHIP;
             }
         }
+        // paired-column pass A: +13% on the 1M transform (N1 = 1024), but slower than the
+        // one-column kernel at N1 = 256 (64k: 2.05-2.10 vs 1.86 ms per 2^28 samples, A/B on
+        // one box), so it is the default only for N1 >= 512
+        p.sa2 = p.N1 >= 512 ? 16 : 0;
+        if (const char* e = getenv("SDRGPU_FFT_SA2")) p.sa2 = atoi(e);
+        if (rc >= 0 && p.sa2 > 0) {   // Tfull[k1][n2] = W_N^(n2 k1), exact argument mod N
+            std::vector<float2> t((size_t)fftSize);
+            for (int k1 = 0; k1 < p.N1; k1++)
+                for (int n2 = 0; n2 < p.N2; n2++) {
+                    const long long m = ((long long)n2 * k1) % fftSize;
+                    const double a = -2.0 * M_PI * (double)m / (double)fftSize;
+                    t[(size_t)k1 * p.N2 + n2] = make_float2((float)std::cos(a), (float)std::sin(a));
+                }
+            rc = p.tfull.ensure(sizeof(float2) * t.size());
+            if (rc >= 0 && hipMemcpy(p.tfull.p, t.data(), sizeof(float2) * t.size(), hipMemcpyHostToDevice) != hipSuccess) {
+                set_error("fft: twiddle upload failed");
+                rc = SDRGPU_EHIP;
+            }
+        }
         if (rc >= 0) rc = p.scratch.ensure((size_t)p.chunkFrames * fftSize * sizeof(float2));
     }
     if (rc >= 0 && hipStreamCreateWithFlags(&p.own, hipStreamNonBlocking) != hipSuccess) {
@@ -552,16 +738,20 @@ extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long f
     if (!h || !in || !out || frames < 0 || frameStride < 0) { set_error("fft_execute: bad argument"); return SDRGPU_EARG; }
     if (frames == 0) return 0;
     FftPlan& p = h->p;
-    SDRGPU_HIP(hipSetDevice(p.device));
+    SDRGPU_SET_DEVICE(p.device);
     hipStream_t s = stream ? (hipStream_t)stream : p.own;
     const float2* x = (const float2*)in;
     if (p.N1 == 0) {
         SDRGPU_CHECK(dispatch_single(p, x, frameStride, frames, out, s));
         return frames;
     }
+    // 16-B loads need an even frame stride and a 16-B aligned base
+    const bool paired = p.sa2 > 0 && (frameStride % 2) == 0 && ((uintptr_t)in & 15) == 0;
     for (int f0 = 0; f0 < frames; f0 += p.chunkFrames) {
         int nf = std::min(p.chunkFrames, frames - f0);
-        SDRGPU_CHECK(dispatch_passA(p, x + (long long)f0 * frameStride, frameStride, nf, s));
+        const float2* xc = x + (long long)f0 * frameStride;
+        if (paired) SDRGPU_CHECK(dispatch_passA2(p, xc, frameStride, nf, s));
+        else SDRGPU_CHECK(dispatch_passA(p, xc, frameStride, nf, s));
         SDRGPU_CHECK(dispatch_passB(p, nf, out + (long long)f0 * p.N, s));
     }
     return frames;
@@ -570,7 +760,7 @@ extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long f
 extern "C" int sdrgpu_fft_logmag(sdrgpu_fft* h, const void* in, float* out) {
     if (!h || !in) { set_error("fft_logmag: null argument"); return SDRGPU_EARG; }
     FftPlan& p = h->p;
-    SDRGPU_HIP(hipSetDevice(p.device));
+    SDRGPU_SET_DEVICE(p.device);
     size_t inB = sizeof(float2) * p.nz, outB = sizeof(float) * p.N;
     SDRGPU_CHECK(p.pin_in.ensure(inB));
     SDRGPU_CHECK(p.dev_in.ensure(inB));

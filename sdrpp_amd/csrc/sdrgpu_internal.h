@@ -21,6 +21,18 @@ void set_error(const char* fmt, ...);
         }                                                                             \
     } while (0)
 
+// Select a device, reporting SDRGPU_ENODEV (not a generic HIP error) when there is no
+// GPU or the index is out of range.
+#define SDRGPU_SET_DEVICE(dev)                                                        \
+    do {                                                                              \
+        int n_ = 0, d_ = (dev);                                                       \
+        if (hipGetDeviceCount(&n_) != hipSuccess || d_ < 0 || d_ >= n_) {             \
+            ::sdrgpu::set_error("HIP device %d not available (%d devices)", d_, n_);  \
+            return SDRGPU_ENODEV;                                                     \
+        }                                                                             \
+        SDRGPU_HIP(hipSetDevice(d_));                                                 \
+    } while (0)
+
 #define SDRGPU_CHECK(call)                 \
     do {                                   \
         int r_ = (call);                   \

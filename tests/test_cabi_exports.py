@@ -28,3 +28,16 @@ def test_host_only_entry_points_work_without_gpu():
     # bad arguments fail loudly with a message, not silently
     assert lib.sdrgpu_create_window(99, None, 10, 1) < 0
     assert b"create_window" in lib.sdrgpu_last_error()
+
+
+def test_create_without_device_reports_enodev():
+    """No CPU fallback: on a host without a GPU (or with a bad device index) every handle
+    constructor fails with SDRGPU_ENODEV and a message."""
+    import sdrpp_amd
+    lib = sdrpp_amd.lib
+    h = ctypes.c_void_p()
+    bad = lib.sdrgpu_device_count()          # first index past the last device
+    assert lib.sdrgpu_rxvfo_create(ctypes.byref(h), bad, 61.44e6, 240e3, 200e3, 0.0) == -5
+    assert b"not available" in lib.sdrgpu_last_error()
+    assert lib.sdrgpu_fft_create(ctypes.byref(h), bad, 1024, 1024, 6) == -5
+    assert lib.sdrgpu_wfm_create(ctypes.byref(h), -1, 100e3, 240e3, 1) == -5
