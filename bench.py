@@ -9,7 +9,8 @@ i.e. a 61.44 MS/s-class IQ stream pushed as fast as the GPU takes it through
 with every rank's last 16 spectra gathered to rank 0 over RCCL each step (N > 1).
 A step = one batch of B synthetic complex-float IQ samples resident in HBM
 (uniform [-1, 1), SpeedTester distribution). Other configs: c2 (1M-point BH7 spectrum,
-nz = 1e6, zero-padded), c3 (xlator + 256-tap FIR /8 + FM quadrature, fused).
+nz = 1e6, zero-padded), c3 (xlator + 256-tap FIR /8 + FM quadrature, fused), c4 (1024-channel
+polyphase channelizer, 16384-tap prototype).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
 """
@@ -39,7 +40,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c5", choices=["c5", "c2", "c3"])
+    ap.add_argument("--config", default="c5", choices=["c5", "c2", "c3", "c4"])
     ap.add_argument("--log2-batch", type=int, default=28, help="IQ samples per GPU per step = 2^k (c5/c3)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -123,6 +124,30 @@ class C3:
         return self.out[:65536]
 
 
+class C4:
+    """1024-channel critically sampled polyphase channelizer at 200 MS/s (prototype
+    windowedSinc(16384, fs/(2M), fs, nuttall), 16 taps/branch), output [frame][channel]."""
+    M = 1024
+
+    def __init__(self, B, shard, dev):
+        self.B = (B // self.M) * self.M
+        taps = dsp.windowed_sinc(16 * self.M, np.pi / self.M)
+        self.ch = dsp.PolyphaseChannelizer(self.M, taps, device=dev)
+        self.out = torch.empty(2 * (self.B + self.M), dtype=torch.float32, device="cuda")
+        self.bytes_per_sample = 16.0
+        self.kernel_bytes = 16.0 * self.B
+        self.kernel_name = "chan_kernel<1024> (16-tap branch FIRs + 1024-pt FFT per frame)"
+
+    def dominant(self, x, s):
+        self.ch.process_dev(x.data_ptr(), self.B, self.out.data_ptr(), s)
+
+    def rest(self, x, s):
+        pass
+
+    def gather_src(self):
+        return self.out[:2 * 16 * self.M]
+
+
 def cpu_baseline(seconds):
     """The oracle's C port of the C5 chain on one host core, time-bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -165,7 +190,7 @@ def main():
     B = 1 << a.log2_batch
     if a.config == "c2":
         B = 256 * 1000000
-    wl = {"c5": C5, "c2": C2, "c3": C3}[a.config](B, shard, dev)
+    wl = {"c5": C5, "c2": C2, "c3": C3, "c4": C4}[a.config](B, shard, dev)
     B = wl.B
     g = torch.Generator(device="cuda")
     g.manual_seed(shard.seed())
@@ -218,7 +243,8 @@ def main():
             "config": {"workload": {"c5": "C5 per-GPU slice: 64k BH7 FFT+log-mag (back-to-back) + RxVFO 61.44M->240k "
                                           "+ BroadcastFM mono; RCCL gather of 16 spectra/rank/step",
                                     "c2": "C2: 1M-point BH7 FFT + log-mag, nz=1e6 zero-padded",
-                                    "c3": "C3: xlator + 256-tap FIR /8 + FM quadrature (fused)"}[a.config],
+                                    "c3": "C3: xlator + 256-tap FIR /8 + FM quadrature (fused)",
+                                    "c4": "C4: 1024-channel polyphase channelizer (16384-tap prototype), 1 stream"}[a.config],
                        "samples_per_gpu_per_step": B, "parallelism": f"replica-streams x{world}",
                        "bytes_per_sample": round(wl.bytes_per_sample, 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

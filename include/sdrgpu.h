@@ -74,6 +74,7 @@ int         sdrgpu_host_unregister(void* ptr);
 int  sdrgpu_create_window(int type, float* buffer, int size, int centered);          /* window.h:38 */
 void sdrgpu_gen_reshape_params(double sampleRate, int size, double rate, int* skip, int* nz); /* iq_frontend.h:56 */
 int  sdrgpu_taps_estimate_count(double transWidth, double sampleRate);               /* estimate_tap_count.h:4 */
+int  sdrgpu_taps_windowed_sinc(int count, double omega, double norm, float* out);   /* windowed_sinc.h:9 (window::nuttall) */
 int  sdrgpu_taps_low_pass(double cutoff, double transWidth, double sampleRate, int odd, float* out); /* low_pass.h:7; out NULL -> count */
 int  sdrgpu_taps_high_pass(double cutoff, double transWidth, double sampleRate, int odd, float* out); /* high_pass.h:7 */
 int  sdrgpu_taps_band_pass_f(double start, double stop, double transWidth, double sampleRate, int odd, float* out); /* band_pass.h:11 */
@@ -119,6 +120,11 @@ int sdrgpu_ddc_fm_create(sdrgpu_block** h, int device, double offsetRad, const f
 /* FM<float> (demod/fm.h) and BroadcastFM mono (stereo_t out, broadcast_fm.h) */
 int sdrgpu_fm_create(sdrgpu_block** h, int device, double samplerate, double bandwidth, int lowPass, int highPass);
 int sdrgpu_wfm_create(sdrgpu_block** h, int device, double deviation, double samplerate, int lowPass);
+/* M-channel critically sampled polyphase channelizer (BASELINE C4): channel k of output frame
+ * m is FrequencyXlator(-k fs/M) -> DecimatingFIR<complex_t,float>(taps, M) (frequency_xlator.h:43,
+ * decimating_fir.h:45) with an exact NCO; taps <= 16 M (bank layout polyphase_bank.h:32).
+ * Output: frames x M complex, out[m*M + k]; out_count = frames * M. M in {256, 512, 1024}. */
+int sdrgpu_channelizer_create(sdrgpu_block** h, int device, int channels, const float* taps, int ntaps);
 
 int sdrgpu_block_process(sdrgpu_block* h, const void* in, int count, void* out);      /* host buffers */
 int sdrgpu_block_process_dev(sdrgpu_block* h, const void* in, int count, void* out, void* stream);

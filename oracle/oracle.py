@@ -91,6 +91,7 @@ def _load():
         "orc_ssb_destroy": (None, [vp]),
         "orc_compress": (i, [i, vp, i, vp]),
         "orc_decompress": (i, [vp, i, vp]),
+        "orc_channelize": (i, [vp, l, vp, i, i, vp, i, vp]),
         "orc_chain_create": (vp, [d, i, d, i]),
         "orc_chain_process": (l, [vp, vp, l, vp, l, vp]),
         "orc_chain_destroy": (None, [vp]),
@@ -121,6 +122,26 @@ def _taps(fn, *args):
     t = np.empty(n, dtype=np.float32)
     fn(*args, _p(t))
     return t
+
+
+def windowed_sinc(count, omega, norm=1.0):
+    """taps/windowed_sinc.h:9-35 with window::nuttall (float taps)."""
+    out = np.empty(count, np.float32)
+    lib.orc_windowed_sinc(int(count), float(omega), float(norm), _p(out))
+    return out
+
+
+def channelize(x, h, M, chans):
+    """C4 definition: channel k = exact-NCO xlator(-k fs/M) -> DecimatingFIR(h, M), fp64.
+    Returns complex128 [len(chans), ceil(len(x)/M)]."""
+    x = np.ascontiguousarray(x, np.complex64)
+    h = np.ascontiguousarray(h, np.float32)
+    ch = np.ascontiguousarray(chans, np.int32)
+    frames = (len(x) + M - 1) // M
+    out = np.zeros((len(ch), frames), np.complex128)
+    rc = lib.orc_channelize(_p(x), len(x), _p(h), len(h), int(M), _p(ch), len(ch), _p(out))
+    assert rc == frames
+    return out
 
 
 def low_pass(cutoff, trans, fs, odd=False):

@@ -869,3 +869,41 @@ void orc_chain_destroy(orc_chain* c) {
     if (!c) return;
     free(c->window); free(c->work); free(c->db); orc_vfo_destroy(c->vfo); orc_wfm_destroy(c->wfm); free(c->vbuf); free(c);
 }
+
+/* ---------------------------------------------------------------- C4 channelizer
+ * Definition restated from its parts: xlator (frequency_xlator.h:43-50) with the exact
+ * angle -2 pi k n / M (reduced as the integer k n mod M, so no phase drift), then the
+ * decimating FIR (decimating_fir.h:45-68): buf = [ntaps-1 zeros || x],
+ * y[m] = sum_j h[j] buf[m M + j]. Accumulated in double. */
+int orc_channelize(const float* in, long count, const float* h, int ntaps, int M, const int* chans, int nchan,
+                   double* out) {
+    if (M < 1 || ntaps < 1 || count < 0) return -1;
+    const long frames = (count + M - 1) / M;
+    const long H = ntaps - 1;
+    double* cs = (double*)malloc(sizeof(double) * 2 * M);
+    for (int c = 0; c < nchan; c++) {
+        const long k = chans[c];
+        for (int i = 0; i < M; i++) {            /* e^{-2 pi i t / M}, t = (k n) mod M */
+            const double a = -2.0 * DB_M_PI * (double)i / (double)M;
+            cs[2 * i] = cos(a);
+            cs[2 * i + 1] = sin(a);
+        }
+        for (long m = 0; m < frames; m++) {
+            double ar = 0.0, ai = 0.0;
+            for (int j = 0; j < ntaps; j++) {
+                const long n = m * M + j - H;     /* absolute input index of buf[m M + j] */
+                if (n < 0 || n >= count) continue;
+                const long t = (long)(((k % M) * (n % M)) % M);
+                const double xr = in[2 * n], xi = in[2 * n + 1];
+                const double pr = cs[2 * t], pi = cs[2 * t + 1];
+                const double zr = xr * pr - xi * pi, zi = xr * pi + xi * pr;
+                ar += (double)h[j] * zr;
+                ai += (double)h[j] * zi;
+            }
+            out[2 * ((long)c * frames + m)] = ar;
+            out[2 * ((long)c * frames + m) + 1] = ai;
+        }
+    }
+    free(cs);
+    return (int)frames;
+}

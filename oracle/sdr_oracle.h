@@ -142,6 +142,13 @@ void orc_ssb_destroy(orc_ssb* s);
 int orc_compress(int pcmType, const float* in, int count, uint8_t* out);
 int orc_decompress(const uint8_t* in, int nbytes, float* out);
 
+/* C4 channelizer definition: channel k = FrequencyXlator(-k fs/M) with an
+ * EXACT NCO (angle 2 pi (k n mod M)/M) -> DecimatingFIR<complex_t, float>(h, M)
+ * (frequency_xlator.h:43-50, decimating_fir.h:45-68), fp64 throughout, from reset.
+ * out: [nchan][frames] complex (re, im doubles), frames = ceil(count / M). */
+int orc_channelize(const float* in, long count, const float* h, int ntaps, int M, const int* chans, int nchan,
+                   double* out);
+
 /* C5 per-stream chain used as the CPU baseline: 64k BH7 spectrum (back-to-back
  * frames) + RxVFO(plan_256 + 91-tap LPF) + BroadcastFM mono. Returns audio pairs. */
 typedef struct orc_chain orc_chain;

@@ -55,6 +55,7 @@ def _load():
         "sdrgpu_create_window": (i, [i, fp, i, i]),
         "sdrgpu_gen_reshape_params": (None, [d, i, d, ctypes.POINTER(i), ctypes.POINTER(i)]),
         "sdrgpu_taps_estimate_count": (i, [d, d]),
+        "sdrgpu_taps_windowed_sinc": (i, [i, d, d, fp]),
         "sdrgpu_taps_low_pass": (i, [d, d, d, i, fp]),
         "sdrgpu_taps_high_pass": (i, [d, d, d, i, fp]),
         "sdrgpu_taps_band_pass_f": (i, [d, d, d, d, i, fp]),
@@ -82,6 +83,7 @@ def _load():
         "sdrgpu_ddc_fm_create": (i, [pp, i, d, fp, i, i, d]),
         "sdrgpu_fm_create": (i, [pp, i, d, d, i, i]),
         "sdrgpu_wfm_create": (i, [pp, i, d, d, i]),
+        "sdrgpu_channelizer_create": (i, [pp, i, i, fp, i]),
         "sdrgpu_block_process": (i, [vp, vp, i, vp]),
         "sdrgpu_block_process_dev": (i, [vp, vp, i, vp, vp]),
         "sdrgpu_block_out_count": (i, [vp, i]),

@@ -23,6 +23,7 @@ SOURCES = [
     ("capi.cpp", []),
     ("fft.hip", []),
     ("blocks.hip", []),
+    ("channelizer.hip", []),
 ]
 
 

@@ -69,6 +69,9 @@ extern "C" void sdrgpu_gen_reshape_params(double sampleRate, int size, double ra
 extern "C" int sdrgpu_taps_estimate_count(double transWidth, double sampleRate) {
     return (int)(3.8 * sampleRate / transWidth);
 }
+extern "C" int sdrgpu_taps_windowed_sinc(int count, double omega, double norm, float* out) {
+    return taps_windowed_sinc(count, omega, norm, out);
+}
 extern "C" int sdrgpu_taps_low_pass(double cutoff, double transWidth, double sampleRate, int odd, float* out) {
     return taps_low_pass(cutoff, transWidth, sampleRate, odd, out);
 }

@@ -1,0 +1,199 @@
+// Critically sampled M-channel polyphase channelizer (BASELINE config C4).
+//
+// Definition: channel k is FrequencyXlator(-k fs/M)
+// (channel/frequency_xlator.h:43-50, exact NCO) -> DecimatingFIR<complex_t, float>(h, M)
+// (filter/decimating_fir.h:45-68) with a Q*M-tap prototype h. With buf = [history || in] and
+// D = M, output m of channel k is
+//   y_k[m] = sum_j h[j] buf[offset + mM + j] exp(-2 pi i k n_j / M),  j = qM + r,
+// and because n_j = mM + j + const, the rotation depends on r only:
+//   y_k[m] = sum_c W_M^(k c) v_m[c],   v_m[(rot + r) mod M] = sum_q h[qM + r] buf[offset + (m+q)M + r].
+// So one launch does, per output frame m: M branch FIRs of Q taps (the polyphase bank of
+// multirate/polyphase_bank.h:32, branch r = bank phase M-1-r) and one M-point forward FFT.
+// That is ~4Q + 5 log2 M flop per input sample (64 + 50 at M = 1024, Q = 16), far below the
+// HBM ridge, so the kernel is HBM-bound: 8 B in + 8 B out per sample. A dense
+// DFT-as-GEMM (512 flop/sample) would make it compute-bound; fp32 MFMA has no higher peak
+// than packed-fp32 VALU on gfx950, so the FFT form is the faster one.
+//
+// Kernel layout: one thread per branch r (NT = M threads), 16 frames per batch. A thread
+// keeps its Q taps and a 16-deep circular window of its branch's samples in registers; each
+// batch loads one new sample per frame (coalesced: consecutive r), forms 16 branch outputs
+// into the batch's 16 LDS sequences (rotated by `rot`), then the workgroup runs 16 M-point
+// Stockham FFTs in LDS and stores the channel vectors, out[m][k]. (Prefetching the next
+// batch across the FFT spills at 1024 threads; with 16 loads in flight per thread at batch
+// start the chip already has ~32 MB outstanding per batch time, above the HBM rate.)
+#include <algorithm>
+#include <cstring>
+#include <vector>
+#include "sdrgpu_internal.h"
+#include "fft_stages.h"
+
+namespace sdrgpu {
+
+constexpr int CHAN_Q = 16;   // taps per branch (prototype padded to Q*M)
+
+template <int L>
+__global__ __launch_bounds__(L) void chan_kernel(const float2* __restrict__ hist, const float2* __restrict__ in, int H,
+                                                 int count, const float* __restrict__ taps, long long offset0, int rot,
+                                                 int frames, int fpw, const float2* __restrict__ tw,
+                                                 float2* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    constexpr int Q = CHAN_Q, T = L / 16, LS = Lds<L>::LS;
+    const int r = threadIdx.x;
+    const int m0 = blockIdx.x * fpw;
+    const int m1 = min(m0 + fpw, frames);
+    auto fetch = [&](long long b) -> float2 {          // buf[b] of [hist (H) || in (count)], 0 outside
+        if (b < H) return hist[b];
+        const long long i = b - H;
+        return i < count ? in[i] : make_float2(0.f, 0.f);
+    };
+    const long long base = offset0 + r;
+    float2 xs[16];                                     // xs[(m - m0) & 15] = buf[base + m L]
+#pragma unroll
+    for (int q = 0; q < 15; q++) xs[q] = fetch(base + (long long)(m0 + q) * L);
+    xs[15] = make_float2(0.f, 0.f);
+    for (int mb = m0; mb < m1; mb += 16) {
+        // re-materialise the lane's LDS/FFT indices per batch instead of letting the compiler
+        // hoist ~50 loop-invariant addresses out of the loop (they spill at 128 VGPRs)
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int sF = tid / T, tF = tid % T;          // FFT role: sequence sF (a frame), thread tF
+        const int c = (rot + tid) & (L - 1);
+        float2 nx[16];                                 // newest tap row of each frame of the batch
+        float h[Q];                                    // (re-read per batch from L2: not live across the FFT)
+#pragma unroll
+        for (int q = 0; q < Q; q++) h[q] = taps[q * L + r];
+#pragma unroll
+        for (int f = 0; f < 16; f++) nx[f] = (mb + f < m1) ? fetch(base + (long long)(mb + f + 15) * L) : make_float2(0.f, 0.f);
+#pragma unroll
+        for (int f = 0; f < 16; f++) {
+            xs[(f + 15) & 15] = nx[f];
+            float2 u = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int q = 0; q < Q; q++) {
+                const float2 x = xs[(f + q) & 15];
+                u.x = fmaf(h[q], x.x, u.x);
+                u.y = fmaf(h[q], x.y, u.y);
+            }
+            lds[f * LS + pad16(c)] = u;
+        }
+        __syncthreads();
+        float2 v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) v[i] = lds[sF * LS + pad16(tF + i * T)];
+        __syncthreads();
+        stage_first<L>(lds + sF * LS, v, tF);
+        __syncthreads();
+        const int m = mb + sF;
+        float2* o = out + (long long)m * L;
+        stages_rest<L>(lds, tw, sF, tF, [&](int k, float2 y) {
+            if (m < m1) o[k] = y;
+        });
+        __syncthreads();
+    }
+}
+
+__global__ void chan_hist_kernel(const float2* __restrict__ hist, const float2* __restrict__ in,
+                                 float2* __restrict__ next, int H, int count) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= H) return;
+    const long long b = (long long)count + k;          // last H samples of [hist || in]
+    next[k] = b < H ? hist[b] : in[b - H];
+}
+
+struct ChannelizerBlock : Block {
+    int M = 0, ntaps = 0, Hp = 0, offset = 0, fpw = 256;
+    long long phase = 0;     // absolute input index mod M of the next sample
+    DevBuf taps, tw, hist[2];
+    int cur = 0;
+
+    int setup(int dev, int channels, const float* t, int n) {
+        device = dev;
+        in_dtype = out_dtype = SDRGPU_C64;
+        if (channels != 256 && channels != 512 && channels != 1024) {
+            set_error("channelizer: %d channels unsupported (256, 512 or 1024)", channels);
+            return SDRGPU_EARG;
+        }
+        if (!t || n < 1 || n > CHAN_Q * channels) {
+            set_error("channelizer: %d taps out of range [1, %d]", n, CHAN_Q * channels);
+            return SDRGPU_EARG;
+        }
+        M = channels;
+        ntaps = n;
+        Hp = CHAN_Q * M - 1;
+        if (const char* e = getenv("SDRGPU_CHAN_FPW")) fpw = std::max(16, atoi(e) / 16 * 16);
+        SDRGPU_CHECK(init_stream());
+        std::vector<float> pq((size_t)CHAN_Q * M, 0.0f);       // [q][r] = h[q M + r]
+        for (int j = 0; j < n; j++) pq[j] = t[j];
+        SDRGPU_CHECK(taps.ensure(sizeof(float) * pq.size()));
+        SDRGPU_HIP(hipMemcpy(taps.p, pq.data(), sizeof(float) * pq.size(), hipMemcpyHostToDevice));
+        std::vector<float2> w(M);
+        for (int i = 0; i < M; i++) {
+            const double a = -2.0 * M_PI * (double)i / (double)M;
+            w[i] = make_float2((float)std::cos(a), (float)std::sin(a));
+        }
+        SDRGPU_CHECK(tw.ensure(sizeof(float2) * M));
+        SDRGPU_HIP(hipMemcpy(tw.p, w.data(), sizeof(float2) * M, hipMemcpyHostToDevice));
+        for (int k = 0; k < 2; k++) SDRGPU_CHECK(hist[k].ensure(sizeof(float2) * Hp));
+        return reset();
+    }
+    // DecimatingFIR output count (decimating_fir.h:45-68) x M channels
+    int out_count(int count) override { return count > offset ? (count - offset + M - 1) / M * M : 0; }
+    int reset() override {
+        SDRGPU_SET_DEVICE(device);
+        SDRGPU_HIP(hipMemset(hist[cur].p, 0, sizeof(float2) * Hp));
+        offset = 0;
+        phase = 0;
+        return SDRGPU_OK;
+    }
+    template <int L>
+    int launch(const void* in, int count, int frames, long long offset0, int rot, void* out, hipStream_t s) {
+        auto k = chan_kernel<L>;
+        const size_t lds = sizeof(float2) * 16 * Lds<L>::LS;
+        SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        const int grid = (frames + fpw - 1) / fpw;
+        hipLaunchKernelGGL(k, dim3(grid), dim3(L), lds, s, hist[cur].as<float2>(), (const float2*)in, Hp, count,
+                           taps.as<float>(), offset0, rot, frames, fpw, tw.as<float2>(), (float2*)out);
+        SDRGPU_HIP(hipGetLastError());
+        return SDRGPU_OK;
+    }
+    int run(const void* in, int count, void* out, hipStream_t s) override {
+        if (count < 0) { set_error("channelizer: negative count"); return SDRGPU_EARG; }
+        SDRGPU_SET_DEVICE(device);
+        const int outN = out_count(count);
+        const int frames = outN / M;
+        const int H = ntaps - 1;                                   // the reference FIR's history
+        if (frames > 0) {
+            // buf' (history H) index b <-> padded buf index b + (Hp - H); absolute sample index
+            // of buf'[b] is phase - H + b, so the NCO rotation of tap row r is (rot + r) mod M
+            const long long offset0 = (long long)offset + (Hp - H);
+            const int rot = (int)((((phase - H + offset) % M) + M) % M);
+            int rc;
+            if (M == 1024) rc = launch<1024>(in, count, frames, offset0, rot, out, s);
+            else if (M == 512) rc = launch<512>(in, count, frames, offset0, rot, out, s);
+            else rc = launch<256>(in, count, frames, offset0, rot, out, s);
+            SDRGPU_CHECK(rc);
+        }
+        if (count > 0) {
+            hipLaunchKernelGGL(chan_hist_kernel, dim3((Hp + 255) / 256), dim3(256), 0, s, hist[cur].as<float2>(),
+                               (const float2*)in, hist[cur ^ 1].as<float2>(), Hp, count);
+            SDRGPU_HIP(hipGetLastError());
+            cur ^= 1;
+        }
+        offset = offset + frames * M - count;
+        phase = (phase + count) % M;
+        return outN;
+    }
+};
+
+}  // namespace sdrgpu
+
+using namespace sdrgpu;
+
+extern "C" int sdrgpu_channelizer_create(sdrgpu_block** h, int device, int channels, const float* taps, int ntaps) {
+    if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
+    auto* b = new ChannelizerBlock();
+    const int rc = b->setup(device, channels, taps, ntaps);
+    if (rc < 0) { delete b; return rc; }
+    *h = new sdrgpu_block{b};
+    return SDRGPU_OK;
+}

@@ -17,164 +17,9 @@
 #include <cstdlib>
 #include <algorithm>
 #include "sdrgpu_internal.h"
+#include "fft_stages.h"
 
 namespace sdrgpu {
-
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 mul_negi(float2 a) { return make_float2(a.y, -a.x); }   // a * (-i)
-
-// ---- small forward DFTs in registers (e^{-i}) ------------------------------
-__device__ __forceinline__ void dft2(float2* v) {
-    float2 a = v[0], b = v[1];
-    v[0] = cadd(a, b);
-    v[1] = csub(a, b);
-}
-__device__ __forceinline__ void dft4(float2& x0, float2& x1, float2& x2, float2& x3) {
-    float2 a0 = cadd(x0, x2), a1 = csub(x0, x2), a2 = cadd(x1, x3), a3 = mul_negi(csub(x1, x3));
-    x0 = cadd(a0, a2);
-    x2 = csub(a0, a2);
-    x1 = cadd(a1, a3);
-    x3 = csub(a1, a3);
-}
-__device__ __forceinline__ void dft4v(float2* v) { dft4(v[0], v[1], v[2], v[3]); }
-
-__device__ __forceinline__ void dft8(float2* v) {
-    const float R2 = 0.70710678118654752440f;
-    float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
-    float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
-    dft4(e0, e1, e2, e3);
-    dft4(o0, o1, o2, o3);
-    o1 = make_float2(R2 * (o1.x + o1.y), R2 * (o1.y - o1.x));   // * W8^1 = (1-i)/sqrt2
-    o2 = mul_negi(o2);                                           // * W8^2 = -i
-    o3 = make_float2(R2 * (o3.y - o3.x), -R2 * (o3.x + o3.y));   // * W8^3 = (-1-i)/sqrt2
-    v[0] = cadd(e0, o0); v[4] = csub(e0, o0);
-    v[1] = cadd(e1, o1); v[5] = csub(e1, o1);
-    v[2] = cadd(e2, o2); v[6] = csub(e2, o2);
-    v[3] = cadd(e3, o3); v[7] = csub(e3, o3);
-}
-
-// 16-point DFT as 4 x 4: X[k1 + 4 k2] = sum_n2 W4^(n2 k2) W16^(n2 k1) DFT4_n1(x[4 n1 + n2])
-__device__ __forceinline__ void dft16(float2* v) {
-    const float C1 = 0.92387953251128675613f, S1 = 0.38268343236508977173f, R2 = 0.70710678118654752440f;
-    float2 y[4][4];
-#pragma unroll
-    for (int n2 = 0; n2 < 4; n2++) {
-        y[n2][0] = v[n2]; y[n2][1] = v[4 + n2]; y[n2][2] = v[8 + n2]; y[n2][3] = v[12 + n2];
-        dft4(y[n2][0], y[n2][1], y[n2][2], y[n2][3]);
-    }
-    // twiddles W16^(n2 k1) = exp(-2 pi i n2 k1 / 16)
-    y[1][1] = cmul(y[1][1], make_float2(C1, -S1));
-    y[1][2] = cmul(y[1][2], make_float2(R2, -R2));
-    y[1][3] = cmul(y[1][3], make_float2(S1, -C1));
-    y[2][1] = cmul(y[2][1], make_float2(R2, -R2));
-    y[2][2] = mul_negi(y[2][2]);
-    y[2][3] = cmul(y[2][3], make_float2(-R2, -R2));
-    y[3][1] = cmul(y[3][1], make_float2(S1, -C1));
-    y[3][2] = cmul(y[3][2], make_float2(-R2, -R2));
-    y[3][3] = cmul(y[3][3], make_float2(-C1, S1));
-#pragma unroll
-    for (int k1 = 0; k1 < 4; k1++) {
-        float2 a = y[0][k1], b = y[1][k1], c = y[2][k1], d = y[3][k1];
-        dft4(a, b, c, d);
-        v[k1] = a; v[k1 + 4] = b; v[k1 + 8] = c; v[k1 + 12] = d;
-    }
-}
-
-template <int R> __device__ __forceinline__ void dft(float2* v);
-template <> __device__ __forceinline__ void dft<2>(float2* v) { dft2(v); }
-template <> __device__ __forceinline__ void dft<4>(float2* v) { dft4v(v); }
-template <> __device__ __forceinline__ void dft<8>(float2* v) { dft8(v); }
-template <> __device__ __forceinline__ void dft<16>(float2* v) { dft16(v); }
-
-__device__ __forceinline__ int pad16(int i) { return i + (i >> 4); }
-template <int L> struct Lds { static constexpr int LS = L + L / 16 + 1; };   // sequence stride (odd)
-
-// One Stockham radix-R stage, LDS -> LDS, for sequence s, thread t (T = L/16 threads per
-// sequence, each owning butterflies j = t + b*T, b < 16/R). Caller provides the barriers.
-template <int L, int R, int NS>
-__device__ __forceinline__ void stage_lds(float2* seq, const float2* __restrict__ tw, int t) {
-    constexpr int T = L / 16;
-    constexpr int BPT = 16 / R;
-    float2 v[BPT][R];
-#pragma unroll
-    for (int b = 0; b < BPT; b++) {
-        const int j = t + b * T;
-#pragma unroll
-        for (int r = 0; r < R; r++) v[b][r] = seq[pad16(j + r * (L / R))];
-        const int jm = j % NS;
-#pragma unroll
-        for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw[r * jm * (L / (NS * R))]);
-        dft<R>(v[b]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int b = 0; b < BPT; b++) {
-        const int j = t + b * T;
-        const int idxD = (j / NS) * NS * R + (j % NS);
-#pragma unroll
-        for (int r = 0; r < R; r++) seq[pad16(idxD + r * NS)] = v[b][r];
-    }
-    __syncthreads();
-}
-
-// Last stage: LDS -> registers -> store functor (output index k, value).
-template <int L, int R, int NS, class Store>
-__device__ __forceinline__ void stage_last(const float2* seq, const float2* __restrict__ tw, int t, Store&& st) {
-    constexpr int T = L / 16;
-    constexpr int BPT = 16 / R;
-    float2 v[BPT][R];
-#pragma unroll
-    for (int b = 0; b < BPT; b++) {
-        const int j = t + b * T;
-#pragma unroll
-        for (int r = 0; r < R; r++) v[b][r] = seq[pad16(j + r * (L / R))];
-        const int jm = j % NS;
-#pragma unroll
-        for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw[r * jm * (L / (NS * R))]);
-        dft<R>(v[b]);
-    }
-#pragma unroll
-    for (int b = 0; b < BPT; b++) {
-        const int j = t + b * T;
-        const int idxD = (j / NS) * NS * R + (j % NS);
-#pragma unroll
-        for (int r = 0; r < R; r++) st(idxD + r * NS, v[b][r]);
-    }
-}
-
-// Stage 1 of a length-L Stockham FFT on a thread's 16 register values (radix 16, NS = 1,
-// no twiddles), written to the sequence's LDS image.
-template <int L>
-__device__ __forceinline__ void stage_first(float2* seq, float2 (&v)[16], int t) {
-    dft16(v);
-#pragma unroll
-    for (int r = 0; r < 16; r++) seq[pad16(t * 16 + r)] = v[r];
-}
-
-// Stages after the first: LDS -> ... -> store functor. Expects stage_first's LDS writes
-// to be complete (caller's barrier); leaves the LDS free for reuse on return.
-template <int L, class Store>
-__device__ __forceinline__ void stages_rest(float2* lds, const float2* __restrict__ tw, int sL, int tL, Store&& st) {
-    constexpr int LS = Lds<L>::LS;
-    const float2* seqL = lds + sL * LS;
-    if constexpr (L == 64) {
-        stage_last<L, 4, 16>(seqL, tw, tL, st);
-    } else if constexpr (L == 128) {
-        stage_last<L, 8, 16>(seqL, tw, tL, st);
-    } else if constexpr (L == 256) {
-        stage_last<L, 16, 16>(seqL, tw, tL, st);
-    } else {
-        stage_lds<L, 16, 16>(lds + sL * LS, tw, tL);   // middle stage (radix 16, NS = 16)
-        if constexpr (L == 512) stage_last<L, 2, 256>(seqL, tw, tL, st);
-        else if constexpr (L == 1024) stage_last<L, 4, 256>(seqL, tw, tL, st);
-        else if constexpr (L == 2048) stage_last<L, 8, 256>(seqL, tw, tL, st);
-        else stage_last<L, 16, 256>(seqL, tw, tL, st);
-    }
-}
 
 __device__ __forceinline__ float db_of(float2 X) {
     // volk_32fc_s32f_power_spectrum_32f(out, X, 1.0, N): 10*log10(re^2 + im^2)

@@ -84,13 +84,19 @@ static int estimate_tap_count(double tw, double fs) { return (int)(3.8 * fs / tw
 // taps/windowed_sinc.h:9-35 with the nuttall window; `win` multiplies the
 // window term exactly like the lambdas of high_pass.h / band_pass.h
 template <typename W>
-static void windowed_sinc(int count, double omega, float* out, W win) {
+static void windowed_sinc(int count, double omega, float* out, W win, double norm = 1.0) {
     double half = (double)count / 2.0;
-    double corr = 1.0 * omega / DB_M_PI;
+    double corr = norm * omega / DB_M_PI;
     for (int i = 0; i < count; i++) {
         double t = (double)i - half + 0.5;
         out[i] = (float)(sinc(t * omega) * win(t - half, (double)count) * corr);
     }
+}
+
+int taps_windowed_sinc(int count, double omega, double norm, float* out) {   // windowed_sinc.h:9-35, window::nuttall
+    if (count < 1) { set_error("windowed_sinc: count %d < 1", count); return SDRGPU_EARG; }
+    if (out) windowed_sinc(count, omega, out, [](double n, double N) { return nuttall(n, N); }, norm);
+    return count;
 }
 
 int taps_low_pass(double cutoff, double tw, double fs, int odd, float* out) {   // taps/low_pass.h:7-11

@@ -62,6 +62,7 @@ inline size_t esize(int dtype) { return dtype == SDRGPU_C64 ? 8 : 4; }
 // ---- host-side design (host_design.cpp) -----------------------------------
 double window_value(int type, double n, double N);
 int create_window(int type, float* buffer, int size, int centered);
+int taps_windowed_sinc(int count, double omega, double norm, float* out);
 int taps_low_pass(double cutoff, double tw, double fs, int odd, float* out);
 int taps_high_pass(double cutoff, double tw, double fs, int odd, float* out);
 int taps_band_pass_f(double start, double stop, double tw, double fs, int odd, float* out);

@@ -240,6 +240,26 @@ def _taps(fn, *args):
     return t
 
 
+def windowed_sinc(count, omega, norm=1.0):
+    """taps::windowedSinc<float>(count, omega, window::nuttall, norm) (taps/windowed_sinc.h:9)."""
+    out = np.empty(int(count), np.float32)
+    check(lib.sdrgpu_taps_windowed_sinc(int(count), float(omega), float(norm), _fptr(out)))
+    return out
+
+
+class PolyphaseChannelizer(Block):
+    """M-channel critically sampled polyphase channelizer (BASELINE C4): channel k of frame m is
+    FrequencyXlator(-k fs/M) -> DecimatingFIR(taps, M) with an exact NCO. ``process`` returns
+    complex64 [frames * M] laid out out[m * M + k]."""
+
+    def __init__(self, channels, taps, device=0):
+        t = np.ascontiguousarray(taps, np.float32)
+        self._taps = t
+        self.channels = int(channels)
+        h = _make(lib.sdrgpu_channelizer_create, device, int(channels), _fptr(t), int(t.shape[0]))
+        super().__init__(h, np.complex64, np.complex64)
+
+
 def low_pass(cutoff, trans, fs, odd=False):
     return _taps(lib.sdrgpu_taps_low_pass, float(cutoff), float(trans), float(fs), int(odd))
 
