@@ -120,6 +120,30 @@ int sdrgpu_ddc_fm_create(sdrgpu_block** h, int device, double offsetRad, const f
 /* FM<float> (demod/fm.h) and BroadcastFM mono (stereo_t out, broadcast_fm.h) */
 int sdrgpu_fm_create(sdrgpu_block** h, int device, double samplerate, double bandwidth, int lowPass, int highPass);
 int sdrgpu_wfm_create(sdrgpu_block** h, int device, double deviation, double samplerate, int lowPass);
+/* Serial loops (one workgroup per stream; bit-identical to the reference arithmetic) */
+/* loop::AGC<T> (loop/agc.h:13-147); dtype F32 or C64; setGain latched at the next process() */
+int sdrgpu_agc_create(sdrgpu_block** h, int device, int dtype, double setPoint, double attack, double decay,
+                      double maxGain, double maxOutputAmp, double initGain);
+int sdrgpu_agc_set_params(sdrgpu_block* h, double setPoint, double attack, double decay, double maxGain,
+                          double maxOutputAmp, double initGain);   /* agc.h:44-79 setters (state kept) */
+int sdrgpu_agc_set_enabled(sdrgpu_block* h, int enabled);      /* agc.h:38 */
+int sdrgpu_agc_set_gain(sdrgpu_block* h, float gain);          /* agc.h:31 */
+int sdrgpu_agc_get_gain(sdrgpu_block* h, float* gain);         /* agc.h:28 (synchronises) */
+/* correction::DCBlocker<T> (correction/dc_blocker.h:17-60); rate = rate_hz / samplerate */
+int sdrgpu_dc_blocker_create(sdrgpu_block** h, int device, int dtype, double rate);
+int sdrgpu_dc_blocker_set_rate(sdrgpu_block* h, double rate);   /* dc_blocker.h:30 (also on an AM handle) */
+/* demod::AM<T> (demod/am.h:27-142): agcMode 0 OFF, 1 CARRIER, 2 AUDIO; stereo != 0 -> stereo_t out */
+int sdrgpu_am_create(sdrgpu_block** h, int device, int agcMode, double bandwidth, double agcAttack, double agcDecay,
+                     double dcBlockRate, double samplerate, int stereo);
+/* demod::SSB<T> (demod/ssb.h:20-105): mode 0 USB, 1 LSB, 2 DSB; stereo != 0 -> stereo_t out */
+int sdrgpu_ssb_create(sdrgpu_block** h, int device, int mode, double bandwidth, double samplerate, int agcEnabled,
+                      double agcAttack, double agcDecay, int stereo);
+/* AGC inside an AM / SSB handle: which 0 = first AGC (AM carrier AGC, SSB AGC), 1 = last (AM audio AGC);
+ * am.h:63-97 setAGCGain/getAGCGain/setAGCAttack/setAGCDecay, ssb.h:62-84 */
+int sdrgpu_demod_agc_set_gain(sdrgpu_block* h, int which, float gain);
+int sdrgpu_demod_agc_get_gain(sdrgpu_block* h, int which, float* gain);
+int sdrgpu_demod_agc_set_enabled(sdrgpu_block* h, int which, int enabled);
+int sdrgpu_demod_agc_set_attack_decay(sdrgpu_block* h, double attack, double decay);
 /* M-channel critically sampled polyphase channelizer (BASELINE C4): channel k of output frame
  * m is FrequencyXlator(-k fs/M) -> DecimatingFIR<complex_t,float>(taps, M) (frequency_xlator.h:43,
  * decimating_fir.h:45) with an exact NCO; taps <= 16 M (bank layout polyphase_bank.h:32).

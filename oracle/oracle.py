@@ -80,6 +80,8 @@ def _load():
         "orc_agc_set_enabled": (None, [vp, i]),
         "orc_agc_process": (i, [vp, vp, i, vp]),
         "orc_agc_destroy": (None, [vp]),
+        "orc_agc_set_gain": (None, [vp, ctypes.c_float]),
+        "orc_agc_get_gain": (ctypes.c_float, [vp]),
         "orc_dcb_create": (vp, [i, d]),
         "orc_dcb_process": (i, [vp, vp, i, vp]),
         "orc_dcb_destroy": (None, [vp]),
@@ -364,6 +366,27 @@ class AGC(_Obj):
 
     def process(self, x):
         return super().process(x, lib.orc_agc_process)
+
+    def set_enabled(self, en):
+        lib.orc_agc_set_enabled(self._h, int(bool(en)))
+
+    def set_gain(self, g):
+        lib.orc_agc_set_gain(self._h, float(g))
+
+    def get_gain(self):
+        return lib.orc_agc_get_gain(self._h)
+
+
+class DCBlocker(_Obj):
+    """correction/dc_blocker.h:54-60"""
+    _destroy = lib.orc_dcb_destroy
+
+    def __init__(self, rate, complex_data=False):
+        dt = np.complex64 if complex_data else np.float32
+        super().__init__(lib.orc_dcb_create(C64 if complex_data else F32, float(rate)), dt, dt)
+
+    def process(self, x):
+        return super().process(x, lib.orc_dcb_process)
 
 
 class AM(_Obj):

@@ -677,6 +677,8 @@ orc_agc* orc_agc_create(int dtype, double setPoint, double attack, double decay,
     return a;
 }
 void orc_agc_set_enabled(orc_agc* a, int en) { a->enabled = en; }
+void orc_agc_set_gain(orc_agc* a, float g) { a->gain = g; }   /* agc.h:31-35 */
+float orc_agc_get_gain(orc_agc* a) { return a->gain; }
 static float amp_of(const float* x, int dtype, int i) {
     if (dtype == ORC_C64) { float re = x[2 * i], im = x[2 * i + 1]; return sqrtf((re * re) + (im * im)); }
     return fabsf(x[i]);

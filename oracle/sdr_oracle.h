@@ -120,6 +120,8 @@ void orc_fm_destroy(orc_fm* f);
 typedef struct orc_agc orc_agc;              /* loop/agc.h */
 orc_agc* orc_agc_create(int dtype, double setPoint, double attack, double decay, double maxGain, double maxOutputAmp, double initGain);
 void orc_agc_set_enabled(orc_agc* a, int en);
+void orc_agc_set_gain(orc_agc* a, float g);
+float orc_agc_get_gain(orc_agc* a);
 int  orc_agc_process(orc_agc* a, const float* in, int count, float* out);
 void orc_agc_destroy(orc_agc* a);
 

@@ -84,6 +84,13 @@ def _load():
         "sdrgpu_fm_create": (i, [pp, i, d, d, i, i]),
         "sdrgpu_wfm_create": (i, [pp, i, d, d, i]),
         "sdrgpu_channelizer_create": (i, [pp, i, i, fp, i]),
+        "sdrgpu_agc_create": (i, [pp, i, i, d, d, d, d, d, d]),
+        "sdrgpu_agc_set_enabled": (i, [vp, i]),
+        "sdrgpu_agc_set_gain": (i, [vp, ctypes.c_float]),
+        "sdrgpu_agc_get_gain": (i, [vp, ctypes.POINTER(ctypes.c_float)]),
+        "sdrgpu_dc_blocker_create": (i, [pp, i, i, d]),
+        "sdrgpu_am_create": (i, [pp, i, i, d, d, d, d, d, i]),
+        "sdrgpu_ssb_create": (i, [pp, i, i, d, d, i, d, d, i]),
         "sdrgpu_block_process": (i, [vp, vp, i, vp]),
         "sdrgpu_block_process_dev": (i, [vp, vp, i, vp, vp]),
         "sdrgpu_block_out_count": (i, [vp, i]),

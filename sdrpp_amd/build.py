@@ -24,6 +24,7 @@ SOURCES = [
     ("fft.hip", []),
     ("blocks.hip", []),
     ("channelizer.hip", []),
+    ("loops.hip", ["-ffp-contract=off"]),   # bit-exact serial recurrences
 ]
 
 

@@ -785,6 +785,40 @@ static std::unique_ptr<FirBlock> make_fir(int dev, int dtype, int ttype, const f
     return f;
 }
 
+// composition helpers for other translation units (loops.hip)
+int chain_new(int dev, int in_dtype, int out_dtype, Block** out) {
+    auto* c = new ChainBlock();
+    c->device = dev; c->in_dtype = in_dtype; c->out_dtype = out_dtype;
+    const int rc = c->init_stream();
+    if (rc < 0) { delete c; return rc; }
+    *out = c;
+    return SDRGPU_OK;
+}
+int chain_append(Block* chain, Block* kid) {
+    auto* c = dynamic_cast<ChainBlock*>(chain);
+    if (!c || !kid) { delete kid; set_error("chain_append: bad argument"); return SDRGPU_EARG; }
+    c->kids.emplace_back(kid);
+    return SDRGPU_OK;
+}
+int chain_size(Block* chain) {
+    auto* c = dynamic_cast<ChainBlock*>(chain);
+    return c ? (int)c->kids.size() : -1;
+}
+Block* chain_kid(Block* chain, int i) {
+    auto* c = dynamic_cast<ChainBlock*>(chain);
+    return (c && i >= 0 && i < (int)c->kids.size()) ? c->kids[i].get() : nullptr;
+}
+Block* make_fir_block(int dev, int dtype, int ttype, const float* taps, int n, int decim, bool stereo, int* rc) {
+    return make_fir(dev, dtype, ttype, taps, n, decim, rc, false, 0.0, false, 1.0f, stereo).release();
+}
+Block* make_xlator_block(int dev, double offsetRad, int* rc) {
+    auto* x = new XlatorBlock();
+    x->device = dev;
+    *rc = x->init_stream();
+    if (*rc >= 0) *rc = x->nco.set_w(xlator_effective_omega(offsetRad));
+    return x;
+}
+
 // PowerDecimator<T> (multirate/power_decimator.h): cascade of plan stages. With
 // `xlFirst` the RxVFO's xlator is fused into the first (full-rate) stage.
 static int build_power_decim(ChainBlock* c, int dev, int dtype, int ratio, bool xlFirst, double w) {

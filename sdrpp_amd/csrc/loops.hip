@@ -1,0 +1,503 @@
+// Serial (data-dependent) loops of the demodulators and the blocks composed from them:
+//   loop::AGC<T>           loop/agc.h:88-147
+//   correction::DCBlocker  correction/dc_blocker.h:54-60
+//   demod::AM<T>           demod/am.h:114-142     ([carrier AGC] -> |x| -> DC block -> [audio AGC] -> LPF)
+//   demod::SSB<T>          demod/ssb.h:90-105     (xlate +-bw/2 -> Re -> AGC)
+//
+// The AGC and the DC blocker are first-order recurrences whose next state depends on the
+// current sample (the AGC nonlinearly), so they run as ONE workgroup per stream: the block is
+// walked in 1024-sample chunks; all 256 lanes stage the chunk (and, for the AGC, its
+// amplitudes and the exact suffix maxima its clip look-ahead needs) in LDS, lane 0 runs the
+// recurrence over the chunk from LDS, and all lanes write the chunk out. This file is compiled
+// with -ffp-contract=off (sdrpp_amd/build.py: HIP contracts a*b+c into an FMA by default),
+// every step is written in the
+// reference's order, and division / square root are IEEE (correctly rounded), so the GPU
+// result is bit-identical to the reference arithmetic (oracle/sdr_oracle.c orc_agc / orc_dcb).
+//
+// The AGC's clip look-ahead scans amplitudes from sample i to the end of the CURRENT block
+// (agc.h:109-118; O(n^2) worst case in the reference). The suffix maximum over the block is
+// precomputed in parallel (max is exact), so the serial loop is O(n) and the result is the
+// same value. State (average amplitude, gain; DC offset) stays on the device between calls.
+#include <algorithm>
+#include <cmath>
+#include <memory>
+#include <vector>
+#include "sdrgpu_internal.h"
+
+namespace sdrgpu {
+
+constexpr int LOOP_CHUNK = 1024;
+constexpr int LOOP_NT = 256;
+
+// |x| exactly as complex_t::amplitude() (types.h:79) / fabsf, no contraction
+__device__ __forceinline__ float amp_of(float x) { return fabsf(x); }
+// (sqrtf is correctly rounded under HIP's default -fhip-fp32-correctly-rounded-divide-sqrt;
+// __fsqrt_rn is the native approximation unless OCML_BASIC_ROUNDED_OPERATIONS is defined)
+__device__ __forceinline__ float amp_of(float2 x) { return sqrtf((x.x * x.x) + (x.y * x.y)); }
+__device__ __forceinline__ float scale_of(float x, float g) { return x * g; }
+__device__ __forceinline__ float2 scale_of(float2 x, float g) { return make_float2(x.x * g, x.y * g); }
+
+struct AgcParams {
+    float setPoint, attack, invAttack, decay, invDecay, maxGain, maxOutputAmp;
+    int enabled;
+};
+struct AgcState {
+    float amp, gain;
+};
+
+// per-chunk amplitude maxima (exact), one workgroup per chunk
+template <typename DT>
+__global__ __launch_bounds__(LOOP_NT) void chunk_max_kernel(const DT* __restrict__ in, int count, float* __restrict__ cm) {
+    __shared__ float red[LOOP_NT];
+    const int c = blockIdx.x;
+    float m = 0.0f;
+    for (int i = c * LOOP_CHUNK + threadIdx.x; i < min(count, (c + 1) * LOOP_CHUNK); i += LOOP_NT) m = fmaxf(m, amp_of(in[i]));
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int s = LOOP_NT / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) cm[c] = red[0];
+}
+
+// One workgroup: the whole block, chunk by chunk. `cm` holds the chunk maxima on entry.
+template <typename DT>
+__global__ __launch_bounds__(LOOP_NT) void agc_kernel(const DT* __restrict__ in, DT* __restrict__ out, int count,
+                                                      AgcParams p, AgcState* __restrict__ st, float* __restrict__ cm,
+                                                      const float* __restrict__ setGain) {
+    __shared__ DT X[LOOP_CHUNK];
+    __shared__ float A[LOOP_CHUNK], S[LOOP_CHUNK], G[LOOP_CHUNK];
+    const int t = threadIdx.x;
+    const int nchunks = (count + LOOP_CHUNK - 1) / LOOP_CHUNK;
+    if (t == 0) {   // cm[c] <- max over chunks > c (the look-ahead beyond chunk c)
+        float run = 0.0f;
+        for (int c = nchunks - 1; c >= 0; c--) {
+            const float v = cm[c];
+            cm[c] = run;
+            run = fmaxf(run, v);
+        }
+    }
+    __syncthreads();
+    float amp = st->amp, gain = st->gain;
+    if (setGain) gain = *setGain;                          // AGC::setGain latched at this call
+    for (int c = 0; c < nchunks; c++) {
+        const int i0 = c * LOOP_CHUNK;
+        const int n = min(LOOP_CHUNK, count - i0);
+        for (int i = t; i < LOOP_CHUNK; i += LOOP_NT) {
+            if (i < n) {
+                const DT v = in[i0 + i];
+                X[i] = v;
+                A[i] = amp_of(v);
+            } else {
+                A[i] = 0.0f;
+            }
+        }
+        __syncthreads();
+        if (p.enabled) {
+            // S[i] = max(A[i..n-1], beyond): Hillis-Steele suffix max, exact
+            for (int i = t; i < LOOP_CHUNK; i += LOOP_NT) S[i] = (i == n - 1) ? fmaxf(A[i], cm[c]) : A[i];
+            __syncthreads();
+            for (int d = 1; d < LOOP_CHUNK; d <<= 1) {
+                float v[LOOP_CHUNK / LOOP_NT];
+#pragma unroll
+                for (int k = 0; k < LOOP_CHUNK / LOOP_NT; k++) {
+                    const int i = t + k * LOOP_NT;
+                    v[k] = (i + d < n) ? fmaxf(S[i], S[i + d]) : S[i];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < LOOP_CHUNK / LOOP_NT; k++) S[t + k * LOOP_NT] = v[k];
+                __syncthreads();
+            }
+        }
+        if (t == 0) {
+            if (p.enabled) {
+                for (int i = 0; i < n; i++) {
+                    const float inAmp = A[i];
+                    if (inAmp != 0.0f) {
+                        amp = (inAmp > amp) ? ((amp * p.invAttack) + (inAmp * p.attack))
+                                            : ((amp * p.invDecay) + (inAmp * p.decay));
+                        const float q = p.setPoint / amp;
+                        gain = (p.maxGain < q) ? p.maxGain : q;              // std::min<float>
+                    } else {
+                        gain = 1.0f;
+                    }
+                    if (inAmp * gain > p.maxOutputAmp) {                     // clip look-ahead
+                        amp = S[i];
+                        const float q = p.setPoint / amp;
+                        gain = (p.maxGain < q) ? p.maxGain : q;
+                    }
+                    G[i] = gain;
+                }
+            } else {
+                for (int i = 0; i < n; i++) {
+                    const float inAmp = A[i];
+                    G[i] = (inAmp * gain > p.maxOutputAmp) ? (p.maxOutputAmp / inAmp) : gain;
+                }
+            }
+        }
+        __syncthreads();
+        for (int i = t; i < n; i += LOOP_NT) out[i0 + i] = scale_of(X[i], G[i]);
+        __syncthreads();
+    }
+    if (t == 0) {
+        st->amp = amp;
+        st->gain = gain;
+    }
+}
+
+// DC blocker (dc_blocker.h:54-60): out = in - off; off += out * rate, per component
+template <typename DT>
+__global__ __launch_bounds__(LOOP_NT) void dcb_kernel(const DT* __restrict__ in, DT* __restrict__ out, int count,
+                                                      float rate, float2* __restrict__ st) {
+    __shared__ DT X[LOOP_CHUNK];
+    const int t = threadIdx.x;
+    float2 off = *st;
+    for (int i0 = 0; i0 < count; i0 += LOOP_CHUNK) {
+        const int n = min(LOOP_CHUNK, count - i0);
+        for (int i = t; i < n; i += LOOP_NT) X[i] = in[i0 + i];
+        __syncthreads();
+        if (t == 0) {
+            for (int i = 0; i < n; i++) {
+                if constexpr (sizeof(DT) == 4) {
+                    const float o = X[i] - off.x;
+                    off.x += o * rate;
+                    X[i] = o;
+                } else {
+                    const float2 v = X[i];
+                    const float ox = v.x - off.x, oy = v.y - off.y;
+                    off.x += ox * rate;
+                    off.y += oy * rate;
+                    X[i] = make_float2(ox, oy);
+                }
+            }
+        }
+        __syncthreads();
+        for (int i = t; i < n; i += LOOP_NT) out[i0 + i] = X[i];
+        __syncthreads();
+    }
+    if (t == 0) *st = off;
+}
+
+// volk_32fc_magnitude_32f (AM) / ComplexToReal (SSB) / MonoToStereo
+__global__ void magnitude_kernel(const float2* __restrict__ in, float* __restrict__ out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = amp_of(in[i]);
+}
+__global__ void real_part_kernel(const float2* __restrict__ in, float* __restrict__ out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = in[i].x;
+}
+__global__ void mono_to_stereo_kernel(const float* __restrict__ in, float2* __restrict__ out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = make_float2(in[i], in[i]);
+}
+
+// ---------------------------------------------------------------- blocks
+struct AgcBlock : Block {
+    AgcParams p{};
+    float initGain = 1.0f;
+    DevBuf state, cm, pend;
+    bool pending = false;
+    float pendingGain = 0.0f;
+    int setup(int dev, int dtype, double setPoint, double attack, double decay, double maxGain, double maxOutputAmp,
+              double initGain_) {
+        device = dev;
+        in_dtype = out_dtype = dtype;
+        // AGC::init (agc.h:13-26): members are float
+        p.setPoint = (float)setPoint;
+        p.attack = (float)attack;
+        p.invAttack = 1.0f - p.attack;
+        p.decay = (float)decay;
+        p.invDecay = 1.0f - p.decay;
+        p.maxGain = (float)maxGain;
+        p.maxOutputAmp = (float)maxOutputAmp;
+        initGain = (float)initGain_;
+        p.enabled = 1;
+        SDRGPU_CHECK(init_stream());
+        SDRGPU_CHECK(state.ensure(sizeof(AgcState)));
+        SDRGPU_CHECK(pend.ensure(sizeof(float)));
+        return reset();
+    }
+    int out_count(int count) override { return count; }
+    int reset() override {   // agc.h:81-86
+        SDRGPU_SET_DEVICE(device);
+        AgcState s;
+        s.amp = p.setPoint / initGain;
+        s.gain = (p.maxGain < initGain) ? p.maxGain : initGain;
+        SDRGPU_HIP(hipMemcpy(state.p, &s, sizeof(s), hipMemcpyHostToDevice));
+        pending = false;
+        return SDRGPU_OK;
+    }
+    int set_gain(float g) {   // agc.h:31-35, applied at the next process()
+        SDRGPU_SET_DEVICE(device);
+        SDRGPU_HIP(hipMemcpy(pend.p, &g, sizeof(g), hipMemcpyHostToDevice));
+        pending = true;
+        pendingGain = g;
+        return SDRGPU_OK;
+    }
+    int run(const void* in, int count, void* out, hipStream_t s) override {
+        if (count < 0) { set_error("agc: negative count"); return SDRGPU_EARG; }
+        SDRGPU_SET_DEVICE(device);
+        const float* pg = pending ? pend.as<float>() : nullptr;
+        pending = false;
+        if (count == 0 && !pg) return 0;
+        const int nchunks = std::max(1, (count + LOOP_CHUNK - 1) / LOOP_CHUNK);
+        SDRGPU_CHECK(cm.ensure(sizeof(float) * nchunks));
+        if (in_dtype == SDRGPU_C64) {
+            if (count > 0 && p.enabled)
+                hipLaunchKernelGGL(chunk_max_kernel<float2>, dim3(nchunks), dim3(LOOP_NT), 0, s, (const float2*)in, count, cm.as<float>());
+            hipLaunchKernelGGL(agc_kernel<float2>, dim3(1), dim3(LOOP_NT), 0, s, (const float2*)in, (float2*)out, count, p,
+                               state.as<AgcState>(), cm.as<float>(), pg);
+        } else {
+            if (count > 0 && p.enabled)
+                hipLaunchKernelGGL(chunk_max_kernel<float>, dim3(nchunks), dim3(LOOP_NT), 0, s, (const float*)in, count, cm.as<float>());
+            hipLaunchKernelGGL(agc_kernel<float>, dim3(1), dim3(LOOP_NT), 0, s, (const float*)in, (float*)out, count, p,
+                               state.as<AgcState>(), cm.as<float>(), pg);
+        }
+        SDRGPU_HIP(hipGetLastError());
+        return count;
+    }
+};
+
+struct DcbBlock : Block {
+    float rate = 0.0f;
+    DevBuf state;
+    int setup(int dev, int dtype, double r) {
+        device = dev;
+        in_dtype = out_dtype = dtype;
+        rate = (float)r;
+        SDRGPU_CHECK(init_stream());
+        SDRGPU_CHECK(state.ensure(sizeof(float2)));
+        return reset();
+    }
+    int out_count(int count) override { return count; }
+    int reset() override {
+        SDRGPU_SET_DEVICE(device);
+        SDRGPU_HIP(hipMemset(state.p, 0, sizeof(float2)));
+        return SDRGPU_OK;
+    }
+    int run(const void* in, int count, void* out, hipStream_t s) override {
+        if (count < 0) { set_error("dc_blocker: negative count"); return SDRGPU_EARG; }
+        if (count == 0) return 0;
+        SDRGPU_SET_DEVICE(device);
+        if (in_dtype == SDRGPU_C64)
+            hipLaunchKernelGGL(dcb_kernel<float2>, dim3(1), dim3(LOOP_NT), 0, s, (const float2*)in, (float2*)out, count, rate, state.as<float2>());
+        else
+            hipLaunchKernelGGL(dcb_kernel<float>, dim3(1), dim3(LOOP_NT), 0, s, (const float*)in, (float*)out, count, rate, state.as<float2>());
+        SDRGPU_HIP(hipGetLastError());
+        return count;
+    }
+};
+
+// elementwise converters used inside the demod chains
+struct MapBlock : Block {
+    int kind = 0;   // 0 magnitude (c64 -> f32), 1 real part (c64 -> f32), 2 mono -> stereo (f32 -> c64)
+    int out_count(int count) override { return count; }
+    int reset() override { return SDRGPU_OK; }
+    int run(const void* in, int count, void* out, hipStream_t s) override {
+        if (count <= 0) return count < 0 ? SDRGPU_EARG : 0;
+        SDRGPU_SET_DEVICE(device);
+        const dim3 g((count + 255) / 256), b(256);
+        if (kind == 0) hipLaunchKernelGGL(magnitude_kernel, g, b, 0, s, (const float2*)in, (float*)out, count);
+        else if (kind == 1) hipLaunchKernelGGL(real_part_kernel, g, b, 0, s, (const float2*)in, (float*)out, count);
+        else hipLaunchKernelGGL(mono_to_stereo_kernel, g, b, 0, s, (const float*)in, (float2*)out, count);
+        SDRGPU_HIP(hipGetLastError());
+        return count;
+    }
+};
+
+static std::unique_ptr<MapBlock> make_map(int dev, int kind) {
+    auto m = std::make_unique<MapBlock>();
+    m->device = dev;
+    m->kind = kind;
+    m->in_dtype = kind == 2 ? SDRGPU_F32 : SDRGPU_C64;
+    m->out_dtype = kind == 2 ? SDRGPU_C64 : SDRGPU_F32;
+    return m;
+}
+
+// A chain of blocks run back to back on one stream (defined in blocks.hip)
+int chain_new(int dev, int in_dtype, int out_dtype, Block** out);
+int chain_append(Block* chain, Block* kid);
+int chain_size(Block* chain);
+Block* chain_kid(Block* chain, int i);
+Block* make_fir_block(int dev, int dtype, int ttype, const float* taps, int n, int decim, bool stereo, int* rc);
+Block* make_xlator_block(int dev, double offsetRad, int* rc);
+
+}  // namespace sdrgpu
+
+using namespace sdrgpu;
+
+namespace {
+int wrap_block(sdrgpu_block** h, Block* b, int rc) {
+    if (rc < 0) { delete b; return rc; }
+    *h = new sdrgpu_block{b};
+    return SDRGPU_OK;
+}
+}  // namespace
+
+extern "C" int sdrgpu_agc_create(sdrgpu_block** h, int device, int dtype, double setPoint, double attack, double decay,
+                                 double maxGain, double maxOutputAmp, double initGain) {
+    if (!h || (dtype != SDRGPU_F32 && dtype != SDRGPU_C64)) { set_error("agc_create: bad argument"); return SDRGPU_EARG; }
+    auto* a = new AgcBlock();
+    return wrap_block(h, a, a->setup(device, dtype, setPoint, attack, decay, maxGain, maxOutputAmp, initGain));
+}
+// AGC setters (agc.h:44-79): parameters change, the running amplitude / gain are kept
+extern "C" int sdrgpu_agc_set_params(sdrgpu_block* h, double setPoint, double attack, double decay, double maxGain,
+                                     double maxOutputAmp, double initGain) {
+    auto* a = h ? dynamic_cast<AgcBlock*>(h->impl) : nullptr;
+    if (!a) { set_error("not an AGC"); return SDRGPU_EARG; }
+    a->p.setPoint = (float)setPoint;
+    a->p.attack = (float)attack;
+    a->p.invAttack = 1.0f - a->p.attack;
+    a->p.decay = (float)decay;
+    a->p.invDecay = 1.0f - a->p.decay;
+    a->p.maxGain = (float)maxGain;
+    a->p.maxOutputAmp = (float)maxOutputAmp;
+    a->initGain = (float)initGain;
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_agc_set_enabled(sdrgpu_block* h, int enabled) {
+    auto* a = h ? dynamic_cast<AgcBlock*>(h->impl) : nullptr;
+    if (!a) { set_error("not an AGC"); return SDRGPU_EARG; }
+    a->p.enabled = enabled ? 1 : 0;
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_agc_set_gain(sdrgpu_block* h, float gain) {
+    auto* a = h ? dynamic_cast<AgcBlock*>(h->impl) : nullptr;
+    if (!a) { set_error("not an AGC"); return SDRGPU_EARG; }
+    return a->set_gain(gain);
+}
+extern "C" int sdrgpu_agc_get_gain(sdrgpu_block* h, float* gain) {
+    auto* a = h ? dynamic_cast<AgcBlock*>(h->impl) : nullptr;
+    if (!a || !gain) { set_error("agc_get_gain: bad argument"); return SDRGPU_EARG; }
+    if (a->pending) { *gain = a->pendingGain; return SDRGPU_OK; }
+    SDRGPU_SET_DEVICE(a->device);
+    AgcState s;
+    SDRGPU_HIP(hipDeviceSynchronize());   // (UI-rate query: waits for the block's queued work)
+    SDRGPU_HIP(hipMemcpy(&s, a->state.p, sizeof(s), hipMemcpyDeviceToHost));
+    *gain = s.gain;
+    return SDRGPU_OK;
+}
+
+extern "C" int sdrgpu_dc_blocker_create(sdrgpu_block** h, int device, int dtype, double rate) {
+    if (!h || (dtype != SDRGPU_F32 && dtype != SDRGPU_C64)) { set_error("dc_blocker_create: bad argument"); return SDRGPU_EARG; }
+    auto* d = new DcbBlock();
+    return wrap_block(h, d, d->setup(device, dtype, rate));
+}
+
+// demod::AM<T> (am.h:27-49, 114-142): agcMode 0 OFF, 1 CARRIER, 2 AUDIO; stereo -> stereo_t out
+extern "C" int sdrgpu_am_create(sdrgpu_block** h, int device, int agcMode, double bandwidth, double agcAttack,
+                                double agcDecay, double dcBlockRate, double samplerate, int stereo) {
+    if (!h || agcMode < 0 || agcMode > 2) { set_error("am_create: bad argument"); return SDRGPU_EARG; }
+    Block* c = nullptr;
+    int rc = chain_new(device, SDRGPU_C64, stereo ? SDRGPU_C64 : SDRGPU_F32, &c);
+    if (rc < 0) return rc;
+    if (agcMode == 1) {
+        auto* a = new AgcBlock();
+        rc = a->setup(device, SDRGPU_C64, 1.0, agcAttack, agcDecay, 10e6, 10.0, INFINITY);
+        if (rc >= 0) rc = chain_append(c, a); else delete a;
+    }
+    if (rc >= 0) rc = chain_append(c, make_map(device, 0).release());
+    if (rc >= 0) {
+        auto* d = new DcbBlock();
+        rc = d->setup(device, SDRGPU_F32, dcBlockRate);
+        if (rc >= 0) rc = chain_append(c, d); else delete d;
+    }
+    if (rc >= 0 && agcMode != 1) {   // audioAgc runs unless CARRIER; enabled only for AUDIO
+        auto* a = new AgcBlock();
+        rc = a->setup(device, SDRGPU_F32, 1.0, agcAttack, agcDecay, 10e6, 10.0, INFINITY);
+        if (rc >= 0) { a->p.enabled = agcMode == 2; rc = chain_append(c, a); } else delete a;
+    }
+    if (rc >= 0) {
+        const double fc = bandwidth / 2.0;
+        const int n = taps_low_pass(fc, fc * 0.1, samplerate, 0, nullptr);
+        rc = n < 1 ? (n < 0 ? n : SDRGPU_EARG) : SDRGPU_OK;
+        if (rc >= 0) {
+            std::vector<float> t(n);
+            taps_low_pass(fc, fc * 0.1, samplerate, 0, t.data());
+            Block* f = make_fir_block(device, SDRGPU_F32, SDRGPU_F32, t.data(), n, 1, stereo != 0, &rc);
+            if (rc >= 0) rc = chain_append(c, f); else delete f;
+        }
+    }
+    return wrap_block(h, c, rc);
+}
+
+// demod::SSB<T> (ssb.h:27-105): mode 0 USB, 1 LSB, 2 DSB
+extern "C" int sdrgpu_ssb_create(sdrgpu_block** h, int device, int mode, double bandwidth, double samplerate,
+                                 int agcEnabled, double agcAttack, double agcDecay, int stereo) {
+    if (!h || mode < 0 || mode > 2) { set_error("ssb_create: bad argument"); return SDRGPU_EARG; }
+    Block* c = nullptr;
+    int rc = chain_new(device, SDRGPU_C64, stereo ? SDRGPU_C64 : SDRGPU_F32, &c);
+    if (rc < 0) return rc;
+    const double tr = mode == 0 ? bandwidth / 2.0 : (mode == 1 ? -bandwidth / 2.0 : 0.0);   // getTranslation
+    Block* x = make_xlator_block(device, hz_to_rads(tr, samplerate), &rc);
+    if (rc >= 0) rc = chain_append(c, x); else delete x;
+    if (rc >= 0) rc = chain_append(c, make_map(device, 1).release());
+    if (rc >= 0) {
+        auto* a = new AgcBlock();
+        rc = a->setup(device, SDRGPU_F32, 1.0, agcAttack, agcDecay, 10e6, 10.0, INFINITY);
+        if (rc >= 0) { a->p.enabled = agcEnabled ? 1 : 0; rc = chain_append(c, a); } else delete a;
+    }
+    if (rc >= 0 && stereo) rc = chain_append(c, make_map(device, 2).release());
+    return wrap_block(h, c, rc);
+}
+
+// AGC access inside the AM / SSB chains: `which` 0 = the first AGC of the chain (AM carrier
+// AGC in CARRIER mode, the SSB AGC), 1 = the last (AM audio AGC)
+static AgcBlock* demod_agc(sdrgpu_block* h, int which) {
+    if (!h || !h->impl) return nullptr;
+    const int n = chain_size(h->impl);
+    AgcBlock* found = nullptr;
+    for (int i = 0; i < n; i++) {
+        auto* a = dynamic_cast<AgcBlock*>(chain_kid(h->impl, i));
+        if (a) {
+            found = a;
+            if (which == 0) break;
+        }
+    }
+    return found;
+}
+extern "C" int sdrgpu_demod_agc_set_gain(sdrgpu_block* h, int which, float gain) {
+    AgcBlock* a = demod_agc(h, which);
+    if (!a) { set_error("demod has no AGC"); return SDRGPU_ESTATE; }
+    return a->set_gain(gain);
+}
+extern "C" int sdrgpu_demod_agc_get_gain(sdrgpu_block* h, int which, float* gain) {
+    AgcBlock* a = demod_agc(h, which);
+    if (!a) { set_error("demod has no AGC"); return SDRGPU_ESTATE; }
+    sdrgpu_block tmp{a};
+    return sdrgpu_agc_get_gain(&tmp, gain);
+}
+extern "C" int sdrgpu_demod_agc_set_enabled(sdrgpu_block* h, int which, int enabled) {
+    AgcBlock* a = demod_agc(h, which);
+    if (!a) { set_error("demod has no AGC"); return SDRGPU_ESTATE; }
+    a->p.enabled = enabled ? 1 : 0;
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_demod_agc_set_attack_decay(sdrgpu_block* h, double attack, double decay) {
+    if (!h || !h->impl) { set_error("null block handle"); return SDRGPU_EARG; }
+    const int n = chain_size(h->impl);
+    int found = 0;
+    for (int i = 0; i < n; i++) {
+        if (auto* a = dynamic_cast<AgcBlock*>(chain_kid(h->impl, i))) {
+            a->p.attack = (float)attack;
+            a->p.invAttack = 1.0f - a->p.attack;
+            a->p.decay = (float)decay;
+            a->p.invDecay = 1.0f - a->p.decay;
+            found++;
+        }
+    }
+    if (!found) { set_error("demod has no AGC"); return SDRGPU_ESTATE; }
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_dc_blocker_set_rate(sdrgpu_block* h, double rate) {
+    DcbBlock* d = h ? dynamic_cast<DcbBlock*>(h->impl) : nullptr;
+    if (!d && h && h->impl) {   // the AM chain's DC blocker
+        for (int i = 0, n = chain_size(h->impl); i < n && !d; i++) d = dynamic_cast<DcbBlock*>(chain_kid(h->impl, i));
+    }
+    if (!d) { set_error("no DC blocker"); return SDRGPU_ESTATE; }
+    d->rate = (float)rate;
+    return SDRGPU_OK;
+}

@@ -260,6 +260,55 @@ class PolyphaseChannelizer(Block):
         super().__init__(h, np.complex64, np.complex64)
 
 
+class AGC(Block):
+    """dsp::loop::AGC<T> (loop/agc.h); complex_data selects T = complex_t (else float)."""
+
+    def __init__(self, set_point, attack, decay, max_gain, max_output_amp, init_gain=1.0, complex_data=False, device=0):
+        dt = C64 if complex_data else F32
+        h = _make(lib.sdrgpu_agc_create, device, dt, float(set_point), float(attack), float(decay), float(max_gain),
+                  float(max_output_amp), float(init_gain))
+        npd = np.complex64 if complex_data else np.float32
+        super().__init__(h, npd, npd)
+
+    def set_enabled(self, enabled):
+        check(lib.sdrgpu_agc_set_enabled(self._h, int(bool(enabled))))
+
+    def set_gain(self, gain):
+        check(lib.sdrgpu_agc_set_gain(self._h, float(gain)))
+
+    def get_gain(self):
+        g = ctypes.c_float()
+        check(lib.sdrgpu_agc_get_gain(self._h, ctypes.byref(g)))
+        return g.value
+
+
+class DCBlocker(Block):
+    """dsp::correction::DCBlocker<T> (correction/dc_blocker.h); rate in 1/sample."""
+
+    def __init__(self, rate, complex_data=False, device=0):
+        dt = C64 if complex_data else F32
+        npd = np.complex64 if complex_data else np.float32
+        super().__init__(_make(lib.sdrgpu_dc_blocker_create, device, dt, float(rate)), npd, npd)
+
+
+class AM(Block):
+    """dsp::demod::AM<T> (demod/am.h); agc_mode 0 OFF, 1 CARRIER, 2 AUDIO."""
+
+    def __init__(self, agc_mode, bandwidth, attack, decay, dc_rate, samplerate, stereo=False, device=0):
+        h = _make(lib.sdrgpu_am_create, device, int(agc_mode), float(bandwidth), float(attack), float(decay),
+                  float(dc_rate), float(samplerate), int(bool(stereo)))
+        super().__init__(h, np.complex64, STEREO if stereo else np.float32)
+
+
+class SSB(Block):
+    """dsp::demod::SSB<T> (demod/ssb.h); mode 0 USB, 1 LSB, 2 DSB."""
+
+    def __init__(self, mode, bandwidth, samplerate, agc_enabled, attack, decay, stereo=False, device=0):
+        h = _make(lib.sdrgpu_ssb_create, device, int(mode), float(bandwidth), float(samplerate), int(bool(agc_enabled)),
+                  float(attack), float(decay), int(bool(stereo)))
+        super().__init__(h, np.complex64, STEREO if stereo else np.float32)
+
+
 def low_pass(cutoff, trans, fs, odd=False):
     return _taps(lib.sdrgpu_taps_low_pass, float(cutoff), float(trans), float(fs), int(odd))
 

@@ -14,6 +14,10 @@
 #include "dsp/demod/quadrature.h"
 #include "dsp/filter/decimating_fir.h"
 #include "dsp/signal_path/gpu_spectrum.h"
+#include "dsp/correction/dc_blocker.h"
+#include "dsp/demod/am.h"
+#include "dsp/demod/ssb.h"
+#include "dsp/loop/agc.h"
 #include "sdr_oracle.h"
 
 static int failures = 0;
@@ -110,6 +114,58 @@ int main() {
         for (int k = 0; k < 65536; k++) if (ref[k] > peak - 60) err = std::fmax(err, std::fabs(row[k] - ref[k]));
         CHECK(err < 2e-3, "spectrum err %g dB", err);
         std::printf("Spectrum 64k BH7 via handler: max |dB err| within 60 dB of peak %.3g\n", err);
+    }
+    // 4. AM<stereo_t> / SSB<float> / AGC<float> / DCBlocker<float> on 48 kS/s IF (am.h, ssb.h)
+    {
+        const int n = 48000;
+        std::vector<dsp::complex_t> ifx(n);
+        for (int i = 0; i < n; i++) {
+            double t = i / 48000.0, env = 1.0 + 0.5 * std::sin(2 * M_PI * 600 * t);
+            ifx[i] = {(float)(0.05 * env * std::cos(2 * M_PI * 400 * t)), (float)(0.05 * env * std::sin(2 * M_PI * 400 * t))};
+        }
+        dsp::stream<dsp::complex_t> dummy;
+        dsp::demod::AM<dsp::stereo_t> am;
+        am.init(&dummy, dsp::demod::AM<dsp::stereo_t>::AUDIO, 10000, 50.0 / 48000, 5.0 / 48000, 10.0 / 48000, 48000);
+        std::vector<dsp::stereo_t> st(n);
+        std::vector<float> ref(n);
+        orc_am* oa = orc_am_create(2, 10000, 50.0 / 48000, 5.0 / 48000, 10.0 / 48000, 48000, 1);
+        int m = am.process(n / 2, ifx.data(), st.data());
+        m += am.process(n - n / 2, ifx.data() + n / 2, st.data() + n / 2);
+        orc_am_process(oa, (const float*)ifx.data(), n / 2, ref.data());
+        orc_am_process(oa, (const float*)(ifx.data() + n / 2), n - n / 2, ref.data() + n / 2);
+        double err = 0, pk = 0;
+        for (int i = 0; i < m; i++) { err = std::fmax(err, std::fabs(st[i].l - ref[i])); pk = std::fmax(pk, std::fabs(ref[i])); CHECK(st[i].l == st[i].r, "am l!=r"); if (failures > 5) break; }
+        CHECK(m == n && err <= 2e-5 * std::fmax(pk, 1.0), "AM<stereo_t> n %d err %g (peak %g)", m, err, pk);
+        std::printf("AM<stereo_t> AUDIO AGC: max err %.3g (peak %.3g), gain %.4g\n", err, pk, am.getAGCGain());
+        orc_am_destroy(oa);
+
+        dsp::demod::SSB<float> ssb;
+        ssb.init(&dummy, dsp::demod::SSB<float>::USB, 2800, 48000, true, 50.0 / 48000, 5.0 / 48000);
+        std::vector<float> so(n), sr(n);
+        orc_ssb* os = orc_ssb_create(0, 2800, 48000, 1, 50.0 / 48000, 5.0 / 48000);
+        int k = ssb.process(n, ifx.data(), so.data());
+        orc_ssb_process(os, (const float*)ifx.data(), n, sr.data());
+        err = 0; pk = 0;
+        for (int i = 0; i < k; i++) { err = std::fmax(err, std::fabs(so[i] - sr[i])); pk = std::fmax(pk, std::fabs(sr[i])); }
+        CHECK(k == n && err <= 1e-5 * std::fmax(pk, 1e-30) + 1e-6, "SSB<float> err %g (peak %g)", err, pk);
+        std::printf("SSB<float> USB: max err %.3g (peak %.3g)\n", err, pk);
+        orc_ssb_destroy(os);
+
+        dsp::stream<float> fdummy;
+        dsp::loop::AGC<float> agc;
+        agc.init(&fdummy, 1.0, 0.01, 0.001, 10e6, 10.0, INFINITY);
+        dsp::correction::DCBlocker<float> dcb(&fdummy, 10.0, 48000.0);
+        std::vector<float> a(n), b(n), c(n), d(n);
+        for (int i = 0; i < n; i++) a[i] = 0.3f + 0.2f * (float)std::sin(0.01 * i) * (i % 5000 < 2500 ? 1.0f : 0.01f);
+        dcb.process(n, a.data(), b.data());
+        agc.process(n, b.data(), c.data());
+        orc_dcb* od = orc_dcb_create(0, 10.0 / 48000.0);
+        orc_agc* og = orc_agc_create(0, 1.0, 0.01, 0.001, 10e6, 10.0, INFINITY);
+        orc_dcb_process(od, a.data(), n, d.data());
+        orc_agc_process(og, d.data(), n, d.data());
+        CHECK(std::memcmp(c.data(), d.data(), sizeof(float) * n) == 0, "DCBlocker->AGC not bit-exact");
+        std::printf("DCBlocker<float> -> AGC<float>: bit-exact %s\n", std::memcmp(c.data(), d.data(), sizeof(float) * n) == 0 ? "yes" : "NO");
+        orc_dcb_destroy(od); orc_agc_destroy(og);
     }
     std::printf(failures ? "FAILED (%d)\n" : "ALL OK\n", failures);
     return failures ? 1 : 0;
