@@ -72,30 +72,40 @@ struct FirArgs {
     int dshift;         // log2(D) when D is a power of two, else -1
     int ntiles;         // tiles of TMS outputs (persistent grid walks them)
     int tapsLdsOff;     // TL: byte offset of the [D][Q] taps in dynamic LDS
+    int simple;         // D | NT and K | NT/D: constant LDS stride per load slot
+    const float2* nstep;  // XL: e^{i w u NT}, u < NCO_PF, for this launch's NT
     float invDev;
 };
 
-// Persistent, software-pipelined FIR tile loop. Workgroup g walks tiles g, g + G, ...; the
-// input span of its next tile is loaded into registers (PF elements per thread) while the
-// current tile is computed from LDS, so HBM latency hides behind the dot products instead
-// of serialising load -> barrier -> compute per tile. Spans longer than
-// PF * NT (very large decimations) load their remainder synchronously at commit time.
+// FIR tile kernel: one tile of NT*K outputs per workgroup.
+//  1. The tile's input span (rows * D elements) is loaded with all PF loads per thread in
+//     flight at once (interior tiles; the few tiles touching the history or the tail of the
+//     call fetch element-wise), the fused xlator's NCO phasor is formed as
+//     base(tid) * S[u] (S[u] = e^{i w u NT}, wave-uniform scalar loads) instead of two table
+//     loads per element, and each element is stored into the phase-major, row-swizzled LDS
+//     image X[p][r % K][r / K] with an address that advances by a constant per slot when
+//     D | NT and K | NT/D (all plan stages), else with the general index split.
+//  2. Each thread computes K consecutive outputs with a register window sliding one row per
+//     tap; taps are staged once per workgroup in LDS (wave-uniform broadcast reads).
+// History / tail samples come from [hist (H) || in (count)]; hist is stored translated.
 template <typename DT, bool XL>
 __device__ __forceinline__ DT fir_fetch(const FirArgs& a, long long b) {
-    // element b of [hist (H) || in (count)] with zero outside; hist is stored translated
     const DT* hist = reinterpret_cast<const DT*>(a.hist);
     const DT* in = reinterpret_cast<const DT*>(a.in);
     DT x = zero_of<DT>();
     if (b >= 0) {
         if (b < a.H) x = hist[b];
-        else if (b - a.H < a.count) x = in[b - a.H];
+        else if (b - a.H < a.count) {
+            x = in[b - a.H];
+            if constexpr (XL) x = cmulf(x, nco_tab(a.phi, a.plo, b - a.H));
+        }
     }
     return x;
 }
 
 template <typename DT, typename TT, int K, bool XL, bool QUAD, bool STEREO, bool TL>
 __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
-    constexpr int PF = sizeof(DT) == 8 ? 36 : 40;   // prefetch slots per thread
+    constexpr int PF = sizeof(DT) == 8 ? 36 : 40;   // load slots per thread issued together
     const int NT = blockDim.x;       // 64, 128 or 256 (host picks the largest tile that fits LDS)
     const int TM = NT * K;
     constexpr int QOFF = QUAD ? 1 : 0;
@@ -103,26 +113,18 @@ __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
     DT* X = reinterpret_cast<DT*>(smem);
     __shared__ float2 lastY[QUAD ? 256 : 1];
 
-    int tid = threadIdx.x;
+    const int tid = threadIdx.x;
+    const int tile = blockIdx.x;
     const int rows = TM + a.Q + K;                               // padded taps + prefetch rows
     const int span = rows * a.D;
     const DT* in = reinterpret_cast<const DT*>(a.in);
-    // Taps: TL -> copied once per (persistent) workgroup behind the span in LDS and read with
-    // wave-uniform (broadcast) LDS loads; else wave-uniform global reads (tap sets too large
-    // for LDS). Global reads inside the tile loop cannot become scalar loads -- the loop's
-    // output stores may alias them -- and a vector load there would wait on the prefetch.
     const TT* __restrict__ taps = reinterpret_cast<const TT*>(a.taps);
     if constexpr (TL) {
         TT* tl = reinterpret_cast<TT*>(smem + a.tapsLdsOff);
-        for (int i = threadIdx.x; i < a.D * a.Q; i += NT) tl[i] = taps[i];
-        taps = tl;                                                // (barrier: first commit's)
+        for (int i = tid; i < a.D * a.Q; i += NT) tl[i] = taps[i];
+        taps = tl;                                                // (ordered by the barrier below)
     }
-    int tile = blockIdx.x;
-    if (tile >= a.ntiles) return;
-
-    auto base = [&](int t) { return (long long)a.offset0 + (long long)(t * a.TMS - QOFF) * a.D; };
-    auto is_interior = [&](long long b0) { return (b0 >= a.H) && (b0 + span <= (long long)a.H + a.count); };
-    auto lds_put = [&](int sx, DT v) {
+    auto lds_index = [&](int sx) {
         int p, r;
         if (a.dshift >= 0) {
             p = sx & (a.D - 1);
@@ -131,152 +133,116 @@ __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
             r = sx / a.D;
             p = sx - r * a.D;
         }
-        X[p * a.RSP + (r % K) * a.RSK + r / K] = v;   // phase-major, row-swizzled
+        return p * a.RSP + (r % K) * a.RSK + r / K;
     };
 
-    // Interior tiles (span entirely inside `in`) are prefetched; the few boundary tiles of a
-    // call (history / tail) are fetched synchronously at commit.
-    DT pf[PF];
-    bool pfValid = false;
-    auto issue = [&](int t) {
-        const long long b0 = base(t);
-        pfValid = is_interior(b0);
-        if (pfValid) {
-            const DT* __restrict__ src = in + (b0 - a.H);
+    const int mFirst = tile * a.TMS - QOFF;                      // output of local index 0
+    const long long b0 = (long long)a.offset0 + (long long)mFirst * a.D;
+    const bool interior = (b0 >= a.H) && (b0 + span <= (long long)a.H + a.count);
+    int sxRest = tid;                                            // first slot fetched element-wise
+    if (interior) {
+        const DT* __restrict__ src = in + (b0 - a.H);
+        DT pf[PF];
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            const int sx = tid + u * NT;
+            if (sx < span) pf[u] = src[sx];
+        }
+        if constexpr (XL) {
+            // phasor(i0 + tid + u NT) = nco(i0 + tid) * e^{i w u NT}
+            const float2 ph0 = nco_tab(a.phi, a.plo, b0 - a.H + tid);
+            const float2* __restrict__ S = a.nstep;
+#pragma unroll
+            for (int u = 0; u < PF; u++) pf[u] = cmulf(pf[u], cmulf(ph0, S[u]));
+        }
+        if (a.simple) {
+            // D | NT and K | NT/D: the slot's phase is fixed, its row advances by NT/D
+            int idx = lds_index(tid);
+            const int inc = (NT / a.D) / K;
 #pragma unroll
             for (int u = 0; u < PF; u++) {
-                const int sx = tid + u * NT;
-                if (sx < span) pf[u] = src[sx];
-            }
-        }
-    };
-    auto xl_apply = [&](DT v, long long b) {
-        if constexpr (XL) {
-            if (b >= a.H && b - a.H < a.count) v = cmulf(v, nco_tab(a.phi, a.plo, b - a.H));
-        }
-        return v;
-    };
-    auto commit = [&](int t) {
-        const long long b0 = base(t);
-        int sx0 = tid;
-        if (pfValid) {
-            if constexpr (XL) {
-                // interior: every element is from `in`. NCO table reads in groups of 8 so
-                // the table latency is paid once per group, not once per element
-                const long long i0 = b0 - a.H;
-#pragma unroll
-                for (int g = 0; g < PF; g += 8) {
-                    float2 ph[8];
-#pragma unroll
-                    for (int u = 0; u < 8 && g + u < PF; u++) {
-                        const int sx = min(tid + (g + u) * NT, span - 1);
-                        ph[u] = nco_tab(a.phi, a.plo, i0 + sx);
-                    }
-#pragma unroll
-                    for (int u = 0; u < 8 && g + u < PF; u++) {
-                        const int sx = tid + (g + u) * NT;
-                        if (sx < span) lds_put(sx, cmulf(pf[g + u], ph[u]));
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int u = 0; u < PF; u++) {
-                    const int sx = tid + u * NT;
-                    if (sx < span) lds_put(sx, pf[u]);
-                }
-            }
-            sx0 = tid + PF * NT;                                   // remainder (rare: huge decimations)
-        }
-        for (int sx = sx0; sx < span; sx += NT) lds_put(sx, xl_apply(fir_fetch<DT, XL>(a, b0 + sx), b0 + sx));
-    };
-
-    const int l = tid;
-    float2 din0 = make_float2(0.f, 0.f);
-    if constexpr (QUAD) din0 = a.din[0];
-    issue(tile);
-    for (;;) {
-        // re-materialise the thread index each tile: keeps the compiler from hoisting the PF
-        // per-slot global/LDS addresses out of the loop (that costs ~2 PF live registers)
-        asm volatile("" : "+v"(tid));
-        commit(tile);
-        __syncthreads();
-        const int next = tile + gridDim.x;
-        if (next < a.ntiles) issue(next);                      // in flight during the dot products
-
-        DT acc[K];
-#pragma unroll
-        for (int i = 0; i < K; i++) acc[i] = zero_of<DT>();
-        // a.Q is padded to a multiple of QC with zero taps: each chunk loads QC taps with one
-        // wave-uniform (scalar) load and issues its QC row reads before the first FMA, so the
-        // loop waits once per chunk instead of once per tap.
-        constexpr int QC = 8;
-        for (int p = 0; p < a.D; p++) {
-            const DT* Xp = X + p * a.RSP;
-            const TT* __restrict__ Hp = taps + p * a.Q;
-            DT w[K];
-#pragma unroll
-            for (int i = 0; i < K; i++) w[i] = Xp[i * a.RSK + l];   // rows l*K + i
-            for (int q0 = 0; q0 < a.Q; q0 += QC) {
-                TT hv[QC];
-                DT nx[QC];
-#pragma unroll
-                for (int u = 0; u < QC; u++) hv[u] = Hp[q0 + u];
-#pragma unroll
-                for (int u = 0; u < QC; u++) {
-                    const int rn = l * K + K + q0 + u;                // row entering slot (q0 + u) % K
-                    nx[u] = Xp[(rn % K) * a.RSK + rn / K];
-                }
-#pragma unroll
-                for (int u = 0; u < QC; u++) {
-#pragma unroll
-                    for (int i = 0; i < K; i++) mac(acc[i], w[(i + u) % K], hv[u]);
-                    w[u % K] = nx[u];
-                }
-            }
-        }
-
-        const int mFirst = tile * a.TMS - QOFF;                    // output of local index 0
-        if constexpr (QUAD) {
-            // FM quadrature (demod/quadrature.h:41-56): out = arg(y[m] * conj(y[m-1])) / dev
-            lastY[l] = acc[K - 1];
-            __syncthreads();
-            float* out = reinterpret_cast<float*>(a.out);
-#pragma unroll
-            for (int i = 0; i < K; i++) {
-                const int m = mFirst + l * K + i;
-                if (m >= 0 && m >= tile * a.TMS && m < a.M) {
-                    float2 prev;
-                    if (m == 0) prev = din0;
-                    else if (i > 0) prev = acc[i - 1];
-                    else prev = lastY[l - 1];
-                    const float2 y = acc[i];
-                    const float br = prev.x, bi = -prev.y;
-                    const float re = (y.x * br) - (y.y * bi);
-                    const float im = (y.y * br) + (y.x * bi);
-                    out[m] = atan2f(im, re) * a.invDev;
-                    if (m == a.M - 1) a.dinNext[0] = y;
-                }
+                if (tid + u * NT < span) X[idx] = pf[u];
+                idx += inc;
             }
         } else {
 #pragma unroll
-            for (int i = 0; i < K; i++) {
-                const int m = mFirst + l * K + i;
-                if (m < a.M && m < (tile + 1) * a.TMS) {
-                    if constexpr (STEREO) {
-                        reinterpret_cast<float2*>(a.out)[m] = make_float2(acc[i], acc[i]);   // LRToStereo(l = r)
-                    } else {
-                        reinterpret_cast<DT*>(a.out)[m] = acc[i];
-                    }
+            for (int u = 0; u < PF; u++) {
+                const int sx = tid + u * NT;
+                if (sx < span) X[lds_index(sx)] = pf[u];
+            }
+        }
+        sxRest = tid + PF * NT;                                  // remainder (rare: huge decimations)
+    }
+    for (int sx = sxRest; sx < span; sx += NT) X[lds_index(sx)] = fir_fetch<DT, XL>(a, b0 + sx);
+    __syncthreads();
+
+    DT acc[K];
+#pragma unroll
+    for (int i = 0; i < K; i++) acc[i] = zero_of<DT>();
+    // a.Q is padded to a multiple of QC with zero taps. Row l*K + j + K*s of phase p sits at
+    // Xj[j][s] (j = row % K), so a chunk's QC row reads are K base addresses + immediates.
+    constexpr int QC = 8;
+    const int l = tid;
+    for (int p = 0; p < a.D; p++) {
+        const DT* Xj[K];
+#pragma unroll
+        for (int j = 0; j < K; j++) Xj[j] = X + p * a.RSP + j * a.RSK + l;
+        const TT* __restrict__ Hp = taps + p * a.Q;
+        DT w[K];
+#pragma unroll
+        for (int i = 0; i < K; i++) w[i] = Xj[i][0];                // rows l*K + i
+        for (int q0 = 0; q0 < a.Q; q0 += QC) {
+            TT hv[QC];
+            DT nx[QC];
+#pragma unroll
+            for (int u = 0; u < QC; u++) hv[u] = Hp[q0 + u];
+#pragma unroll
+            for (int u = 0; u < QC; u++) nx[u] = Xj[u % K][1 + (q0 + u) / K];   // row l*K + K + q0 + u
+#pragma unroll
+            for (int u = 0; u < QC; u++) {
+#pragma unroll
+                for (int i = 0; i < K; i++) mac(acc[i], w[(i + u) % K], hv[u]);
+                w[u % K] = nx[u];
+            }
+        }
+    }
+
+    if constexpr (QUAD) {
+        // FM quadrature (demod/quadrature.h:41-56): out = arg(y[m] * conj(y[m-1])) / dev
+        lastY[l] = acc[K - 1];
+        const float2 din0 = a.din[0];                 // y[-1] of the stream: carried from the last call
+        __syncthreads();
+        float* out = reinterpret_cast<float*>(a.out);
+        const float2 left = lastY[l > 0 ? l - 1 : 0];
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            const int m = mFirst + l * K + i;
+            if (m >= 0 && m >= tile * a.TMS && m < a.M) {
+                float2 prev = (i > 0) ? acc[i > 0 ? i - 1 : 0] : left;
+                if (m == 0) prev = din0;
+                const float2 y = acc[i];
+                const float br = prev.x, bi = -prev.y;
+                const float re = (y.x * br) - (y.y * bi);
+                const float im = (y.y * br) + (y.x * bi);
+                out[m] = atan2f(im, re) * a.invDev;
+                if (m == a.M - 1) a.dinNext[0] = y;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            const int m = mFirst + l * K + i;
+            if (m < a.M && m < (tile + 1) * a.TMS) {
+                if constexpr (STEREO) {
+                    reinterpret_cast<float2*>(a.out)[m] = make_float2(acc[i], acc[i]);   // LRToStereo(l = r)
+                } else {
+                    reinterpret_cast<DT*>(a.out)[m] = acc[i];
                 }
             }
         }
-        __syncthreads();                                            // LDS span free for the next commit
-        if (next >= a.ntiles) break;
-        tile = next;
     }
 }
 
-// history for the next call: the last H elements of hist | xl(in)
 template <typename DT, bool XL>
 __global__ void fir_hist_kernel(const DT* __restrict__ hist, const DT* __restrict__ in, DT* __restrict__ next, int H,
                                 int count, const float2* __restrict__ phi, const float2* __restrict__ plo) {
@@ -302,12 +268,26 @@ __global__ void xlator_kernel(const float2* __restrict__ in, float2* __restrict_
 }
 
 // host side of the NCO tables
+constexpr int NCO_PF = 64;   // >= the FIR kernel's load slots per thread
 struct Nco {
     double w = 0.0;
     PhaseAcc phase;     // phase of the next input sample
     DevBuf plo, phi;
+    DevBuf step;        // [3][NCO_PF]: e^{i w u NT}, NT = 64, 128, 256 (fp64 -> float)
+    const float2* step_for(int NT) const { return step.as<float2>() + (NT == 64 ? 0 : NT == 128 ? 1 : 2) * NCO_PF; }
     int set_w(double w_) {
         w = w_;
+        {
+            std::vector<float2> st(3 * NCO_PF);
+            const int nts[3] = {64, 128, 256};
+            for (int k = 0; k < 3; k++)
+                for (int u = 0; u < NCO_PF; u++) {
+                    const double a = std::fmod(w * (double)u * (double)nts[k], 2.0 * M_PI);
+                    st[k * NCO_PF + u] = make_float2((float)std::cos(a), (float)std::sin(a));
+                }
+            SDRGPU_CHECK(step.ensure(sizeof(float2) * st.size()));
+            SDRGPU_HIP(hipMemcpy(step.p, st.data(), sizeof(float2) * st.size(), hipMemcpyHostToDevice));
+        }
         std::vector<float2> t(NCO_LO);
         for (int k = 0; k < NCO_LO; k++) {
             const double a = std::fmod(w * (double)k, 2.0 * M_PI);
@@ -445,7 +425,6 @@ struct FirBlock : Block {
         ttype = ttype_;
         if (decim < 1) { set_error("fir: decimation %d < 1", decim); return SDRGPU_EARG; }
         D = decim;
-        if (const char* e = getenv("SDRGPU_FIR_TPW")) tilesPerWG = std::max(1, atoi(e));
         if (const char* e = getenv("SDRGPU_FIR_NT")) forceNT = atoi(e);
         if (const char* e = getenv("SDRGPU_FIR_LDS_KB")) ldsCap = std::max(8, atoi(e));
         SDRGPU_CHECK(init_stream());
@@ -515,7 +494,6 @@ struct FirBlock : Block {
         return 1;
     }
     int NT = 256;
-    int tilesPerWG = 1;     // SDRGPU_FIR_TPW (tuning)
     int forceNT = 0;        // SDRGPU_FIR_NT (tuning): threads per tile
     int ldsCap = 76;        // SDRGPU_FIR_LDS_KB (tuning): preferred LDS per tile
     template <typename DT, typename TT, int K, bool XL, bool QD, bool ST>
@@ -528,12 +506,12 @@ struct FirBlock : Block {
         auto k = tl ? fir_kernel<DT, TT, K, XL, QD, ST, true> : fir_kernel<DT, TT, K, XL, QD, ST, false>;
         SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         a.ntiles = tiles;
-        // tilesPerWG consecutive-in-stride tiles per workgroup. A co-resident persistent grid
-        // (tilesPerWG ~ tiles / (2 * CUs)) with the register prefetch was measured 1.5x SLOWER
-        // than one tile per workgroup on C3 (the hardware's own workgroup turnover staggers the
-        // load/compute phases of the workgroups sharing a CU better), so the default is 1.
-        const int grid = (tiles + tilesPerWG - 1) / tilesPerWG;
-        hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, s, a);
+        a.simple = (NT % D == 0) && ((NT / D) % K == 0);
+        a.nstep = xl ? nco.step_for(NT) : nullptr;
+        // one tile per workgroup: a co-resident persistent grid with a register prefetch of the
+        // next tile was measured 1.5x SLOWER on C3 (the hardware's own workgroup turnover
+        // staggers the load/compute phases of the workgroups sharing a CU better)
+        hipLaunchKernelGGL(k, dim3(tiles), dim3(NT), lds, s, a);
         SDRGPU_HIP(hipGetLastError());
         return SDRGPU_OK;
     }
