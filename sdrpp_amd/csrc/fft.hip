@@ -314,11 +314,18 @@ struct FftPlan {
     int chunkFrames = 1;
     int sa = 16, sb = 32;             // pass-A columns / pass-B rows per workgroup (tuning)
     int dbg = 0;                      // timing-only ablations (SDRGPU_FFT_DEBUG; wrong results)
+    float2* cur = nullptr;            // scratch buffer of the chunk being launched
     int tcolS = 0;                    // columns of the [k1][c] twiddle table
     int sa2 = 0;                      // paired pass-A columns per workgroup (0: paired kernel off)
     hipStream_t own = nullptr;
     PinnedBuf pin_in, pin_out;
     DevBuf dev_in, dev_out;
+    // two-stream chunk pipeline: pass A of chunk i+1 (caller stream) overlaps pass B of chunk
+    // i (second stream); scratch is double-buffered
+    int pipe = 1;
+    hipStream_t s2 = nullptr;
+    hipEvent_t evFork = nullptr, evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr};
+    DevBuf scratch2;
 };
 
 // t[m] = exp(-2 pi i (m * step) / L) for m < count (fp64 -> float)
@@ -360,7 +367,7 @@ static int launch_passA(const FftPlan& p, const float2* in, long long stride, in
     SDRGPU_CHECK(set_lds(k, lds));
     const int g = (p.N2 / S) * frames;
     hipLaunchKernelGGL(k, dim3(g), dim3(S * L / 16), lds, s, in, stride, frames, p.win.as<float>(), p.nz, p.N2,
-                       p.logN, p.tw1.as<float2>(), p.tbase.as<float2>(), p.tcol.as<float2>(), p.scratch.as<float2>());
+                       p.logN, p.tw1.as<float2>(), p.tbase.as<float2>(), p.tcol.as<float2>(), p.cur);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
@@ -373,7 +380,7 @@ static int launch_passA2(const FftPlan& p, const float2* in, long long stride, i
     SDRGPU_CHECK(set_lds(k, lds));
     const int g = (p.N2 / S) * frames;
     hipLaunchKernelGGL(k, dim3(g), dim3(S / 2 * L / 16), lds, s, in, stride, frames, p.win.as<float>(), p.nz, p.N2,
-                       p.logN, p.tw1.as<float2>(), p.tfull.as<float2>(), p.scratch.as<float2>(), p.dbg);
+                       p.logN, p.tw1.as<float2>(), p.tfull.as<float2>(), p.cur, p.dbg);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
@@ -384,7 +391,7 @@ static int launch_passB(const FftPlan& p, int frames, float* out, hipStream_t s)
     size_t lds = sizeof(float2) * S * Lds<L>::LS;
     SDRGPU_CHECK(set_lds(k, lds));
     const int g = (p.N1 / S) * frames;
-    hipLaunchKernelGGL(k, dim3(g), dim3(S * L / 16), lds, s, p.scratch.as<float2>(), frames, p.N1, p.logN,
+    hipLaunchKernelGGL(k, dim3(g), dim3(S * L / 16), lds, s, p.cur, frames, p.N1, p.logN,
                        p.tw2.as<float2>(), out);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
@@ -500,6 +507,7 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         if (const char* e = getenv("SDRGPU_FFT_SA")) p.sa = atoi(e);
         if (const char* e = getenv("SDRGPU_FFT_SB")) p.sb = atoi(e);
         if (const char* e = getenv("SDRGPU_FFT_DEBUG")) p.dbg = atoi(e);
+        if (const char* e = getenv("SDRGPU_FFT_PIPE")) p.pipe = atoi(e);
         p.chunkFrames = std::max(1, (int)((chunkMB << 20) / ((long long)fftSize * 8)));
         // pass-A columns per workgroup actually dispatched for this N1 (see dispatch_passA)
         p.tcolS = (p.N1 == 256) ? (p.sa == 64 ? 64 : p.sa == 32 ? 32 : 16)
@@ -592,13 +600,40 @@ extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long f
     }
     // 16-B loads need an even frame stride and a 16-B aligned base
     const bool paired = p.sa2 > 0 && (frameStride % 2) == 0 && ((uintptr_t)in & 15) == 0;
-    for (int f0 = 0; f0 < frames; f0 += p.chunkFrames) {
-        int nf = std::min(p.chunkFrames, frames - f0);
+    const int nchunks = (frames + p.chunkFrames - 1) / p.chunkFrames;
+    const bool pipe = p.pipe && nchunks > 1;
+    if (pipe) {
+        if (!p.s2) {
+            SDRGPU_HIP(hipStreamCreateWithFlags(&p.s2, hipStreamNonBlocking));
+            SDRGPU_HIP(hipEventCreateWithFlags(&p.evFork, hipEventDisableTiming));
+            for (int k = 0; k < 2; k++) {
+                SDRGPU_HIP(hipEventCreateWithFlags(&p.evA[k], hipEventDisableTiming));
+                SDRGPU_HIP(hipEventCreateWithFlags(&p.evB[k], hipEventDisableTiming));
+            }
+        }
+        SDRGPU_CHECK(p.scratch2.ensure(p.scratch.bytes));
+        SDRGPU_HIP(hipEventRecord(p.evFork, s));
+        SDRGPU_HIP(hipStreamWaitEvent(p.s2, p.evFork, 0));
+    }
+    for (int c = 0; c < nchunks; c++) {
+        const int f0 = c * p.chunkFrames;
+        const int nf = std::min(p.chunkFrames, frames - f0);
         const float2* xc = x + (long long)f0 * frameStride;
+        const int b = pipe ? (c & 1) : 0;
+        p.cur = b ? p.scratch2.as<float2>() : p.scratch.as<float2>();
+        if (pipe && c >= 2) SDRGPU_HIP(hipStreamWaitEvent(s, p.evB[b], 0));   // buffer b free again
         if (paired) SDRGPU_CHECK(dispatch_passA2(p, xc, frameStride, nf, s));
         else SDRGPU_CHECK(dispatch_passA(p, xc, frameStride, nf, s));
-        SDRGPU_CHECK(dispatch_passB(p, nf, out + (long long)f0 * p.N, s));
+        hipStream_t sb = s;
+        if (pipe) {
+            SDRGPU_HIP(hipEventRecord(p.evA[b], s));
+            SDRGPU_HIP(hipStreamWaitEvent(p.s2, p.evA[b], 0));
+            sb = p.s2;
+        }
+        SDRGPU_CHECK(dispatch_passB(p, nf, out + (long long)f0 * p.N, sb));
+        if (pipe) SDRGPU_HIP(hipEventRecord(p.evB[b], p.s2));
     }
+    if (pipe) SDRGPU_HIP(hipStreamWaitEvent(s, p.evB[(nchunks - 1) & 1], 0));   // join
     return frames;
 }
 
@@ -628,6 +663,15 @@ extern "C" int sdrgpu_fft_destroy(sdrgpu_fft* h) {
     if (!h) return SDRGPU_OK;
     (void)hipSetDevice(h->p.device);
     if (h->p.own) (void)hipStreamDestroy(h->p.own);
+    if (h->p.s2) {
+        (void)hipStreamSynchronize(h->p.s2);
+        (void)hipStreamDestroy(h->p.s2);
+        (void)hipEventDestroy(h->p.evFork);
+        for (int k = 0; k < 2; k++) {
+            (void)hipEventDestroy(h->p.evA[k]);
+            (void)hipEventDestroy(h->p.evB[k]);
+        }
+    }
     delete h;
     return SDRGPU_OK;
 }
