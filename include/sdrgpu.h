@@ -144,6 +144,10 @@ int sdrgpu_demod_agc_set_gain(sdrgpu_block* h, int which, float gain);
 int sdrgpu_demod_agc_get_gain(sdrgpu_block* h, int which, float* gain);
 int sdrgpu_demod_agc_set_enabled(sdrgpu_block* h, int which, int enabled);
 int sdrgpu_demod_agc_set_attack_decay(sdrgpu_block* h, double attack, double decay);
+/* demod::BroadcastFM with the stereo decoder (broadcast_fm.h:34-60, 144-215): quadrature ->
+ * pilot band-pass (complex taps) -> PLL (loop/pll.h) -> L+R / L-R matrix -> audio low-pass;
+ * stereo_t out. stereo = 0 gives the mono path (= sdrgpu_wfm_create). RDS output: not provided. */
+int sdrgpu_broadcast_fm_create(sdrgpu_block** h, int device, double deviation, double samplerate, int stereo, int lowPass);
 /* M-channel critically sampled polyphase channelizer (BASELINE C4): channel k of output frame
  * m is FrequencyXlator(-k fs/M) -> DecimatingFIR<complex_t,float>(taps, M) (frequency_xlator.h:43,
  * decimating_fir.h:45) with an exact NCO; taps <= 16 M (bank layout polyphase_bank.h:32).

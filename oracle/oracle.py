@@ -94,6 +94,9 @@ def _load():
         "orc_compress": (i, [i, vp, i, vp]),
         "orc_decompress": (i, [vp, i, vp]),
         "orc_channelize": (i, [vp, l, vp, i, i, vp, i, vp]),
+        "orc_wfms_create": (vp, [d, d, i, i, i]),
+        "orc_wfms_process": (i, [vp, vp, i, vp]),
+        "orc_wfms_destroy": (None, [vp]),
         "orc_chain_create": (vp, [d, i, d, i]),
         "orc_chain_process": (l, [vp, vp, l, vp, l, vp]),
         "orc_chain_destroy": (None, [vp]),
@@ -343,6 +346,18 @@ class BroadcastFM(_Obj):
 
     def process(self, x):
         return super().process(x, lib.orc_wfm_process)
+
+
+class BroadcastFMStereo(_Obj):
+    """demod/broadcast_fm.h with the stereo decoder (pilot BPF -> PLL -> L+R / L-R matrix)."""
+    _destroy = lib.orc_wfms_destroy
+
+    def __init__(self, deviation, samplerate, stereo=True, low_pass=True, precise=True):
+        super().__init__(lib.orc_wfms_create(float(deviation), float(samplerate), int(stereo), int(low_pass), int(precise)),
+                         np.complex64, STEREO)
+
+    def process(self, x):
+        return super().process(x, lib.orc_wfms_process)
 
 
 class FM(_Obj):

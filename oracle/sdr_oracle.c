@@ -628,6 +628,123 @@ int orc_wfm_process(orc_wfm* w, const float* in, int count, float* out) {
 }
 void orc_wfm_destroy(orc_wfm* w) { if (!w) return; orc_quad_destroy(w->q); orc_fir_destroy(w->al); free(w->tmp); free(w); }
 
+/* ----------------------------------------------------- BroadcastFM stereo */
+/* demod/broadcast_fm.h:34-60 (init), :144-191 (process, _stereo == true, no RDS);
+ * loop/pll.h:13-72, loop/phase_control_loop.h:17-89, math/normalize_phase.h,
+ * math/phasor.h, math/delay.h. All PLL state and coefficients are float (T = float). */
+struct orc_pll { float alpha, beta, phase, freq, minPhase, maxPhase, phaseDelta, minFreq, maxFreq, initPhase, initFreq; };
+static void orc_pll_init(struct orc_pll* p, double bandwidth, double initPhase, double initFreq, double minFreq, double maxFreq) {
+    /* PhaseControlLoop<float>::criticallyDamped (phase_control_loop.h:31-36), T = float */
+    float bw = (float)bandwidth;
+    float df = (float)(sqrt(2.0) / 2.0);
+    float denominator = (float)((1.0 + 2.0 * (double)df * (double)bw) + (double)(bw * bw));
+    p->alpha = ((float)4 * df * bw) / denominator;
+    p->beta = ((float)4 * bw * bw) / denominator;
+    p->initPhase = (float)initPhase;
+    p->initFreq = (float)initFreq;
+    p->phase = p->initPhase;
+    p->minPhase = -FL_M_PI; p->maxPhase = FL_M_PI;
+    p->phaseDelta = p->maxPhase - p->minPhase;
+    p->freq = p->initFreq;
+    p->minFreq = (float)minFreq; p->maxFreq = (float)maxFreq;
+}
+static void orc_pll_process(struct orc_pll* p, const float* in, int count, float* out) {
+    for (int i = 0; i < count; i++) {
+        out[2 * i] = cosf(p->phase);                                   /* math::phasor */
+        out[2 * i + 1] = sinf(p->phase);
+        float diff = atan2f(in[2 * i + 1], in[2 * i]) - p->phase;      /* in[i].phase() - phase */
+        if (diff > FL_M_PI) diff -= 2.0f * FL_M_PI;                    /* normalizePhase */
+        else if (diff <= -FL_M_PI) diff += 2.0f * FL_M_PI;
+        p->freq += p->beta * diff;                                     /* advance */
+        if (p->freq > p->maxFreq) p->freq = p->maxFreq;
+        else if (p->freq < p->minFreq) p->freq = p->minFreq;
+        p->phase += p->freq + (p->alpha * diff);
+        while (p->phase > p->maxPhase) p->phase -= p->phaseDelta;
+        while (p->phase < p->minPhase) p->phase += p->phaseDelta;
+    }
+}
+
+struct orc_wfms {
+    orc_quad* q; orc_fir *pilot, *al, *ar; struct orc_pll pll;
+    int stereo, lowPass, delay;
+    float *mpx, *cplx, *pf, *vco, *lmr, *l, *r, *dlpr, *dlmr; int cap;
+};
+orc_wfms* orc_wfms_create(double deviation, double samplerate, int stereo, int lowPass, int precise) {
+    orc_wfms* w = (orc_wfms*)calloc(1, sizeof(orc_wfms));
+    w->q = orc_quad_create(hz_to_rads(deviation, samplerate));
+    int np = orc_band_pass_c(18750.0, 19250.0, 3000.0, samplerate, 1, NULL);
+    float* pt = (float*)malloc(sizeof(float) * 2 * np);
+    orc_band_pass_c(18750.0, 19250.0, 3000.0, samplerate, 1, pt);
+    w->pilot = orc_fir_create(ORC_C64, ORC_C64, pt, np, 1, precise);
+    free(pt);
+    orc_pll_init(&w->pll, 25000.0 / samplerate, 0.0, hz_to_rads(19000.0, samplerate), hz_to_rads(18750.0, samplerate),
+                 hz_to_rads(19250.0, samplerate));
+    w->delay = ((np - 1) / 2) + 1;
+    int n = orc_low_pass(15000.0, 4000.0, samplerate, 0, NULL);
+    float* t = (float*)malloc(sizeof(float) * n);
+    orc_low_pass(15000.0, 4000.0, samplerate, 0, t);
+    w->al = orc_fir_create(ORC_F32, ORC_F32, t, n, 1, precise);
+    w->ar = orc_fir_create(ORC_F32, ORC_F32, t, n, 1, precise);
+    free(t);
+    w->stereo = stereo; w->lowPass = lowPass;
+    w->dlpr = (float*)calloc(w->delay, sizeof(float));            /* Delay<float> state */
+    w->dlmr = (float*)calloc(2 * w->delay, sizeof(float));        /* Delay<complex_t> state */
+    return w;
+}
+static void orc_delay(float* state, int delay, int e, const float* in, int count, float* out) {
+    /* math/delay.h:39-50: out = [state || in][0:count], state = last `delay` of [state || in] */
+    float* buf = (float*)malloc(sizeof(float) * e * (delay + count));
+    memcpy(buf, state, sizeof(float) * e * delay);
+    memcpy(buf + e * delay, in, sizeof(float) * e * count);
+    memcpy(out, buf, sizeof(float) * e * count);
+    memcpy(state, buf + e * count, sizeof(float) * e * delay);
+    free(buf);
+}
+int orc_wfms_process(orc_wfms* w, const float* in, int count, float* out) {
+    if (w->cap < count) {
+        free(w->mpx); free(w->cplx); free(w->pf); free(w->vco); free(w->lmr); free(w->l); free(w->r);
+        w->mpx = (float*)malloc(sizeof(float) * count); w->cplx = (float*)malloc(sizeof(float) * 2 * count);
+        w->pf = (float*)malloc(sizeof(float) * 2 * count); w->vco = (float*)malloc(sizeof(float) * 2 * count);
+        w->lmr = (float*)malloc(sizeof(float) * 2 * count); w->l = (float*)malloc(sizeof(float) * count);
+        w->r = (float*)malloc(sizeof(float) * count);
+        w->cap = count;
+    }
+    orc_quad_process(w->q, in, count, w->mpx);
+    if (!w->stereo) {
+        if (w->lowPass) orc_fir_process(w->al, w->mpx, count, w->mpx);
+        for (int i = 0; i < count; i++) { out[2 * i] = w->mpx[i]; out[2 * i + 1] = w->mpx[i]; }
+        return count;
+    }
+    for (int i = 0; i < count; i++) { w->cplx[2 * i] = w->mpx[i]; w->cplx[2 * i + 1] = 0.0f; }   /* RealToComplex */
+    orc_fir_process(w->pilot, w->cplx, count, w->pf);
+    orc_pll_process(&w->pll, w->pf, count, w->vco);
+    orc_delay(w->dlpr, w->delay, 1, w->mpx, count, w->mpx);          /* lprDelay (in place) */
+    orc_delay(w->dlmr, w->delay, 2, w->cplx, count, w->lmr);         /* lmrDelay */
+    for (int i = 0; i < count; i++) {
+        float vr = w->vco[2 * i], vi = -w->vco[2 * i + 1];            /* Conjugate */
+        for (int k = 0; k < 2; k++) {                                  /* Multiply<complex_t> twice */
+            float ar = w->lmr[2 * i], ai = w->lmr[2 * i + 1];
+            w->lmr[2 * i] = (ar * vr) - (ai * vi);
+            w->lmr[2 * i + 1] = (ai * vr) + (ar * vi);
+        }
+        float lmr = w->lmr[2 * i] * 2.0f;                              /* ComplexToReal, x2 */
+        w->l[i] = w->mpx[i] + lmr;                                     /* Add */
+        w->r[i] = w->mpx[i] - lmr;                                     /* Subtract */
+    }
+    if (w->lowPass) {
+        orc_fir_process(w->al, w->l, count, w->l);
+        orc_fir_process(w->ar, w->r, count, w->r);
+    }
+    for (int i = 0; i < count; i++) { out[2 * i] = w->l[i]; out[2 * i + 1] = w->r[i]; }   /* LRToStereo */
+    return count;
+}
+void orc_wfms_destroy(orc_wfms* w) {
+    if (!w) return;
+    orc_quad_destroy(w->q); orc_fir_destroy(w->pilot); orc_fir_destroy(w->al); orc_fir_destroy(w->ar);
+    free(w->mpx); free(w->cplx); free(w->pf); free(w->vco); free(w->lmr); free(w->l); free(w->r);
+    free(w->dlpr); free(w->dlmr); free(w);
+}
+
 /* --------------------------------------------------------------- FM (NFM) */
 /* demod/fm.h:25-96 (T = float) */
 struct orc_fm { orc_quad* q; orc_fir* fir; int filtering; };

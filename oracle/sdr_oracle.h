@@ -110,6 +110,10 @@ typedef struct orc_wfm orc_wfm;              /* demod/broadcast_fm.h (mono path)
 orc_wfm* orc_wfm_create(double deviation, double samplerate, int lowPass, int precise);
 int  orc_wfm_process(orc_wfm* w, const float* in, int count, float* out_stereo);
 void orc_wfm_destroy(orc_wfm* w);
+typedef struct orc_wfms orc_wfms;            /* demod/broadcast_fm.h, stereo or mono (no RDS) */
+orc_wfms* orc_wfms_create(double deviation, double samplerate, int stereo, int lowPass, int precise);
+int  orc_wfms_process(orc_wfms* w, const float* in, int count, float* out_stereo);
+void orc_wfms_destroy(orc_wfms* w);
 
 typedef struct orc_fm orc_fm;                /* demod/fm.h */
 orc_fm* orc_fm_create(double samplerate, double bandwidth, int lowPass, int highPass, int precise);

@@ -84,6 +84,7 @@ def _load():
         "sdrgpu_fm_create": (i, [pp, i, d, d, i, i]),
         "sdrgpu_wfm_create": (i, [pp, i, d, d, i]),
         "sdrgpu_channelizer_create": (i, [pp, i, i, fp, i]),
+        "sdrgpu_broadcast_fm_create": (i, [pp, i, d, d, i, i]),
         "sdrgpu_agc_create": (i, [pp, i, i, d, d, d, d, d, d]),
         "sdrgpu_agc_set_enabled": (i, [vp, i]),
         "sdrgpu_agc_set_gain": (i, [vp, ctypes.c_float]),

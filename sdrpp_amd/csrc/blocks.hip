@@ -795,6 +795,17 @@ Block* chain_kid(Block* chain, int i) {
 Block* make_fir_block(int dev, int dtype, int ttype, const float* taps, int n, int decim, bool stereo, int* rc) {
     return make_fir(dev, dtype, ttype, taps, n, decim, rc, false, 0.0, false, 1.0f, stereo).release();
 }
+Block* make_quad_block(int dev, double deviationRad, int* rc) {
+    auto* q = new QuadBlock();
+    q->device = dev;
+    q->in_dtype = SDRGPU_C64;
+    q->out_dtype = SDRGPU_F32;
+    q->invDev = (float)(1.0 / deviationRad);
+    *rc = q->init_stream();
+    for (int k = 0; k < 2 && *rc >= 0; k++) *rc = q->din[k].ensure(sizeof(float2));
+    if (*rc >= 0) *rc = q->reset();
+    return q;
+}
 Block* make_xlator_block(int dev, double offsetRad, int* rc) {
     auto* x = new XlatorBlock();
     x->device = dev;

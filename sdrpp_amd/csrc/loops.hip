@@ -194,6 +194,79 @@ __global__ void mono_to_stereo_kernel(const float* __restrict__ in, float2* __re
     if (i < n) out[i] = make_float2(in[i], in[i]);
 }
 
+// ------------------------------------------------------- BroadcastFM stereo
+// demod/broadcast_fm.h:144-191 with loop/pll.h:64-70 + loop/phase_control_loop.h:59-66.
+struct PllParams {
+    float alpha, beta, minPhase, maxPhase, phaseDelta, minFreq, maxFreq;
+};
+__global__ void real_to_complex_kernel(const float* __restrict__ in, float2* __restrict__ out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = make_float2(in[i], 0.0f);           // convert::RealToComplex
+}
+__global__ void phase_kernel(const float2* __restrict__ in, float* __restrict__ out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = atan2f(in[i].y, in[i].x);             // complex_t::phase() (types.h:57)
+}
+// The PLL recurrence (one workgroup): in place, th[i] = input phase -> the phase the VCO
+// outputs for sample i (math::phasor(pcl.phase) BEFORE advance). State (phase, freq) on device.
+__global__ __launch_bounds__(LOOP_NT) void pll_kernel(float* __restrict__ th, int count, PllParams p, float2* __restrict__ st) {
+    __shared__ float T[LOOP_CHUNK];
+    const int t = threadIdx.x;
+    float phase = st->x, freq = st->y;
+    const float PI = 3.1415926535f;                            // FL_M_PI (math/constants.h:4)
+    for (int i0 = 0; i0 < count; i0 += LOOP_CHUNK) {
+        const int n = min(LOOP_CHUNK, count - i0);
+        for (int i = t; i < n; i += LOOP_NT) T[i] = th[i0 + i];
+        __syncthreads();
+        if (t == 0) {
+            for (int i = 0; i < n; i++) {
+                float diff = T[i] - phase;
+                T[i] = phase;
+                if (diff > PI) diff -= 2.0f * PI;               // math::normalizePhase
+                else if (diff <= -PI) diff += 2.0f * PI;
+                freq += p.beta * diff;                          // PhaseControlLoop::advance
+                if (freq > p.maxFreq) freq = p.maxFreq;
+                else if (freq < p.minFreq) freq = p.minFreq;
+                phase += freq + (p.alpha * diff);
+                while (phase > p.maxPhase) phase -= p.phaseDelta;
+                while (phase < p.minPhase) phase += p.phaseDelta;
+            }
+        }
+        __syncthreads();
+        for (int i = t; i < n; i += LOOP_NT) th[i0 + i] = T[i];
+        __syncthreads();
+    }
+    if (t == 0) *st = make_float2(phase, freq);
+}
+// Delays, conjugate, the two complex multiplies, x2, L = (L+R) + (L-R), R = (L+R) - (L-R),
+// written (l, r) as a float2 pair for the audio FIR. lmrDelay's input is RealToComplex of
+// the MPX, so its delayed imaginary part is exactly 0: the products are formed as the
+// reference forms them (0 * x terms included) and round identically.
+__global__ void stereo_matrix_kernel(const float* __restrict__ mpx, const float* __restrict__ hist, int delay,
+                                     const float* __restrict__ vcoPhase, float2* __restrict__ lr, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float d = i < delay ? hist[i] : mpx[i - delay];       // Delay<float> / Delay<complex_t>.re
+    const float vr = cosf(vcoPhase[i]), vi = -sinf(vcoPhase[i]);   // Conjugate(phasor)
+    float ar = d, ai = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {                              // Multiply<complex_t>, twice
+        const float nr = (ar * vr) - (ai * vi);
+        const float ni = (ai * vr) + (ar * vi);
+        ar = nr;
+        ai = ni;
+    }
+    const float lmr = ar * 2.0f;
+    lr[i] = make_float2(d + lmr, d - lmr);
+}
+__global__ void delay_hist_kernel(const float* __restrict__ hist, const float* __restrict__ in, float* __restrict__ next,
+                                  int delay, int count) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= delay) return;
+    const long long b = (long long)count + k;                  // last `delay` of [hist || in]
+    next[k] = b < delay ? hist[b] : in[b - delay];
+}
+
 // ---------------------------------------------------------------- blocks
 struct AgcBlock : Block {
     AgcParams p{};
@@ -325,6 +398,102 @@ Block* chain_kid(Block* chain, int i);
 Block* make_fir_block(int dev, int dtype, int ttype, const float* taps, int n, int decim, bool stereo, int* rc);
 Block* make_xlator_block(int dev, double offsetRad, int* rc);
 
+
+// BroadcastFM (demod/broadcast_fm.h:34-60, 144-215): quadrature -> [stereo: pilot band-pass
+// (complex, 305 taps at 240 kS/s) -> PLL -> matrix] -> audio low-pass -> stereo_t
+Block* make_quad_block(int dev, double deviationRad, int* rc);
+struct BroadcastFmBlock : Block {
+    bool stereo = true, lowPass = true;
+    std::unique_ptr<Block> quad, pilot, audio;
+    PllParams pp{};
+    float initPhase = 0.0f, initFreq = 0.0f;
+    int delay = 0;
+    DevBuf mpx, cplx, pf, ph, lr, pllState, hist[2];
+    int cur = 0;
+    int setup(int dev, double deviation, double samplerate, bool st, bool lp) {
+        device = dev;
+        in_dtype = SDRGPU_C64;
+        out_dtype = SDRGPU_C64;
+        stereo = st;
+        lowPass = lp;
+        SDRGPU_CHECK(init_stream());
+        int rc;
+        quad.reset(make_quad_block(dev, hz_to_rads(deviation, samplerate), &rc));
+        SDRGPU_CHECK(rc);
+        const int np = taps_band_pass_c(18750.0, 19250.0, 3000.0, samplerate, 1, nullptr);
+        if (np < 1) return np < 0 ? np : SDRGPU_EARG;
+        std::vector<float> pt(2 * (size_t)np);
+        taps_band_pass_c(18750.0, 19250.0, 3000.0, samplerate, 1, pt.data());
+        pilot.reset(make_fir_block(dev, SDRGPU_C64, SDRGPU_C64, pt.data(), np, 1, false, &rc));
+        SDRGPU_CHECK(rc);
+        delay = ((np - 1) / 2) + 1;                                   // lprDelay / lmrDelay
+        // PLL(25000 / fs, 0, 19 kHz, 18.75 kHz, 19.25 kHz) (broadcast_fm.h:47); criticallyDamped
+        // evaluated as PhaseControlLoop<float> does (phase_control_loop.h:31-36)
+        const float bw = (float)(25000.0 / samplerate);
+        const float df = (float)(std::sqrt(2.0) / 2.0);
+        const float den = (float)((1.0 + 2.0 * (double)df * (double)bw) + (double)(bw * bw));
+        pp.alpha = ((float)4 * df * bw) / den;
+        pp.beta = ((float)4 * bw * bw) / den;
+        pp.minPhase = -3.1415926535f;
+        pp.maxPhase = 3.1415926535f;
+        pp.phaseDelta = pp.maxPhase - pp.minPhase;
+        pp.minFreq = (float)hz_to_rads(18750.0, samplerate);
+        pp.maxFreq = (float)hz_to_rads(19250.0, samplerate);
+        initPhase = 0.0f;
+        initFreq = (float)hz_to_rads(19000.0, samplerate);
+        const int na = taps_low_pass(15000.0, 4000.0, samplerate, 0, nullptr);
+        if (na < 1) return na < 0 ? na : SDRGPU_EARG;
+        std::vector<float> at(na);
+        taps_low_pass(15000.0, 4000.0, samplerate, 0, at.data());
+        if (!lowPass) { at.assign(1, 1.0f); }                          // identity: raw L/R (or MPX) pairs
+        // (l, r) pairs filtered as one complex stream with real taps = alFir / arFir
+        audio.reset(make_fir_block(dev, SDRGPU_C64, SDRGPU_F32, at.data(), (int)at.size(), 1, false, &rc));
+        SDRGPU_CHECK(rc);
+        SDRGPU_CHECK(pllState.ensure(sizeof(float2)));
+        for (int k = 0; k < 2; k++) SDRGPU_CHECK(hist[k].ensure(sizeof(float) * delay));
+        return reset();
+    }
+    int out_count(int count) override { return count; }
+    int reset() override {   // broadcast_fm.h:129-141
+        SDRGPU_SET_DEVICE(device);
+        SDRGPU_CHECK(quad->reset());
+        SDRGPU_CHECK(pilot->reset());
+        SDRGPU_CHECK(audio->reset());
+        const float2 st = make_float2(initPhase, initFreq);
+        SDRGPU_HIP(hipMemcpy(pllState.p, &st, sizeof(st), hipMemcpyHostToDevice));
+        SDRGPU_HIP(hipMemset(hist[cur].p, 0, sizeof(float) * delay));
+        return SDRGPU_OK;
+    }
+    int run(const void* in, int count, void* out, hipStream_t s) override {
+        if (count < 0) { set_error("broadcast_fm: negative count"); return SDRGPU_EARG; }
+        if (count == 0) return 0;
+        SDRGPU_SET_DEVICE(device);
+        SDRGPU_CHECK(mpx.ensure(sizeof(float) * count));
+        SDRGPU_CHECK(lr.ensure(sizeof(float2) * count));
+        int m = quad->run(in, count, mpx.p, s);
+        if (m < 0) return m;
+        const dim3 g((count + 255) / 256), b(256);
+        if (stereo) {
+            SDRGPU_CHECK(cplx.ensure(sizeof(float2) * count));
+            SDRGPU_CHECK(pf.ensure(sizeof(float2) * count));
+            SDRGPU_CHECK(ph.ensure(sizeof(float) * count));
+            hipLaunchKernelGGL(real_to_complex_kernel, g, b, 0, s, mpx.as<float>(), cplx.as<float2>(), count);
+            m = pilot->run(cplx.p, count, pf.p, s);
+            if (m < 0) return m;
+            hipLaunchKernelGGL(phase_kernel, g, b, 0, s, pf.as<float2>(), ph.as<float>(), count);
+            hipLaunchKernelGGL(pll_kernel, dim3(1), dim3(LOOP_NT), 0, s, ph.as<float>(), count, pp, pllState.as<float2>());
+            hipLaunchKernelGGL(stereo_matrix_kernel, g, b, 0, s, mpx.as<float>(), hist[cur].as<float>(), delay,
+                               ph.as<float>(), lr.as<float2>(), count);
+            hipLaunchKernelGGL(delay_hist_kernel, dim3((delay + 255) / 256), dim3(256), 0, s, hist[cur].as<float>(),
+                               mpx.as<float>(), hist[cur ^ 1].as<float>(), delay, count);
+            cur ^= 1;
+        } else {
+            hipLaunchKernelGGL(mono_to_stereo_kernel, g, b, 0, s, mpx.as<float>(), lr.as<float2>(), count);
+        }
+        SDRGPU_HIP(hipGetLastError());
+        return audio->run(lr.p, count, out, s);
+    }
+};
 }  // namespace sdrgpu
 
 using namespace sdrgpu;
@@ -500,4 +669,12 @@ extern "C" int sdrgpu_dc_blocker_set_rate(sdrgpu_block* h, double rate) {
     if (!d) { set_error("no DC blocker"); return SDRGPU_ESTATE; }
     d->rate = (float)rate;
     return SDRGPU_OK;
+}
+
+// demod::BroadcastFM (broadcast_fm.h), stereo decoder included (RDS output: not provided)
+extern "C" int sdrgpu_broadcast_fm_create(sdrgpu_block** h, int device, double deviation, double samplerate, int stereo,
+                                          int lowPass) {
+    if (!h || !(samplerate > 0)) { set_error("broadcast_fm_create: bad argument"); return SDRGPU_EARG; }
+    auto* w = new BroadcastFmBlock();
+    return wrap_block(h, w, w->setup(device, deviation, samplerate, stereo != 0, lowPass != 0));
 }

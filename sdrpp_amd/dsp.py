@@ -173,10 +173,14 @@ class FM(Block):
 
 
 class BroadcastFM(Block):
-    """dsp::demod::BroadcastFM, mono path (demod/broadcast_fm.h:144-215); stereo_t out."""
+    """dsp::demod::BroadcastFM (demod/broadcast_fm.h:144-215); stereo_t out. stereo=False is
+    the mono path (the C5 bench chain); stereo=True adds the pilot PLL stereo decoder."""
 
-    def __init__(self, deviation, samplerate, low_pass=True, device=0):
-        h = _make(lib.sdrgpu_wfm_create, device, float(deviation), float(samplerate), int(low_pass))
+    def __init__(self, deviation, samplerate, low_pass=True, device=0, stereo=False):
+        if stereo:
+            h = _make(lib.sdrgpu_broadcast_fm_create, device, float(deviation), float(samplerate), 1, int(low_pass))
+        else:
+            h = _make(lib.sdrgpu_wfm_create, device, float(deviation), float(samplerate), int(low_pass))
         super().__init__(h, np.complex64, STEREO)
 
 

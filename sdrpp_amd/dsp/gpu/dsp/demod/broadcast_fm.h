@@ -1,8 +1,9 @@
-// GPU-backed dsp::demod::BroadcastFM -- drop-in for core/src/dsp/demod/broadcast_fm.h,
-// mono path (stereo == false, no RDS; broadcast_fm.h:144-215 else-branch): quadrature(dev)
-// -> 15 kHz audio low-pass (lowPass(15e3, 4e3, fs)) -> LRToStereo(l = r).
-// Stereo decoding (pilot PLL) and RDS are not on the GPU yet: init()/setStereo(true)
-// report an error instead of silently producing mono (DESIGN.md, section 8 "next").
+// GPU-backed dsp::demod::BroadcastFM -- drop-in for core/src/dsp/demod/broadcast_fm.h:
+//  stereo: quadrature -> pilot band-pass -> PLL -> L+R / L-R matrix -> audio low-pass
+//          (broadcast_fm.h:144-191, sdrgpu_broadcast_fm_create);
+//  mono:   quadrature -> 15 kHz low-pass -> LRToStereo (:193-211, sdrgpu_wfm_create).
+// The RDS branch feeds the RDS decoder module (out of scope): rdsOut = true reports an error
+// and produces no RDS samples; the audio path is unaffected.
 #pragma once
 #include "../processor.h"
 #include "../sdrgpu_handle.h"
@@ -43,7 +44,6 @@ public:
     }
     inline int process(int count, complex_t* in, stereo_t* out, int& rdsOutCount, complex_t* rdsout = nullptr) {
         rdsOutCount = 0;
-        if (_stereo || _rdsOut) return -1;
         return _h.process(in, count, out, "wfm");
     }
     int run() override {
@@ -66,11 +66,10 @@ protected:
         base_type::tempStart();
     }
     void rebuild() {
-        if (_stereo || _rdsOut) {
-            std::fprintf(stderr, "[sdrgpu] BroadcastFM: stereo/RDS decoding is not available on the GPU path yet\n");
-        }
+        if (_rdsOut) std::fprintf(stderr, "[sdrgpu] BroadcastFM: RDS output is not provided by the GPU path\n");
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_wfm_create(&h, gpu::device(), _deviation, _samplerate, _lowPass), "wfm_create");
+        if (_stereo) gpu::ok(sdrgpu_broadcast_fm_create(&h, gpu::device(), _deviation, _samplerate, 1, _lowPass), "broadcast_fm_create");
+        else gpu::ok(sdrgpu_wfm_create(&h, gpu::device(), _deviation, _samplerate, _lowPass), "wfm_create");
         _h.reset(h);
     }
     double _deviation = 0, _samplerate = 0;
