@@ -100,7 +100,10 @@ def _load():
         "sdrgpu_convert_dev": (i, [i, i, vp, ll, vp, vp]),
         "sdrgpu_convert": (i, [i, i, vp, ll, vp]),
     }
+    alt = bool(os.environ.get("SDRGPU_LIB_PATH"))
     for name, (res, args) in sig.items():
+        if alt and not hasattr(L, name):   # an older build under A/B timing: newer entry points absent
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

@@ -39,6 +39,8 @@ __global__ __launch_bounds__(L) void chan_kernel(const float2* __restrict__ hist
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     constexpr int Q = CHAN_Q, T = L / 16, LS = Lds<L>::LS;
     const int r = threadIdx.x;
+    float2* twl = lds + 16 * LS;                       // FFT twiddles staged once in LDS
+    twl[r] = tw[r];                                    // (L threads, L twiddles; first barrier orders it)
     const int m0 = blockIdx.x * fpw;
     const int m1 = min(m0 + fpw, frames);
     auto fetch = [&](long long b) -> float2 {          // buf[b] of [hist (H) || in (count)], 0 outside
@@ -62,8 +64,17 @@ __global__ __launch_bounds__(L) void chan_kernel(const float2* __restrict__ hist
         float h[Q];                                    // (re-read per batch from L2: not live across the FFT)
 #pragma unroll
         for (int q = 0; q < Q; q++) h[q] = taps[q * L + r];
+        // interior batch (all 16 rows inside `in`): per-row uniform base + the lane's r, so the
+        // 16 loads share one offset register instead of 16 64-bit addresses
+        const long long lo = offset0 + (long long)(mb + 15) * L, hi = offset0 + (long long)(mb + 31) * L + L;
+        if (mb + 16 <= m1 && lo >= H && hi <= (long long)H + count) {
+            const float2* __restrict__ src = in + (lo - H);
 #pragma unroll
-        for (int f = 0; f < 16; f++) nx[f] = (mb + f < m1) ? fetch(base + (long long)(mb + f + 15) * L) : make_float2(0.f, 0.f);
+            for (int f = 0; f < 16; f++) nx[f] = src[(long long)f * L + tid];
+        } else {
+#pragma unroll
+            for (int f = 0; f < 16; f++) nx[f] = (mb + f < m1) ? fetch(base + (long long)(mb + f + 15) * L) : make_float2(0.f, 0.f);
+        }
 #pragma unroll
         for (int f = 0; f < 16; f++) {
             xs[(f + 15) & 15] = nx[f];
@@ -85,10 +96,93 @@ __global__ __launch_bounds__(L) void chan_kernel(const float2* __restrict__ hist
         __syncthreads();
         const int m = mb + sF;
         float2* o = out + (long long)m * L;
-        stages_rest<L>(lds, tw, sF, tF, [&](int k, float2 y) {
+        stages_rest<L>(lds, twl, sF, tF, [&](int k, float2 y) {
             if (m < m1) o[k] = y;
         });
         __syncthreads();
+    }
+}
+
+// Two branches per thread (L/2 threads): the kernel above needs ~180 VGPRs and spills at
+// 1024 threads (128-VGPR cap); here each lane owns branches r and r + L/2 and plays two FFT
+// roles in turn (sequences sF and sF + 8), with a 256-VGPR cap at L/2 threads.
+template <int L>
+__global__ __launch_bounds__(L / 2) void chan2_kernel(const float2* __restrict__ hist, const float2* __restrict__ in, int H,
+                                                      int count, const float* __restrict__ taps, long long offset0,
+                                                      int rot, int frames, int fpw, const float2* __restrict__ tw,
+                                                      float2* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    constexpr int Q = CHAN_Q, T = L / 16, LS = Lds<L>::LS, NT = L / 2;
+    float2* twl = lds + 16 * LS;
+    twl[threadIdx.x] = tw[threadIdx.x];
+    twl[threadIdx.x + NT] = tw[threadIdx.x + NT];
+    const int m0 = blockIdx.x * fpw;
+    const int m1 = min(m0 + fpw, frames);
+    auto fetch = [&](long long b) -> float2 {
+        if (b < H) return hist[b];
+        const long long i = b - H;
+        return i < count ? in[i] : make_float2(0.f, 0.f);
+    };
+    float2 xs[2][16];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; h2++) {
+        const long long base = offset0 + threadIdx.x + h2 * NT;
+#pragma unroll
+        for (int q = 0; q < 15; q++) xs[h2][q] = fetch(base + (long long)(m0 + q) * L);
+        xs[h2][15] = make_float2(0.f, 0.f);
+    }
+    for (int mb = m0; mb < m1; mb += 16) {
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const long long lo = offset0 + (long long)(mb + 15) * L, hi = offset0 + (long long)(mb + 31) * L + L;
+        const bool inner = mb + 16 <= m1 && lo >= H && hi <= (long long)H + count;
+#pragma unroll
+        for (int h2 = 0; h2 < 2; h2++) {
+            const int r = tid + h2 * NT;
+            const int c = (rot + r) & (L - 1);
+            float2 nx[16];
+            float h[Q];
+#pragma unroll
+            for (int q = 0; q < Q; q++) h[q] = taps[q * L + r];
+            if (inner) {
+                const float2* __restrict__ src = in + (lo - H);
+#pragma unroll
+                for (int f = 0; f < 16; f++) nx[f] = src[(long long)f * L + r];
+            } else {
+                const long long base = offset0 + r;
+#pragma unroll
+                for (int f = 0; f < 16; f++) nx[f] = (mb + f < m1) ? fetch(base + (long long)(mb + f + 15) * L) : make_float2(0.f, 0.f);
+            }
+#pragma unroll
+            for (int f = 0; f < 16; f++) {
+                xs[h2][(f + 15) & 15] = nx[f];
+                float2 u = make_float2(0.f, 0.f);
+#pragma unroll
+                for (int q = 0; q < Q; q++) {
+                    const float2 x = xs[h2][(f + q) & 15];
+                    u.x = fmaf(h[q], x.x, u.x);
+                    u.y = fmaf(h[q], x.y, u.y);
+                }
+                lds[f * LS + pad16(c)] = u;
+            }
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int half = 0; half < 2; half++) {
+            const int sF = tid / T + 8 * half, tF = tid % T;
+            float2 v[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++) v[i] = lds[sF * LS + pad16(tF + i * T)];
+            __syncthreads();
+            stage_first<L>(lds + sF * LS, v, tF);
+            __syncthreads();
+            const int m = mb + sF;
+            float2* o = out + (long long)m * L;
+            stages_rest<L>(lds, twl, sF, tF, [&](int k, float2 y) {
+                if (m < m1) o[k] = y;
+            });
+            __syncthreads();
+        }
     }
 }
 
@@ -102,6 +196,9 @@ __global__ void chan_hist_kernel(const float2* __restrict__ hist, const float2* 
 
 struct ChannelizerBlock : Block {
     int M = 0, ntaps = 0, Hp = 0, offset = 0, fpw = 256;
+    // two branches per thread (chan2_kernel, no spill): 1.17 vs 1.63 ms per 2^28 samples
+    // against the one-branch kernel on one box; SDRGPU_CHAN_TWO=0 selects chan_kernel
+    bool two = true;
     long long phase = 0;     // absolute input index mod M of the next sample
     DevBuf taps, tw, hist[2];
     int cur = 0;
@@ -121,6 +218,7 @@ struct ChannelizerBlock : Block {
         ntaps = n;
         Hp = CHAN_Q * M - 1;
         if (const char* e = getenv("SDRGPU_CHAN_FPW")) fpw = std::max(16, atoi(e) / 16 * 16);
+        if (const char* e = getenv("SDRGPU_CHAN_TWO")) two = atoi(e) != 0;
         SDRGPU_CHECK(init_stream());
         std::vector<float> pq((size_t)CHAN_Q * M, 0.0f);       // [q][r] = h[q M + r]
         for (int j = 0; j < n; j++) pq[j] = t[j];
@@ -147,11 +245,11 @@ struct ChannelizerBlock : Block {
     }
     template <int L>
     int launch(const void* in, int count, int frames, long long offset0, int rot, void* out, hipStream_t s) {
-        auto k = chan_kernel<L>;
-        const size_t lds = sizeof(float2) * 16 * Lds<L>::LS;
+        auto k = two ? chan2_kernel<L> : chan_kernel<L>;
+        const size_t lds = sizeof(float2) * (16 * Lds<L>::LS + L);
         SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         const int grid = (frames + fpw - 1) / fpw;
-        hipLaunchKernelGGL(k, dim3(grid), dim3(L), lds, s, hist[cur].as<float2>(), (const float2*)in, Hp, count,
+        hipLaunchKernelGGL(k, dim3(grid), dim3(two ? L / 2 : L), lds, s, hist[cur].as<float2>(), (const float2*)in, Hp, count,
                            taps.as<float>(), offset0, rot, frames, fpw, tw.as<float2>(), (float2*)out);
         SDRGPU_HIP(hipGetLastError());
         return SDRGPU_OK;

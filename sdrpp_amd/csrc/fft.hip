@@ -321,8 +321,10 @@ struct FftPlan {
     PinnedBuf pin_in, pin_out;
     DevBuf dev_in, dev_out;
     // two-stream chunk pipeline: pass A of chunk i+1 (caller stream) overlaps pass B of chunk
-    // i (second stream); scratch is double-buffered
-    int pipe = 1;
+    // i (second stream), scratch double-buffered. Measured SLOWER (64k: 2.16 vs 1.86 ms, 1M:
+    // 2.98 vs 2.39 ms per step; the concurrent passes evict each other's Infinity-Cache
+    // working set), so it is off unless SDRGPU_FFT_PIPE=1.
+    int pipe = 0;
     hipStream_t s2 = nullptr;
     hipEvent_t evFork = nullptr, evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr};
     DevBuf scratch2;
