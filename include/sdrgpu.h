@@ -160,7 +160,34 @@ int sdrgpu_block_out_count(sdrgpu_block* h, int count);   /* exact output count 
 int sdrgpu_block_reset(sdrgpu_block* h);
 int sdrgpu_block_destroy(sdrgpu_block* h);
 
+/* ------------------------------------------------- device IQ front end ---- */
+/* IQFrontEnd's data path on the device (signal_path/iq_frontend.cpp:15-52, 115-249; SURVEY
+ * 8f rank 1): ingest conversion -> [PowerDecimator] -> [DCBlocker] -> [Conjugate] -> VFOs
+ * (RxVFO, read in place) + spectrum frames (Reshaper keep = nz / skip from genReshapeParams,
+ * window * FFT * log-power). Replaces the SampleFrameBuffer -> Splitter -> Reshaper memcpy
+ * fan-out: one H2D per sample, every consumer reads the block from HBM.
+ * kind: -1 complex float, else SDRGPU_CONV_* (interleaved IQ of that sample format). */
+typedef struct sdrgpu_frontend sdrgpu_frontend;
+int sdrgpu_frontend_create(sdrgpu_frontend** f, int device, double sampleRate, int decimRatio, int dcBlocking,
+                           int fftSize, double fftRate, int windowType);                    /* IQFrontEnd::init */
+int sdrgpu_frontend_destroy(sdrgpu_frontend* f);
+int sdrgpu_frontend_configure(sdrgpu_frontend* f, double sampleRate, int decimRatio, int dcBlocking); /* setSampleRate/setDecimation/setDCBlocking */
+int sdrgpu_frontend_set_invert_iq(sdrgpu_frontend* f, int enabled);                       /* setInvertIQ */
+int sdrgpu_frontend_set_fft(sdrgpu_frontend* f, int fftSize, double fftRate, int windowType);  /* setFFTSize/Rate/Window */
+int sdrgpu_frontend_framing(sdrgpu_frontend* f, int* nz, int* skip, double* effectiveSampleRate);
+int sdrgpu_frontend_add_vfo(sdrgpu_frontend* f, int* id, double outSampleRate, double bandwidth, double offset); /* addVFO */
+int sdrgpu_frontend_remove_vfo(sdrgpu_frontend* f, int id);                                /* removeVFO */
+int sdrgpu_frontend_set_vfo_offset(sdrgpu_frontend* f, int id, double offset);
+/* push a block; returns the number of spectrum rows completed by it */
+int sdrgpu_frontend_push(sdrgpu_frontend* f, const void* in, int count, int kind);          /* host block (synchronous) */
+int sdrgpu_frontend_push_dev(sdrgpu_frontend* f, const void* in, int count, int kind, void* stream); /* device block (async) */
+int sdrgpu_frontend_spectra_dev(sdrgpu_frontend* f, const float** rows, int* nrows);       /* returns N */
+int sdrgpu_frontend_read_spectra(sdrgpu_frontend* f, float* out, int maxRows);
+int sdrgpu_frontend_vfo_dev(sdrgpu_frontend* f, int id, const void** out, int* n);
+int sdrgpu_frontend_read_vfo(sdrgpu_frontend* f, int id, void* out, int max);
+
 /* ------------------------------------------------------------ ingest ---- */
+
 /* file_source / rtl_sdr / hackrf sample converters (elementwise, n scalars):
  * kind 0 u8 (b-128+0.5f)/127.5f, 1 i16 (s+0.5f)/32767.5f, 2 i24 packed LE,
  * 3 i32 ((v+0.5)/(2^31-0.5) in double), 4 f64 -> f32, 5 i8 x*(1/128) */

@@ -85,6 +85,21 @@ def _load():
         "sdrgpu_wfm_create": (i, [pp, i, d, d, i]),
         "sdrgpu_channelizer_create": (i, [pp, i, i, fp, i]),
         "sdrgpu_broadcast_fm_create": (i, [pp, i, d, d, i, i]),
+        "sdrgpu_frontend_create": (i, [pp, i, d, i, i, i, d, i]),
+        "sdrgpu_frontend_destroy": (i, [vp]),
+        "sdrgpu_frontend_configure": (i, [vp, d, i, i]),
+        "sdrgpu_frontend_set_invert_iq": (i, [vp, i]),
+        "sdrgpu_frontend_set_fft": (i, [vp, i, d, i]),
+        "sdrgpu_frontend_framing": (i, [vp, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(d)]),
+        "sdrgpu_frontend_add_vfo": (i, [vp, ctypes.POINTER(i), d, d, d]),
+        "sdrgpu_frontend_remove_vfo": (i, [vp, i]),
+        "sdrgpu_frontend_set_vfo_offset": (i, [vp, i, d]),
+        "sdrgpu_frontend_push": (i, [vp, vp, i, i]),
+        "sdrgpu_frontend_push_dev": (i, [vp, vp, i, i, vp]),
+        "sdrgpu_frontend_spectra_dev": (i, [vp, pp, ctypes.POINTER(i)]),
+        "sdrgpu_frontend_read_spectra": (i, [vp, fp, i]),
+        "sdrgpu_frontend_vfo_dev": (i, [vp, i, pp, ctypes.POINTER(i)]),
+        "sdrgpu_frontend_read_vfo": (i, [vp, i, vp, i]),
         "sdrgpu_agc_create": (i, [pp, i, i, d, d, d, d, d, d]),
         "sdrgpu_agc_set_enabled": (i, [vp, i]),
         "sdrgpu_agc_set_gain": (i, [vp, ctypes.c_float]),

@@ -25,6 +25,7 @@ SOURCES = [
     ("blocks.hip", []),
     ("channelizer.hip", []),
     ("loops.hip", ["-ffp-contract=off"]),   # bit-exact serial recurrences
+    ("frontend.hip", []),
 ]
 
 

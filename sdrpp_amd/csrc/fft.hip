@@ -93,13 +93,14 @@ __global__ __launch_bounds__(S * L / 16) void fft_single_kernel(
 // Column c of the frame viewed as N1 x N2: x[n1*N2 + c0 + c]. The column index is the
 // fastest-varying thread coordinate in both the load and the store, so each wave reads
 // and writes whole 128-B row segments (S = 16 columns x 8 B).
-// Four-step twiddle W_N^(n2 k1), n2 = c0 + c = S*b + c:
-//   W_N^(S b k1) from Tbase[b][k1] (one value per 16 lanes) x W_N^(c k1) from Tcol[k1][c]
-// (contiguous per 16 lanes); both fp64-generated, one complex product.
+// Four-step twiddle W_N^(n2 k1), n2 = S*b + c: one load of the exact fp64-generated value
+// from the N-entry Tfull[k1][n2] table (contiguous per 16 lanes, L2-resident). A product of
+// two table values (W_N^(S b k1) x W_N^(c k1)) saved a little table space but added an
+// fp32 rounding: the 64k spectrum's rms dB error on a tonal signal was 2.1x pocketfft's.
 template <int L, int S>
 __global__ __launch_bounds__(S * L / 16) void fft_passA_kernel(
     const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
-    int logN, const float2* __restrict__ tw, const float2* __restrict__ tbase, const float2* __restrict__ tcol,
+    int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull,
     float2* __restrict__ scratch) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int tid = threadIdx.x;
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(S * L / 16) void fft_passA_kernel(
         [&](int tile, int k1, float2 y) {
             const int b = tile % nb;
             const long long f = tile / nb;
-            const float2 t0 = cmul(tbase[(long long)b * L + k1], tcol[k1 * S + c]);
+            const float2 t0 = tfull[(long long)k1 * N2 + b * S + c];   // exact W_N^(n2 k1)
             scratch[(f << logN) + (long long)k1 * N2 + b * S + c] = cmul(y, t0);
         });
 }
@@ -310,12 +311,11 @@ __global__ __launch_bounds__(S * L / 16) void fft_passB_kernel(
 struct FftPlan {
     int device = 0, N = 0, logN = 0, nz = 0;
     int N1 = 0, N2 = 0;               // two-pass split (N1 * N2 = N); N1 = 0 -> single pass
-    DevBuf win, tw1, tw2, tbase, tcol, tfull, scratch;
+    DevBuf win, tw1, tw2, tfull, scratch;
     int chunkFrames = 1;
     int sa = 16, sb = 32;             // pass-A columns / pass-B rows per workgroup (tuning)
     int dbg = 0;                      // timing-only ablations (SDRGPU_FFT_DEBUG; wrong results)
     float2* cur = nullptr;            // scratch buffer of the chunk being launched
-    int tcolS = 0;                    // columns of the [k1][c] twiddle table
     int sa2 = 0;                      // paired pass-A columns per workgroup (0: paired kernel off)
     hipStream_t own = nullptr;
     PinnedBuf pin_in, pin_out;
@@ -363,13 +363,12 @@ static int launch_single(const FftPlan& p, const float2* in, long long stride, i
 
 template <int L, int S>
 static int launch_passA(const FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
-    if (p.tcolS != S) { set_error("fft: column twiddle table built for %d columns, kernel uses %d", p.tcolS, S); return SDRGPU_ESTATE; }
     auto k = fft_passA_kernel<L, S>;
     size_t lds = sizeof(float2) * S * Lds<L>::LS;
     SDRGPU_CHECK(set_lds(k, lds));
     const int g = (p.N2 / S) * frames;
     hipLaunchKernelGGL(k, dim3(g), dim3(S * L / 16), lds, s, in, stride, frames, p.win.as<float>(), p.nz, p.N2,
-                       p.logN, p.tw1.as<float2>(), p.tbase.as<float2>(), p.tcol.as<float2>(), p.cur);
+                       p.logN, p.tw1.as<float2>(), p.tfull.as<float2>(), p.cur);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
@@ -498,6 +497,10 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         rc = make_twiddles(p.tw1, fftSize);
     } else {
         p.N1 = 1 << ((logN + 1) / 2);   // N1 >= N2, both <= 1024
+        if (const char* e = getenv("SDRGPU_FFT_N1")) {   // (tuning) another split, N1, N2 in [64, 1024]
+            const int n1 = atoi(e);
+            if (n1 >= 64 && n1 <= 1024 && (n1 & (n1 - 1)) == 0 && fftSize / n1 >= 64 && fftSize / n1 <= 1024) p.N1 = n1;
+        }
         p.N2 = fftSize / p.N1;
         rc = make_twiddles(p.tw1, p.N1);
         if (rc >= 0) rc = make_twiddles(p.tw2, p.N2);
@@ -511,43 +514,12 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         if (const char* e = getenv("SDRGPU_FFT_DEBUG")) p.dbg = atoi(e);
         if (const char* e = getenv("SDRGPU_FFT_PIPE")) p.pipe = atoi(e);
         p.chunkFrames = std::max(1, (int)((chunkMB << 20) / ((long long)fftSize * 8)));
-        // pass-A columns per workgroup actually dispatched for this N1 (see dispatch_passA)
-        p.tcolS = (p.N1 == 256) ? (p.sa == 64 ? 64 : p.sa == 32 ? 32 : 16)
-                : (p.N1 == 512) ? 8 : (p.N1 == 1024) ? (p.sa == 16 ? 16 : 8) : 16;
-        if (rc >= 0) {   // Tbase[b][k1] = W_N^(S b k1) for the N2/S column blocks
-            const int nb = p.N2 / p.tcolS;
-            std::vector<float2> t((size_t)nb * p.N1);
-            for (int b = 0; b < nb; b++)
-                for (int k1 = 0; k1 < p.N1; k1++) {
-                    const long long m = ((long long)b * p.tcolS * k1) % fftSize;
-                    const double a = -2.0 * M_PI * (double)m / (double)fftSize;
-                    t[(size_t)b * p.N1 + k1] = make_float2((float)std::cos(a), (float)std::sin(a));
-                }
-            rc = p.tbase.ensure(sizeof(float2) * t.size());
-            if (rc >= 0 && hipMemcpy(p.tbase.p, t.data(), sizeof(float2) * t.size(), hipMemcpyHostToDevice) != hipSuccess) {
-                set_error("fft: twiddle upload failed");
-                rc = SDRGPU_EHIP;
-            }
-        }
-        if (rc >= 0) {
-            std::vector<float2> t((size_t)p.N1 * p.tcolS);
-            for (int k1 = 0; k1 < p.N1; k1++)
-                for (int c = 0; c < p.tcolS; c++) {
-                    const double a = -2.0 * M_PI * (double)((long long)c * k1) / (double)fftSize;
-                    t[(size_t)k1 * p.tcolS + c] = make_float2((float)std::cos(a), (float)std::sin(a));
-                }
-            rc = p.tcol.ensure(sizeof(float2) * t.size());
-            if (rc >= 0 && hipMemcpy(p.tcol.p, t.data(), sizeof(float2) * t.size(), hipMemcpyHostToDevice) != hipSuccess) {
-                set_error("fft: twiddle upload failed");
-                rc = SDRGPU_EHIP;
-            }
-        }
         // paired-column pass A: +13% on the 1M transform (N1 = 1024), but slower than the
         // one-column kernel at N1 = 256 (64k: 2.05-2.10 vs 1.86 ms per 2^28 samples, A/B on
         // one box), so it is the default only for N1 >= 512
         p.sa2 = p.N1 >= 512 ? 16 : 0;
         if (const char* e = getenv("SDRGPU_FFT_SA2")) p.sa2 = atoi(e);
-        if (rc >= 0 && p.sa2 > 0) {   // Tfull[k1][n2] = W_N^(n2 k1), exact argument mod N
+        if (rc >= 0) {   // Tfull[k1][n2] = W_N^(n2 k1), exact argument mod N (both pass-A kernels)
             std::vector<float2> t((size_t)fftSize);
             for (int k1 = 0; k1 < p.N1; k1++)
                 for (int n2 = 0; n2 < p.N2; n2++) {

@@ -1,0 +1,362 @@
+// Device-resident IQ front end: the MI355X replacement of IQFrontEnd's data path
+// (signal_path/iq_frontend.cpp:15-52, 115-249) and of the host fan-out it runs on
+// (buffer/frame_buffer.h SampleFrameBuffer -> routing/splitter.h Splitter -> one memcpy per
+// VFO + buffer/reshaper.h Reshaper -> FFT handler). SURVEY.md §8f rank 1.
+//
+// One push of a source block does, all on one HIP stream:
+//   [H2D of the raw block] -> ingest conversion (u8/i16/i24/i32/f64/i8 or complex float,
+//   file_source/src/main.cpp:361-542) -> [PowerDecimator] -> [DCBlocker<complex_t>]
+//   -> [Conjugate] -> every VFO (RxVFO) reads the block in place, and the spectrum frames
+//   whose samples are complete are transformed straight out of the block.
+// Framing is the Reshaper's keep/skip (reshaper.h:100-127, keep = nz, skip from
+// genReshapeParams, iq_frontend.h:56-60): frame j covers samples [j*(nz+skip), j*(nz+skip)+nz)
+// of the preprocessed stream. Only the (at most one) frame straddling two pushes is
+// stitched, from a device tail buffer of < nz samples; every other frame is read in place,
+// so each sample crosses PCIe once and is read from HBM once per consumer.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <vector>
+#include "sdrgpu_internal.h"
+
+namespace sdrgpu {
+__global__ void conjugate_kernel(float2* __restrict__ x, int n) {   // math/conjugate.h
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) x[i].y = -x[i].y;
+}
+}  // namespace sdrgpu
+
+using namespace sdrgpu;
+
+namespace {
+struct VfoSlot {
+    sdrgpu_block* vfo = nullptr;
+    DevBuf out;
+    PinnedBuf pin;
+    int n = 0;
+};
+const int kConvSize[] = {1, 2, 3, 4, 8, 1};   // bytes per real value of SDRGPU_CONV_U8..I8
+}  // namespace
+
+struct sdrgpu_frontend {
+    int device = 0;
+    double sampleRate = 0, fftRate = 0, effSr = 0;
+    int decim = 1, fftSize = 0, window = 0, nz = 0, skip = 0;
+    bool dcBlocking = false, invertIQ = false;
+    hipStream_t s = nullptr;
+    sdrgpu_block* decimB = nullptr;
+    sdrgpu_block* dcb = nullptr;
+    sdrgpu_fft* fft = nullptr;
+    PinnedBuf pin, pinSpec;
+    DevBuf raw, conv, pre, tail[2], stitch, spectra;
+    int curTail = 0;
+    long long total = 0;      // preprocessed samples seen before this push
+    long long nextFrame = 0;  // absolute start of the next spectrum frame
+    int tailLen = 0;          // device tail = samples [total - tailLen, total), all >= nextFrame
+    int nSpec = 0;
+    int nextVfoId = 1;
+    std::map<int, VfoSlot> vfos;
+    long long stride() const { return (long long)nz + skip; }
+};
+
+static void destroy_parts(sdrgpu_frontend* f) {
+    if (f->decimB) sdrgpu_block_destroy(f->decimB);
+    if (f->dcb) sdrgpu_block_destroy(f->dcb);
+    if (f->fft) sdrgpu_fft_destroy(f->fft);
+    f->decimB = f->dcb = nullptr;
+    f->fft = nullptr;
+}
+
+// IQFrontEnd::updateFFTPath / updateFFTSize (iq_frontend.cpp:251-296): reshaper keep/skip and plan
+static int fe_update_fft(sdrgpu_frontend* f) {
+    int skip = 0, nz = 0;
+    sdrgpu_gen_reshape_params(f->effSr, f->fftSize, f->fftRate, &skip, &nz);
+    if (nz < 1 || skip < 0) { set_error("frontend: bad FFT framing (size %d, rate %g)", f->fftSize, f->fftRate); return SDRGPU_EARG; }
+    if (f->fft) sdrgpu_fft_destroy(f->fft);
+    f->fft = nullptr;
+    SDRGPU_CHECK(sdrgpu_fft_create(&f->fft, f->device, f->fftSize, nz, f->window));
+    f->nz = nz;
+    f->skip = skip;
+    // the reshaper restarts on a path update: the next frame starts at the next sample
+    f->nextFrame = f->total;
+    f->tailLen = 0;
+    return SDRGPU_OK;
+}
+
+// preproc chain of IQFrontEnd::init (iq_frontend.cpp:29-39)
+static int fe_build_preproc(sdrgpu_frontend* f) {
+    if (f->decimB) sdrgpu_block_destroy(f->decimB);
+    if (f->dcb) sdrgpu_block_destroy(f->dcb);
+    f->decimB = f->dcb = nullptr;
+    f->effSr = f->sampleRate / f->decim;
+    if (f->decim > 1) SDRGPU_CHECK(sdrgpu_power_decimator_create(&f->decimB, f->device, SDRGPU_C64, f->decim));
+    if (f->dcBlocking) SDRGPU_CHECK(sdrgpu_dc_blocker_create(&f->dcb, f->device, SDRGPU_C64, 50.0 / f->effSr));   // genDCBlockRate
+    return SDRGPU_OK;
+}
+
+extern "C" int sdrgpu_frontend_create(sdrgpu_frontend** out, int device, double sampleRate, int decimRatio, int dcBlocking,
+                                      int fftSize, double fftRate, int windowType) {
+    if (!out || !(sampleRate > 0) || decimRatio < 1 || !(fftRate > 0)) { set_error("frontend_create: bad argument"); return SDRGPU_EARG; }
+    *out = nullptr;
+    SDRGPU_SET_DEVICE(device);
+    auto* f = new sdrgpu_frontend();
+    f->device = device;
+    f->sampleRate = sampleRate;
+    f->decim = decimRatio;
+    f->dcBlocking = dcBlocking != 0;
+    f->fftSize = fftSize;
+    f->fftRate = fftRate;
+    f->window = windowType;
+    int rc = hipStreamCreateWithFlags(&f->s, hipStreamNonBlocking) == hipSuccess ? SDRGPU_OK : SDRGPU_EHIP;
+    if (rc < 0) set_error("frontend_create: hipStreamCreate failed");
+    if (rc >= 0) rc = fe_build_preproc(f);
+    if (rc >= 0) rc = fe_update_fft(f);
+    if (rc < 0) {
+        destroy_parts(f);
+        if (f->s) (void)hipStreamDestroy(f->s);
+        delete f;
+        return rc;
+    }
+    *out = f;
+    return SDRGPU_OK;
+}
+
+extern "C" int sdrgpu_frontend_destroy(sdrgpu_frontend* f) {
+    if (!f) return SDRGPU_OK;
+    (void)hipSetDevice(f->device);
+    if (f->s) (void)hipStreamSynchronize(f->s);
+    for (auto& [id, v] : f->vfos) sdrgpu_block_destroy(v.vfo);
+    destroy_parts(f);
+    if (f->s) (void)hipStreamDestroy(f->s);
+    delete f;
+    return SDRGPU_OK;
+}
+
+#define NEED_FE(f) do { if (!(f)) { set_error("null frontend"); return SDRGPU_EARG; } } while (0)
+
+// setSampleRate / setDecimation / setDCBlocking (iq_frontend.cpp:54-106): VFOs follow the new rate
+extern "C" int sdrgpu_frontend_configure(sdrgpu_frontend* f, double sampleRate, int decimRatio, int dcBlocking) {
+    NEED_FE(f);
+    if (!(sampleRate > 0) || decimRatio < 1) { set_error("frontend_configure: bad argument"); return SDRGPU_EARG; }
+    SDRGPU_SET_DEVICE(f->device);
+    SDRGPU_HIP(hipStreamSynchronize(f->s));
+    f->sampleRate = sampleRate;
+    f->decim = decimRatio;
+    f->dcBlocking = dcBlocking != 0;
+    SDRGPU_CHECK(fe_build_preproc(f));
+    SDRGPU_CHECK(fe_update_fft(f));
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_frontend_set_invert_iq(sdrgpu_frontend* f, int enabled) {
+    NEED_FE(f);
+    f->invertIQ = enabled != 0;
+    return SDRGPU_OK;
+}
+// setFFTSize / setFFTRate / setFFTWindow (iq_frontend.cpp:173-186)
+extern "C" int sdrgpu_frontend_set_fft(sdrgpu_frontend* f, int fftSize, double fftRate, int windowType) {
+    NEED_FE(f);
+    if (!(fftRate > 0)) { set_error("frontend_set_fft: bad rate"); return SDRGPU_EARG; }
+    SDRGPU_SET_DEVICE(f->device);
+    SDRGPU_HIP(hipStreamSynchronize(f->s));
+    f->fftSize = fftSize;
+    f->fftRate = fftRate;
+    f->window = windowType;
+    return fe_update_fft(f);
+}
+extern "C" int sdrgpu_frontend_framing(sdrgpu_frontend* f, int* nz, int* skip, double* effectiveSampleRate) {
+    NEED_FE(f);
+    if (nz) *nz = f->nz;
+    if (skip) *skip = f->skip;
+    if (effectiveSampleRate) *effectiveSampleRate = f->effSr;
+    return SDRGPU_OK;
+}
+
+// addVFO / removeVFO (iq_frontend.cpp:115-160): an RxVFO fed from the device block in place
+extern "C" int sdrgpu_frontend_add_vfo(sdrgpu_frontend* f, int* id, double outSampleRate, double bandwidth, double offset) {
+    NEED_FE(f);
+    if (!id) { set_error("frontend_add_vfo: null id"); return SDRGPU_EARG; }
+    VfoSlot v;
+    SDRGPU_CHECK(sdrgpu_rxvfo_create(&v.vfo, f->device, f->effSr, outSampleRate, bandwidth, offset));
+    *id = f->nextVfoId++;
+    f->vfos[*id] = std::move(v);
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_frontend_remove_vfo(sdrgpu_frontend* f, int id) {
+    NEED_FE(f);
+    auto it = f->vfos.find(id);
+    if (it == f->vfos.end()) { set_error("frontend: no VFO %d", id); return SDRGPU_EARG; }
+    SDRGPU_SET_DEVICE(f->device);
+    SDRGPU_HIP(hipStreamSynchronize(f->s));
+    sdrgpu_block_destroy(it->second.vfo);
+    f->vfos.erase(it);
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_frontend_set_vfo_offset(sdrgpu_frontend* f, int id, double offset) {
+    NEED_FE(f);
+    auto it = f->vfos.find(id);
+    if (it == f->vfos.end()) { set_error("frontend: no VFO %d", id); return SDRGPU_EARG; }
+    return sdrgpu_rxvfo_set_offset(it->second.vfo, offset);
+}
+
+// Core of a push: the preprocessed block `x` (m samples, device) -> VFOs + spectrum frames.
+static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s) {
+    for (auto& [id, v] : f->vfos) {
+        const int want = sdrgpu_block_out_count(v.vfo, m);
+        if (want < 0) return want;
+        SDRGPU_CHECK(v.out.ensure(sizeof(float2) * (size_t)std::max(want, 1)));
+        const int n = m > 0 ? sdrgpu_block_process_dev(v.vfo, x, m, v.out.p, s) : 0;
+        if (n < 0) return n;
+        v.n = n;
+    }
+    // frames with start s_j = nextFrame + j*stride and s_j + nz <= total + m
+    const long long T = f->total, st = f->stride();
+    int nf = 0;
+    if (T + m >= f->nextFrame + f->nz) nf = (int)((T + m - f->nextFrame - f->nz) / st) + 1;
+    SDRGPU_CHECK(f->spectra.ensure(sizeof(float) * (size_t)std::max(nf, 1) * f->fftSize));
+    float* spec = f->spectra.as<float>();
+    int done = 0;
+    if (nf > 0 && f->nextFrame < T) {
+        // the one frame straddling the previous push: [tail (tailLen) || x[0 : nz - tailLen])
+        const int head = (int)(T - f->nextFrame);   // == tailLen
+        SDRGPU_CHECK(f->stitch.ensure(sizeof(float2) * f->nz));
+        SDRGPU_HIP(hipMemcpyAsync(f->stitch.p, f->tail[f->curTail].p, sizeof(float2) * head, hipMemcpyDeviceToDevice, s));
+        SDRGPU_HIP(hipMemcpyAsync(f->stitch.as<float2>() + head, x, sizeof(float2) * (f->nz - head), hipMemcpyDeviceToDevice, s));
+        SDRGPU_CHECK(sdrgpu_fft_execute_dev(f->fft, f->stitch.p, f->nz, 1, spec, s));
+        done = 1;
+    }
+    if (nf > done) {   // frames entirely inside this block, read in place with the reshaper's stride
+        const long long first = f->nextFrame + done * st - T;
+        SDRGPU_CHECK(sdrgpu_fft_execute_dev(f->fft, x + first, st, nf - done, spec + (size_t)done * f->fftSize, s));
+    }
+    f->nSpec = nf;
+    f->nextFrame += (long long)nf * st;
+    // new tail: samples [nextFrame, T + m) (fewer than nz), from the old tail and/or this block
+    const long long end = T + m;
+    int newLen = 0;
+    if (f->nextFrame < end) {
+        newLen = (int)(end - f->nextFrame);
+        const int nb = (int)(f->curTail ^ 1);
+        SDRGPU_CHECK(f->tail[0].ensure(sizeof(float2) * f->nz));
+        SDRGPU_CHECK(f->tail[1].ensure(sizeof(float2) * f->nz));
+        float2* dst = f->tail[nb].as<float2>();
+        int fromOld = 0;
+        if (f->nextFrame < T) {   // keep part of the old tail (no frame completed)
+            fromOld = (int)(T - f->nextFrame);
+            const int oldOff = f->tailLen - fromOld;
+            SDRGPU_HIP(hipMemcpyAsync(dst, f->tail[f->curTail].as<float2>() + oldOff, sizeof(float2) * fromOld,
+                                      hipMemcpyDeviceToDevice, s));
+        }
+        const long long fromBlock = newLen - fromOld;
+        if (fromBlock > 0)
+            SDRGPU_HIP(hipMemcpyAsync(dst + fromOld, x + (m - fromBlock), sizeof(float2) * fromBlock, hipMemcpyDeviceToDevice, s));
+        f->curTail = nb;
+    }
+    f->tailLen = newLen;
+    f->total = end;
+    return nf;
+}
+
+// preprocessing of a converted full-rate block in `conv` (n samples) -> f->pre / returned pointer
+static int fe_preproc(sdrgpu_frontend* f, const float2* in, int n, hipStream_t s, const float2** outp) {
+    const float2* x = in;
+    int m = n;
+    if (f->decimB) {
+        const int want = sdrgpu_block_out_count(f->decimB, n);
+        if (want < 0) return want;
+        SDRGPU_CHECK(f->pre.ensure(sizeof(float2) * (size_t)std::max(want, 1)));
+        m = n > 0 ? sdrgpu_block_process_dev(f->decimB, x, n, f->pre.p, s) : 0;
+        if (m < 0) return m;
+        x = f->pre.as<float2>();
+    }
+    if ((f->dcb || f->invertIQ) && x == in) {   // in-place stages need a private copy of the caller's block
+        SDRGPU_CHECK(f->pre.ensure(sizeof(float2) * (size_t)std::max(m, 1)));
+        SDRGPU_HIP(hipMemcpyAsync(f->pre.p, x, sizeof(float2) * m, hipMemcpyDeviceToDevice, s));
+        x = f->pre.as<float2>();
+    }
+    if (f->dcb && m > 0) {
+        const int r = sdrgpu_block_process_dev(f->dcb, x, m, (void*)x, s);
+        if (r < 0) return r;
+    }
+    if (f->invertIQ && m > 0) {
+        hipLaunchKernelGGL(conjugate_kernel, dim3((m + 255) / 256), dim3(256), 0, s, (float2*)x, m);
+        SDRGPU_HIP(hipGetLastError());
+    }
+    *outp = x;
+    return m;
+}
+
+// Device-resident block (complex float, or raw `kind` samples), caller stream (NULL = own).
+// Returns the number of spectrum rows produced; rows and VFO outputs stay on the device.
+extern "C" int sdrgpu_frontend_push_dev(sdrgpu_frontend* f, const void* in, int count, int kind, void* stream) {
+    NEED_FE(f);
+    if (count < 0 || (count > 0 && !in) || kind < -1 || kind > SDRGPU_CONV_I8) { set_error("frontend_push: bad argument"); return SDRGPU_EARG; }
+    SDRGPU_SET_DEVICE(f->device);
+    hipStream_t s = stream ? (hipStream_t)stream : f->s;
+    const float2* x = (const float2*)in;
+    if (kind >= 0 && count > 0) {
+        SDRGPU_CHECK(f->conv.ensure(sizeof(float2) * count));
+        SDRGPU_CHECK(sdrgpu_convert_dev(f->device, kind, in, 2LL * count, f->conv.as<float>(), s));
+        x = f->conv.as<float2>();
+    }
+    const float2* p = nullptr;
+    const int m = fe_preproc(f, x, count, s, &p);
+    if (m < 0) return m;
+    return fe_consume(f, p, m, s);
+}
+
+// Host block (the drop-in call style): one H2D of the raw bytes, then as push_dev on the
+// frontend's stream; synchronises so the host can read the results.
+extern "C" int sdrgpu_frontend_push(sdrgpu_frontend* f, const void* in, int count, int kind) {
+    NEED_FE(f);
+    if (count < 0 || (count > 0 && !in) || kind < -1 || kind > SDRGPU_CONV_I8) { set_error("frontend_push: bad argument"); return SDRGPU_EARG; }
+    SDRGPU_SET_DEVICE(f->device);
+    const size_t bytes = (size_t)count * (kind < 0 ? sizeof(float2) : 2 * kConvSize[kind]);
+    if (count > 0) {
+        SDRGPU_CHECK(f->pin.ensure(bytes));
+        SDRGPU_CHECK(f->raw.ensure(bytes));
+        SDRGPU_HIP(hipStreamSynchronize(f->s));   // the staging buffer is reused
+        std::memcpy(f->pin.p, in, bytes);
+        SDRGPU_HIP(hipMemcpyAsync(f->raw.p, f->pin.p, bytes, hipMemcpyHostToDevice, f->s));
+    }
+    const int nf = sdrgpu_frontend_push_dev(f, count > 0 ? f->raw.p : nullptr, count, kind, f->s);
+    if (nf < 0) return nf;
+    SDRGPU_HIP(hipStreamSynchronize(f->s));
+    return nf;
+}
+
+// results of the last push: device pointers (push_dev) or host copies (drop-in)
+extern "C" int sdrgpu_frontend_spectra_dev(sdrgpu_frontend* f, const float** rows, int* nrows) {
+    NEED_FE(f);
+    if (rows) *rows = f->spectra.as<float>();
+    if (nrows) *nrows = f->nSpec;
+    return f->fftSize;
+}
+extern "C" int sdrgpu_frontend_read_spectra(sdrgpu_frontend* f, float* out, int maxRows) {
+    NEED_FE(f);
+    const int n = std::min(maxRows, f->nSpec);
+    if (n <= 0) return 0;
+    SDRGPU_SET_DEVICE(f->device);
+    SDRGPU_HIP(hipStreamSynchronize(f->s));
+    SDRGPU_HIP(hipMemcpy(out, f->spectra.p, sizeof(float) * (size_t)n * f->fftSize, hipMemcpyDeviceToHost));
+    return n;
+}
+extern "C" int sdrgpu_frontend_vfo_dev(sdrgpu_frontend* f, int id, const void** out, int* n) {
+    NEED_FE(f);
+    auto it = f->vfos.find(id);
+    if (it == f->vfos.end()) { set_error("frontend: no VFO %d", id); return SDRGPU_EARG; }
+    if (out) *out = it->second.out.p;
+    if (n) *n = it->second.n;
+    return it->second.n;
+}
+extern "C" int sdrgpu_frontend_read_vfo(sdrgpu_frontend* f, int id, void* out, int max) {
+    NEED_FE(f);
+    auto it = f->vfos.find(id);
+    if (it == f->vfos.end()) { set_error("frontend: no VFO %d", id); return SDRGPU_EARG; }
+    const int n = std::min(max, it->second.n);
+    if (n <= 0) return 0;
+    SDRGPU_SET_DEVICE(f->device);
+    SDRGPU_HIP(hipStreamSynchronize(f->s));
+    SDRGPU_HIP(hipMemcpy(out, it->second.out.p, sizeof(float2) * (size_t)n, hipMemcpyDeviceToHost));
+    return n;
+}

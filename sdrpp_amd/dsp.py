@@ -313,6 +313,76 @@ class SSB(Block):
         super().__init__(h, np.complex64, STEREO if stereo else np.float32)
 
 
+class IQFrontEnd:
+    """Device IQ front end (signal_path/iq_frontend.cpp; include/sdrgpu.h sdrgpu_frontend_*):
+    ingest conversion -> [decimation] -> [DC block] -> [IQ inversion] -> VFOs + spectrum rows.
+    ``push(block, kind=-1)`` takes a host block (complex64, or raw interleaved samples of a
+    SDRGPU_CONV_* kind) and returns the dB rows completed by it; ``vfo_output(id)`` is that
+    VFO's output for the block."""
+
+    def __init__(self, sample_rate, decim=1, dc_blocking=False, fft_size=65536, fft_rate=15.0, window=6, device=0):
+        self._h = _make(lib.sdrgpu_frontend_create, device, float(sample_rate), int(decim), int(bool(dc_blocking)),
+                        int(fft_size), float(fft_rate), int(window))
+        self.fft_size = int(fft_size)
+
+    def framing(self):
+        nz, skip, sr = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
+        check(lib.sdrgpu_frontend_framing(self._h, ctypes.byref(nz), ctypes.byref(skip), ctypes.byref(sr)))
+        return nz.value, skip.value, sr.value
+
+    def configure(self, sample_rate, decim=1, dc_blocking=False):
+        check(lib.sdrgpu_frontend_configure(self._h, float(sample_rate), int(decim), int(bool(dc_blocking))))
+
+    def set_invert_iq(self, enabled):
+        check(lib.sdrgpu_frontend_set_invert_iq(self._h, int(bool(enabled))))
+
+    def set_fft(self, fft_size, fft_rate, window=6):
+        check(lib.sdrgpu_frontend_set_fft(self._h, int(fft_size), float(fft_rate), int(window)))
+        self.fft_size = int(fft_size)
+
+    def add_vfo(self, out_sr, bandwidth, offset):
+        i = ctypes.c_int()
+        check(lib.sdrgpu_frontend_add_vfo(self._h, ctypes.byref(i), float(out_sr), float(bandwidth), float(offset)))
+        return i.value
+
+    def remove_vfo(self, vid):
+        check(lib.sdrgpu_frontend_remove_vfo(self._h, int(vid)))
+
+    def set_vfo_offset(self, vid, offset):
+        check(lib.sdrgpu_frontend_set_vfo_offset(self._h, int(vid), float(offset)))
+
+    def push(self, block, kind=-1):
+        a = np.ascontiguousarray(block)
+        count = a.shape[0] if kind < 0 else a.size // 2
+        nf = check(lib.sdrgpu_frontend_push(self._h, _fptr(a), int(count), int(kind)))
+        rows = np.empty((nf, self.fft_size), np.float32)
+        if nf:
+            check(lib.sdrgpu_frontend_read_spectra(self._h, _fptr(rows), nf))
+        return rows
+
+    def push_dev(self, ptr, count, kind=-1, stream=None):
+        return check(lib.sdrgpu_frontend_push_dev(self._h, _vp(ptr), int(count), int(kind), _vp(stream or 0)))
+
+    def vfo_output(self, vid):
+        n = ctypes.c_int()
+        check(lib.sdrgpu_frontend_vfo_dev(self._h, int(vid), None, ctypes.byref(n)))
+        out = np.empty(n.value, np.complex64)
+        if n.value:
+            check(lib.sdrgpu_frontend_read_vfo(self._h, int(vid), _fptr(out), n.value))
+        return out
+
+    def close(self):
+        if self._h:
+            lib.sdrgpu_frontend_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def low_pass(cutoff, trans, fs, odd=False):
     return _taps(lib.sdrgpu_taps_low_pass, float(cutoff), float(trans), float(fs), int(odd))
 

@@ -27,8 +27,8 @@ def assert_close_c(a, b, atol, what=""):
 def db_check(db_gpu, power_true, N, ref32_db=None, floor_db=60.0):
     """Spectrum parity (DESIGN.md 'Parity bar'), on bins within `floor_db` of the frame peak:
     1. the GPU's dB error vs the fp64 truth is in the accuracy class of a reference-class fp32
-       FFT (pocketfft single precision) on the same windowed input: rms <= 2x its rms and
-       max <= 3x its max (+2 ulp of the fp32 dB value);
+       FFT (pocketfft single precision) on the same windowed input: rms <= 2x its rms (+ the
+       rms of 1 ulp of the fp32 dB values) and max <= 3x its max (+2 ulp of the fp32 dB value);
     2. normwise: || |X_gpu| - |X_true| ||_2 <= 4 * eps32 * log2(N) * ||X_true||_2 (all bins).
     Without a reference-class FFT the bound is 2e-4 dB.
     """
@@ -40,7 +40,11 @@ def db_check(db_gpu, power_true, N, ref32_db=None, floor_db=60.0):
     if ref32_db is not None:
         rerr = np.abs(ref32_db.astype(np.float64) - db_true)[sel]
         rms_g, rms_r = np.sqrt(np.mean(err ** 2)), np.sqrt(np.mean(rerr ** 2))
-        assert rms_g <= 2.0 * rms_r + 1e-12, f"rms dB err {rms_g:.3e} > 2 x fp32-ref {rms_r:.3e}"
+        # + the rms of 1 ulp of the fp32 dB value: the reference writes 10*log10f(re^2+im^2) in
+        # fp32 (volk_32fc_s32f_power_spectrum_32f), i.e. the dB row itself carries ~1 ulp
+        # (log10f + the x10 rounding); the scipy row here is rounded once from fp64
+        ulp_rms = np.sqrt(np.mean(ulp ** 2))
+        assert rms_g <= 2.0 * rms_r + ulp_rms + 1e-12, f"rms dB err {rms_g:.3e} > 2 x fp32-ref {rms_r:.3e} + ulp {ulp_rms:.3e}"
         assert np.all(err <= 3.0 * rerr.max() + 2.0 * ulp), f"max dB err {err.max():.3e} > 3 x fp32-ref {rerr.max():.3e}"
     else:
         assert np.all(err <= np.maximum(2e-4, 2.0 * ulp)), f"max dB err {err.max():.3e}"

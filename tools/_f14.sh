@@ -1,0 +1,3 @@
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
+timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/f14_tests.log 2>&1; echo "rc=$?" >> gpurun_out/f14_tests.log; \
+TAG=f14 CFGS="c5 c2" bash tools/ab.sh r3
