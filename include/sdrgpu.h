@@ -148,6 +148,10 @@ int sdrgpu_demod_agc_set_attack_decay(sdrgpu_block* h, double attack, double dec
  * pilot band-pass (complex taps) -> PLL (loop/pll.h) -> L+R / L-R matrix -> audio low-pass;
  * stereo_t out. stereo = 0 gives the mono path (= sdrgpu_wfm_create). RDS output: not provided. */
 int sdrgpu_broadcast_fm_create(sdrgpu_block** h, int device, double deviation, double samplerate, int stereo, int lowPass);
+/* filter::Deemphasis<T> (filter/deephasis.h:57-93): dtype F32 (float) or C64 (stereo_t);
+ * serial recurrence, bit-identical to the reference arithmetic */
+int sdrgpu_deemphasis_create(sdrgpu_block** h, int device, int dtype, double tau, double samplerate);
+int sdrgpu_deemphasis_set(sdrgpu_block* h, double tau, double samplerate);   /* setTau / setSamplerate */
 /* M-channel critically sampled polyphase channelizer (BASELINE C4): channel k of output frame
  * m is FrequencyXlator(-k fs/M) -> DecimatingFIR<complex_t,float>(taps, M) (frequency_xlator.h:43,
  * decimating_fir.h:45) with an exact NCO; taps <= 16 M (bank layout polyphase_bank.h:32).
@@ -185,6 +189,21 @@ int sdrgpu_frontend_spectra_dev(sdrgpu_frontend* f, const float** rows, int* nro
 int sdrgpu_frontend_read_spectra(sdrgpu_frontend* f, float* out, int maxRows);
 int sdrgpu_frontend_vfo_dev(sdrgpu_frontend* f, int id, const void** out, int* n);
 int sdrgpu_frontend_read_vfo(sdrgpu_frontend* f, int id, void* out, int max);
+
+/* ---------------------------------------------- spectrum/IQ consumers ---- */
+/* waterfall zoom, fft_scaler(viewOffset, viewBandwidth, wholeBandwidth, fftSize, outSize).doZoom
+ * (gui/widgets/fft_scaler.h:27-64) on device dB rows: out[r][o] = max over the reference's bins */
+typedef struct sdrgpu_zoom sdrgpu_zoom;
+int sdrgpu_zoom_create(sdrgpu_zoom** z, int device, double viewOffset, double viewBandwidth, double wholeBandwidth,
+                       int fftSize, int outSize);
+int sdrgpu_zoom_execute_dev(sdrgpu_zoom* z, const float* rows, int nrows, float* out, void* stream);
+int sdrgpu_zoom_destroy(sdrgpu_zoom* z);
+/* SampleStreamCompressor::process (compression/sample_stream_compressor.h:26-60) of a device block:
+ * pcmType 0 I8, 1 I16, 2 F32; `scratch` = 4 device bytes (I8/I16); returns bytes written */
+int sdrgpu_compress_dev(int device, int pcmType, const float* in, int count, unsigned char* out, unsigned* scratch, void* stream);
+/* SampleStreamDecompressor::process (sample_stream_decompressor.h:13-33): hdr = host copy of the
+ * 8-byte header, payload = device bytes after it; returns complex samples written */
+int sdrgpu_decompress_dev(int device, const unsigned char* hdr, const unsigned char* payload, int nbytes, float* out, void* stream);
 
 /* ------------------------------------------------------------ ingest ---- */
 

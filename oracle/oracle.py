@@ -97,6 +97,10 @@ def _load():
         "orc_wfms_create": (vp, [d, d, i, i, i]),
         "orc_wfms_process": (i, [vp, vp, i, vp]),
         "orc_wfms_destroy": (None, [vp]),
+        "orc_deemp_create": (vp, [i, d, d]),
+        "orc_deemp_process": (i, [vp, vp, i, vp]),
+        "orc_deemp_destroy": (None, [vp]),
+        "orc_zoom": (i, [vp, i, d, d, d, i, vp]),
         "orc_chain_create": (vp, [d, i, d, i]),
         "orc_chain_process": (l, [vp, vp, l, vp, l, vp]),
         "orc_chain_destroy": (None, [vp]),
@@ -358,6 +362,41 @@ class BroadcastFMStereo(_Obj):
 
     def process(self, x):
         return super().process(x, lib.orc_wfms_process)
+
+
+class Deemphasis(_Obj):
+    """filter/deephasis.h (stereo=True: stereo_t pairs)."""
+    _destroy = lib.orc_deemp_destroy
+
+    def __init__(self, tau, samplerate, stereo=False):
+        dt = STEREO if stereo else np.float32
+        super().__init__(lib.orc_deemp_create(2 if stereo else 1, float(tau), float(samplerate)), dt, dt)
+
+    def process(self, x):
+        return super().process(x, lib.orc_deemp_process)
+
+
+def zoom(row, view_offset, view_bw, whole_bw, out_size):
+    """gui/widgets/fft_scaler.h doZoom of one spectrum row."""
+    row = np.ascontiguousarray(row, np.float32)
+    out = np.empty(out_size, np.float32)
+    lib.orc_zoom(_p(row), len(row), float(view_offset), float(view_bw), float(whole_bw), int(out_size), _p(out))
+    return out
+
+
+def compress(pcm_type, x):
+    """compression/sample_stream_compressor.h: bytes of one block."""
+    x = np.ascontiguousarray(x, np.complex64)
+    out = np.empty(8 + 8 * len(x), np.uint8)
+    n = lib.orc_compress(int(pcm_type), _p(x), len(x), _p(out))
+    return out[:n]
+
+
+def decompress(buf):
+    buf = np.ascontiguousarray(buf, np.uint8)
+    out = np.empty(max(len(buf) // 2, 1), np.complex64)
+    n = lib.orc_decompress(_p(buf), len(buf), _p(out))
+    return out[:n]
 
 
 class FM(_Obj):

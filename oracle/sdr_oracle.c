@@ -1026,3 +1026,58 @@ int orc_channelize(const float* in, long count, const float* h, int ntaps, int M
     free(cs);
     return (int)frames;
 }
+
+/* ------------------------------------------------------------ Deemphasis */
+/* filter/deephasis.h:14-93 (T = float or stereo_t: `ch` interleaved channels) */
+struct orc_deemp { float alpha; float last[2]; int ch; };
+orc_deemp* orc_deemp_create(int channels, double tau, double samplerate) {
+    orc_deemp* d = (orc_deemp*)calloc(1, sizeof(orc_deemp));
+    float dt = (float)(1.0f / samplerate);              /* float dt = 1.0f / _samplerate */
+    d->alpha = (float)((double)dt / (tau + (double)dt)); /* alpha = dt / (_tau + dt) */
+    d->ch = channels;
+    return d;
+}
+int orc_deemp_process(orc_deemp* d, const float* in, int count, float* out) {
+    const float beta = 1 - d->alpha;
+    for (int i = 0; i < count; i++)
+        for (int c = 0; c < d->ch; c++) {
+            float y = (d->alpha * in[i * d->ch + c]) + (beta * d->last[c]);
+            out[i * d->ch + c] = y;
+            d->last[c] = y;
+        }
+    return count;
+}
+void orc_deemp_destroy(orc_deemp* d) { free(d); }
+
+/* ------------------------------------------------------ fft_scaler::doZoom */
+/* gui/widgets/fft_scaler.h:27-64 */
+int orc_zoom(const float* data, int fftSize, double viewOffset, double viewBandwidth, double wholeBandwidth,
+             int outSize, float* out) {
+    const double offsetRatio = viewOffset / (wholeBandwidth / 2.0);
+    double width = (viewBandwidth / wholeBandwidth) * fftSize;
+    double offset = (((double)fftSize / 2.0) * (offsetRatio + 1)) - (width / 2);
+    if (offset < 0) offset = 0;
+    if (width > fftSize - offset) width = fftSize - offset;
+    const double factor = width / outSize;
+    double f0 = offset;
+    if (factor <= 1.0) {
+        for (int i = 0; i < outSize; i++) {
+            double f1 = f0 + factor;
+            int i0 = (int)roundf((float)f0);
+            *out++ = data[i0];
+            f0 = f1;
+        }
+    } else {
+        int i0 = (int)roundf((float)f0);
+        for (int i = 0; i < outSize; i++) {
+            double f1 = f0 + factor;
+            int i1 = (int)roundf((float)f1);
+            float maxVal = data[i0];
+            for (int j = i0 + 1; j < i1; j++) maxVal = (maxVal < data[j]) ? data[j] : maxVal;   /* std::max */
+            *out++ = maxVal;
+            f0 = f1;
+            i0 = i1;
+        }
+    }
+    return outSize;
+}

@@ -155,6 +155,14 @@ int orc_decompress(const uint8_t* in, int nbytes, float* out);
 int orc_channelize(const float* in, long count, const float* h, int ntaps, int M, const int* chans, int nchan,
                    double* out);
 
+typedef struct orc_deemp orc_deemp;          /* filter/deephasis.h, channels 1 (float) or 2 (stereo_t) */
+orc_deemp* orc_deemp_create(int channels, double tau, double samplerate);
+int  orc_deemp_process(orc_deemp* d, const float* in, int count, float* out);
+void orc_deemp_destroy(orc_deemp* d);
+/* gui/widgets/fft_scaler.h doZoom */
+int orc_zoom(const float* data, int fftSize, double viewOffset, double viewBandwidth, double wholeBandwidth,
+             int outSize, float* out);
+
 /* C5 per-stream chain used as the CPU baseline: 64k BH7 spectrum (back-to-back
  * frames) + RxVFO(plan_256 + 91-tap LPF) + BroadcastFM mono. Returns audio pairs. */
 typedef struct orc_chain orc_chain;

@@ -85,6 +85,13 @@ def _load():
         "sdrgpu_wfm_create": (i, [pp, i, d, d, i]),
         "sdrgpu_channelizer_create": (i, [pp, i, i, fp, i]),
         "sdrgpu_broadcast_fm_create": (i, [pp, i, d, d, i, i]),
+        "sdrgpu_deemphasis_create": (i, [pp, i, i, d, d]),
+        "sdrgpu_deemphasis_set": (i, [vp, d, d]),
+        "sdrgpu_zoom_create": (i, [pp, i, d, d, d, i, i]),
+        "sdrgpu_zoom_execute_dev": (i, [vp, vp, i, vp, vp]),
+        "sdrgpu_zoom_destroy": (i, [vp]),
+        "sdrgpu_compress_dev": (i, [i, i, vp, i, vp, vp, vp]),
+        "sdrgpu_decompress_dev": (i, [i, vp, vp, i, vp, vp]),
         "sdrgpu_frontend_create": (i, [pp, i, d, i, i, i, d, i]),
         "sdrgpu_frontend_destroy": (i, [vp]),
         "sdrgpu_frontend_configure": (i, [vp, d, i, i]),

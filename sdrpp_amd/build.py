@@ -26,6 +26,7 @@ SOURCES = [
     ("channelizer.hip", []),
     ("loops.hip", ["-ffp-contract=off"]),   # bit-exact serial recurrences
     ("frontend.hip", []),
+    ("consumers.hip", []),
 ]
 
 

@@ -1,0 +1,219 @@
+// Consumers on either side of the hot path:
+//   * the waterfall's max-decimating zoom, fft_scaler::doZoom (gui/widgets/fft_scaler.h:27-64),
+//     applied to device spectrum rows so only display-width rows leave the GPU;
+//   * the IQ wire codec, SampleStreamCompressor / Decompressor
+//     (dsp/compression/sample_stream_compressor.h:26-60, sample_stream_decompressor.h:13-33).
+// Both are bit-identical to the reference arithmetic: the zoom's bin ranges are the reference's
+// own sequential double accumulation, evaluated on the host once per geometry; the codec
+// reduces the SIGNED maximum (volk_32f_index_max_32u, first index on ties -- a quirk: not
+// the magnitude) exactly and converts with the VOLK generic rounding (x * s, clamp, rintf).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+#include "sdrgpu_internal.h"
+
+namespace sdrgpu {
+
+// ------------------------------------------------------------------ zoom
+// one output per thread: max over data[i0[o], i1[o]) (i1 = i0 + 1 when factor <= 1)
+__global__ void zoom_kernel(const float* __restrict__ rows, int fftSize, int nrows, const int2* __restrict__ range,
+                            int outSize, float* __restrict__ out) {
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.y;
+    if (o >= outSize || r >= nrows) return;
+    const float* d = rows + (size_t)r * fftSize;
+    const int2 rg = range[o];
+    float m = d[rg.x];
+    for (int j = rg.x + 1; j < rg.y; j++) m = fmaxf(m, d[j]);   // std::max(maxVal, data[j])
+    out[(size_t)r * outSize + o] = m;
+}
+
+// ---------------------------------------------------------------- codec
+__global__ void signed_max_kernel(const float* __restrict__ x, long long n, unsigned* __restrict__ bits) {
+    // max over floats as an order-preserving unsigned key (exact; NaN-free input)
+    float m = -INFINITY;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        m = fmaxf(m, x[i]);
+    for (int s = 32; s > 0; s >>= 1) m = fmaxf(m, __shfl_xor(m, s));
+    if ((threadIdx.x & 63) == 0) {
+        const unsigned u = __float_as_uint(m);
+        const unsigned key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        atomicMax(bits, key);
+    }
+}
+__device__ __forceinline__ float key_to_float(unsigned key) {
+    return __uint_as_float((key & 0x80000000u) ? (key & 0x7fffffffu) : ~key);
+}
+template <typename IT>
+__global__ void compress_kernel(const float* __restrict__ x, long long n, const unsigned* __restrict__ maxKey,
+                                float full, float lo, float hi, unsigned char* __restrict__ out) {
+    const float mv = key_to_float(*maxKey);
+    const float sc = full / mv;                                   // 128.0f / maxVal, 32768.0f / maxVal
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i == 0) {                                                  // header: {u16 0, u16 type, f32 scaler}
+        const unsigned short ct = 0, st = sizeof(IT) == 1 ? 0 : 1;
+        memcpy(out, &ct, 2);
+        memcpy(out + 2, &st, 2);
+        memcpy(out + 4, &mv, 4);
+    }
+    if (i >= n) return;
+    float r = x[i] * sc;                                           // volk_32f_s32f_convert_{8,16}i generic
+    if (r > hi) r = hi;
+    else if (r < lo) r = lo;
+    reinterpret_cast<IT*>(out + 8)[i] = (IT)rintf(r);
+}
+__global__ void f32_header_kernel(unsigned char* __restrict__ out) {
+    const unsigned short ct = 0, st = 2;
+    const float z = 0.0f;
+    memcpy(out, &ct, 2);
+    memcpy(out + 2, &st, 2);
+    memcpy(out + 4, &z, 4);
+}
+__global__ void decompress16_kernel(const short* __restrict__ in, long long n, float scaler, float* __restrict__ out) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    const float sc = 32768.0f / scaler;
+    if (i < n) out[i] = ((float)in[i]) / sc;                       // volk_16i_s32f_convert_32f generic
+}
+__global__ void decompress8_kernel(const signed char* __restrict__ in, long long n, float isc, float* __restrict__ out) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i < n) out[i] = ((float)in[i]) * isc;                      // volk_8i_s32f_convert_32f generic
+}
+
+struct ZoomPlan {
+    int device = 0, fftSize = 0, outSize = 0;
+    DevBuf range;
+};
+
+}  // namespace sdrgpu
+
+using namespace sdrgpu;
+
+struct sdrgpu_zoom {
+    ZoomPlan p;
+};
+
+// fft_scaler(viewOffset, viewBandwidth, wholeBandwidth, fftSize, outSize) + its doZoom index walk
+extern "C" int sdrgpu_zoom_create(sdrgpu_zoom** out, int device, double viewOffset, double viewBandwidth,
+                                  double wholeBandwidth, int fftSize, int outSize) {
+    if (!out || fftSize < 1 || outSize < 1 || !(wholeBandwidth > 0)) { set_error("zoom_create: bad argument"); return SDRGPU_EARG; }
+    SDRGPU_SET_DEVICE(device);
+    const double offsetRatio = viewOffset / (wholeBandwidth / 2.0);
+    double width = (viewBandwidth / wholeBandwidth) * fftSize;
+    double offset = (((double)fftSize / 2.0) * (offsetRatio + 1)) - (width / 2);
+    if (offset < 0) offset = 0;
+    if (width > fftSize - offset) width = fftSize - offset;
+    const double factor = width / outSize;
+    std::vector<int2> rg(outSize);
+    double f0 = offset;
+    if (factor <= 1.0) {
+        for (int i = 0; i < outSize; i++) {
+            const double f1 = f0 + factor;
+            const int i0 = (int)roundf((float)f0);
+            rg[i] = make_int2(i0, i0 + 1);
+            f0 = f1;
+        }
+    } else {
+        int i0 = (int)roundf((float)f0);
+        for (int i = 0; i < outSize; i++) {
+            const double f1 = f0 + factor;
+            const int i1 = (int)roundf((float)f1);
+            rg[i] = make_int2(i0, std::max(i1, i0 + 1));
+            f0 = f1;
+            i0 = i1;
+        }
+    }
+    for (auto& r : rg)
+        if (r.x < 0 || r.x >= fftSize || r.y > fftSize) {
+            set_error("zoom_create: view outside the spectrum (bins %d..%d of %d)", r.x, r.y, fftSize);
+            return SDRGPU_EARG;
+        }
+    auto* z = new sdrgpu_zoom();
+    z->p.device = device;
+    z->p.fftSize = fftSize;
+    z->p.outSize = outSize;
+    int rc = z->p.range.ensure(sizeof(int2) * outSize);
+    if (rc >= 0 && hipMemcpy(z->p.range.p, rg.data(), sizeof(int2) * outSize, hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("zoom_create: upload failed");
+        rc = SDRGPU_EHIP;
+    }
+    if (rc < 0) { delete z; return rc; }
+    *out = z;
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_zoom_execute_dev(sdrgpu_zoom* z, const float* rows, int nrows, float* out, void* stream) {
+    if (!z || nrows < 0 || (nrows > 0 && (!rows || !out))) { set_error("zoom_execute: bad argument"); return SDRGPU_EARG; }
+    if (nrows == 0) return 0;
+    SDRGPU_SET_DEVICE(z->p.device);
+    hipLaunchKernelGGL(zoom_kernel, dim3((z->p.outSize + 255) / 256, nrows), dim3(256), 0, (hipStream_t)stream, rows,
+                       z->p.fftSize, nrows, z->p.range.as<int2>(), z->p.outSize, out);
+    SDRGPU_HIP(hipGetLastError());
+    return nrows;
+}
+extern "C" int sdrgpu_zoom_destroy(sdrgpu_zoom* z) {
+    delete z;
+    return SDRGPU_OK;
+}
+
+// SampleStreamCompressor::process on a device block of `count` complex samples. pcmType:
+// 0 I8, 1 I16, 2 F32 (dsp/compression/pcm_type.h). Returns the byte count written to `out`.
+extern "C" int sdrgpu_compress_dev(int device, int pcmType, const float* in, int count, unsigned char* out,
+                                   unsigned* scratch, void* stream) {
+    if (pcmType < 0 || pcmType > 2 || count < 1 || !in || !out || (pcmType != 2 && !scratch)) { set_error("compress: bad argument"); return SDRGPU_EARG; }
+    SDRGPU_SET_DEVICE(device);
+    hipStream_t s = (hipStream_t)stream;
+    const long long n = 2LL * count;
+    if (pcmType == 2) {   // F32: no compression, scaler 0
+        hipLaunchKernelGGL(f32_header_kernel, dim3(1), dim3(1), 0, s, out);
+        SDRGPU_HIP(hipMemcpyAsync(out + 8, in, sizeof(float) * n, hipMemcpyDeviceToDevice, s));
+        return 8 + count * 8;
+    }
+    SDRGPU_HIP(hipMemsetAsync(scratch, 0, sizeof(unsigned), s));
+    const int g = (int)std::min<long long>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(signed_max_kernel, dim3(g), dim3(256), 0, s, in, n, scratch);
+    const dim3 gc((unsigned)((n + 255) / 256)), b(256);
+    if (pcmType == 0)
+        hipLaunchKernelGGL((compress_kernel<signed char>), gc, b, 0, s, in, n, scratch, 128.0f, -128.0f, 127.0f, out);
+    else
+        hipLaunchKernelGGL((compress_kernel<short>), gc, b, 0, s, in, n, scratch, 32768.0f, -32768.0f, 32767.0f, out);
+    SDRGPU_HIP(hipGetLastError());
+    return (int)(8 + n * (pcmType == 0 ? 1 : 2));
+}
+
+// SampleStreamDecompressor::process: `hdr` is the 8-byte header (host copy: it decides the
+// output count), `payload` the device bytes after it. Returns complex samples written.
+extern "C" int sdrgpu_decompress_dev(int device, const unsigned char* hdr, const unsigned char* payload, int nbytes,
+                                     float* out, void* stream) {
+    if (!hdr || nbytes < 8 || (nbytes > 8 && (!payload || !out))) { set_error("decompress: bad argument"); return SDRGPU_EARG; }
+    SDRGPU_SET_DEVICE(device);
+    hipStream_t s = (hipStream_t)stream;
+    unsigned short st;
+    float scaler;
+    std::memcpy(&st, hdr + 2, 2);
+    std::memcpy(&scaler, hdr + 4, 4);
+    if (st == 2) {
+        const int oc = (nbytes - 8) / 8;
+        if (oc > 0) SDRGPU_HIP(hipMemcpyAsync(out, payload, (size_t)oc * 8, hipMemcpyDeviceToDevice, s));
+        return oc;
+    }
+    if (st == 1) {
+        const int oc = (nbytes - 8) / 4;
+        const long long n = 2LL * oc;
+        if (n > 0) hipLaunchKernelGGL(decompress16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                                      (const short*)payload, n, scaler, out);
+        SDRGPU_HIP(hipGetLastError());
+        return oc;
+    }
+    if (st == 0) {
+        const int oc = (nbytes - 8) / 2;
+        const long long n = 2LL * oc;
+        const float sc = 128.0f / scaler;
+        const float isc = (float)(1.0 / sc);                      // volk generic: iScalar = 1.0 / scalar
+        if (n > 0) hipLaunchKernelGGL(decompress8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                                      (const signed char*)payload, n, isc, out);
+        SDRGPU_HIP(hipGetLastError());
+        return oc;
+    }
+    set_error("decompress: unknown sample type %u", (unsigned)st);
+    return SDRGPU_EARG;
+}

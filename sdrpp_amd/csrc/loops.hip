@@ -180,6 +180,35 @@ __global__ __launch_bounds__(LOOP_NT) void dcb_kernel(const DT* __restrict__ in,
     if (t == 0) *st = off;
 }
 
+// filter::Deemphasis<T> (filter/deephasis.h:57-77): out = alpha * in + (1 - alpha) * prev,
+// per channel (float: 1, stereo_t: 2); prev carried on the device
+template <int C>
+__global__ __launch_bounds__(LOOP_NT) void deemp_kernel(const float* __restrict__ in, float* __restrict__ out, int count,
+                                                        float alpha, float2* __restrict__ st) {
+    __shared__ float X[LOOP_CHUNK * C];
+    const int t = threadIdx.x;
+    float last[2] = {st->x, st->y};
+    const float beta = 1 - alpha;                               // (1 - alpha): int - float -> float
+    for (int i0 = 0; i0 < count; i0 += LOOP_CHUNK) {
+        const int n = min(LOOP_CHUNK, count - i0);
+        for (int i = t; i < n * C; i += LOOP_NT) X[i] = in[(size_t)i0 * C + i];
+        __syncthreads();
+        if (t == 0) {
+            for (int i = 0; i < n; i++)
+#pragma unroll
+                for (int c = 0; c < C; c++) {
+                    const float y = (alpha * X[i * C + c]) + (beta * last[c]);
+                    X[i * C + c] = y;
+                    last[c] = y;
+                }
+        }
+        __syncthreads();
+        for (int i = t; i < n * C; i += LOOP_NT) out[(size_t)i0 * C + i] = X[i];
+        __syncthreads();
+    }
+    if (t == 0) *st = make_float2(last[0], last[1]);
+}
+
 // volk_32fc_magnitude_32f (AM) / ComplexToReal (SSB) / MonoToStereo
 __global__ void magnitude_kernel(const float2* __restrict__ in, float* __restrict__ out, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -359,6 +388,40 @@ struct DcbBlock : Block {
             hipLaunchKernelGGL(dcb_kernel<float2>, dim3(1), dim3(LOOP_NT), 0, s, (const float2*)in, (float2*)out, count, rate, state.as<float2>());
         else
             hipLaunchKernelGGL(dcb_kernel<float>, dim3(1), dim3(LOOP_NT), 0, s, (const float*)in, (float*)out, count, rate, state.as<float2>());
+        SDRGPU_HIP(hipGetLastError());
+        return count;
+    }
+};
+
+struct DeempBlock : Block {
+    float alpha = 1.0f;
+    DevBuf state;
+    int setup(int dev, int dtype, double tau, double samplerate) {
+        device = dev;
+        in_dtype = out_dtype = dtype;                 // F32 (float) or C64 (stereo_t)
+        set_alpha(tau, samplerate);
+        SDRGPU_CHECK(init_stream());
+        SDRGPU_CHECK(state.ensure(sizeof(float2)));
+        return reset();
+    }
+    void set_alpha(double tau, double samplerate) {   // updateAlpha (deephasis.h:90-93)
+        const float dt = (float)(1.0f / samplerate);
+        alpha = (float)((double)dt / (tau + (double)dt));
+    }
+    int out_count(int count) override { return count; }
+    int reset() override {
+        SDRGPU_SET_DEVICE(device);
+        SDRGPU_HIP(hipMemset(state.p, 0, sizeof(float2)));
+        return SDRGPU_OK;
+    }
+    int run(const void* in, int count, void* out, hipStream_t s) override {
+        if (count < 0) { set_error("deemphasis: negative count"); return SDRGPU_EARG; }
+        if (count == 0) return 0;     // (the reference reads out[-1] for count == 0)
+        SDRGPU_SET_DEVICE(device);
+        if (in_dtype == SDRGPU_C64)
+            hipLaunchKernelGGL(deemp_kernel<2>, dim3(1), dim3(LOOP_NT), 0, s, (const float*)in, (float*)out, count, alpha, state.as<float2>());
+        else
+            hipLaunchKernelGGL(deemp_kernel<1>, dim3(1), dim3(LOOP_NT), 0, s, (const float*)in, (float*)out, count, alpha, state.as<float2>());
         SDRGPU_HIP(hipGetLastError());
         return count;
     }
@@ -677,4 +740,17 @@ extern "C" int sdrgpu_broadcast_fm_create(sdrgpu_block** h, int device, double d
     if (!h || !(samplerate > 0)) { set_error("broadcast_fm_create: bad argument"); return SDRGPU_EARG; }
     auto* w = new BroadcastFmBlock();
     return wrap_block(h, w, w->setup(device, deviation, samplerate, stereo != 0, lowPass != 0));
+}
+
+// filter::Deemphasis<T> (deephasis.h): dtype F32 (float) or C64 (stereo_t)
+extern "C" int sdrgpu_deemphasis_create(sdrgpu_block** h, int device, int dtype, double tau, double samplerate) {
+    if (!h || (dtype != SDRGPU_F32 && dtype != SDRGPU_C64) || !(samplerate > 0)) { set_error("deemphasis_create: bad argument"); return SDRGPU_EARG; }
+    auto* d = new DeempBlock();
+    return wrap_block(h, d, d->setup(device, dtype, tau, samplerate));
+}
+extern "C" int sdrgpu_deemphasis_set(sdrgpu_block* h, double tau, double samplerate) {   // setTau / setSamplerate
+    auto* d = h ? dynamic_cast<DeempBlock*>(h->impl) : nullptr;
+    if (!d || !(samplerate > 0)) { set_error("not a deemphasis block"); return SDRGPU_EARG; }
+    d->set_alpha(tau, samplerate);
+    return SDRGPU_OK;
 }

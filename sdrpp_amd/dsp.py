@@ -383,6 +383,33 @@ class IQFrontEnd:
             pass
 
 
+class Deemphasis(Block):
+    """dsp::filter::Deemphasis<T> (filter/deephasis.h); stereo=True for stereo_t."""
+
+    def __init__(self, tau, samplerate, stereo=False, device=0):
+        h = _make(lib.sdrgpu_deemphasis_create, device, C64 if stereo else F32, float(tau), float(samplerate))
+        super().__init__(h, STEREO if stereo else np.float32, STEREO if stereo else np.float32)
+
+
+class Zoom:
+    """fft_scaler::doZoom on device dB rows (gui/widgets/fft_scaler.h)."""
+
+    def __init__(self, view_offset, view_bw, whole_bw, fft_size, out_size, device=0):
+        self._h = _make(lib.sdrgpu_zoom_create, device, float(view_offset), float(view_bw), float(whole_bw), int(fft_size),
+                        int(out_size))
+        self.out_size = int(out_size)
+
+    def execute_dev(self, rows_ptr, nrows, out_ptr, stream=None):
+        return check(lib.sdrgpu_zoom_execute_dev(self._h, _vp(rows_ptr), int(nrows), _vp(out_ptr), _vp(stream or 0)))
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib.sdrgpu_zoom_destroy(self._h)
+        except Exception:
+            pass
+
+
 def low_pass(cutoff, trans, fs, odd=False):
     return _taps(lib.sdrgpu_taps_low_pass, float(cutoff), float(trans), float(fs), int(odd))
 

@@ -1,0 +1,2 @@
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
+timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/f15_tests.log 2>&1; echo "rc=$?" >> gpurun_out/f15_tests.log
