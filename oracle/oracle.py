@@ -101,6 +101,9 @@ def _load():
         "orc_deemp_process": (i, [vp, vp, i, vp]),
         "orc_deemp_destroy": (None, [vp]),
         "orc_zoom": (i, [vp, i, d, d, d, i, vp]),
+        "orc_ddcfm_create": (vp, [d, vp, i, i, d, i]),
+        "orc_ddcfm_process": (i, [vp, vp, i, vp]),
+        "orc_ddcfm_destroy": (None, [vp]),
         "orc_chain_create": (vp, [d, i, d, i]),
         "orc_chain_process": (l, [vp, vp, l, vp, l, vp]),
         "orc_chain_destroy": (None, [vp]),
@@ -362,6 +365,20 @@ class BroadcastFMStereo(_Obj):
 
     def process(self, x):
         return super().process(x, lib.orc_wfms_process)
+
+
+class DDCFM(_Obj):
+    """C3: FrequencyXlator -> DecimatingFIR<complex_t,float> -> Quadrature (precise=False: the
+    VOLK-style fp32 CPU path used as the CPU baseline)."""
+    _destroy = lib.orc_ddcfm_destroy
+
+    def __init__(self, offset_rad, taps, decim, deviation_rad, precise=False):
+        self._t = np.ascontiguousarray(taps, np.float32)
+        super().__init__(lib.orc_ddcfm_create(float(offset_rad), _p(self._t), len(self._t), int(decim), float(deviation_rad),
+                                              int(precise)), np.complex64, np.float32, 1.0 / decim)
+
+    def process(self, x):
+        return super().process(x, lib.orc_ddcfm_process)
 
 
 class Deemphasis(_Obj):

@@ -1081,3 +1081,25 @@ int orc_zoom(const float* data, int fftSize, double viewOffset, double viewBandw
     }
     return outSize;
 }
+
+/* ----------------------------------------------------- C3 chain (CPU baseline) */
+/* FrequencyXlator -> DecimatingFIR<complex_t, float> -> Quadrature, one block at a time
+ * (the three reference blocks back to back; precise = 0: VOLK-style fp32 rotator and dots) */
+struct orc_ddcfm { orc_xlator* x; orc_fir* f; orc_quad* q; float *a, *b; int cap; };
+orc_ddcfm* orc_ddcfm_create(double offsetRad, const float* taps, int ntaps, int decim, double deviationRad, int precise) {
+    orc_ddcfm* d = (orc_ddcfm*)calloc(1, sizeof(orc_ddcfm));
+    d->x = precise ? orc_xlator_create(offsetRad) : orc_xlator_create_fast(offsetRad);
+    d->f = orc_fir_create(ORC_C64, ORC_F32, taps, ntaps, decim, precise);
+    d->q = orc_quad_create(deviationRad);
+    return d;
+}
+int orc_ddcfm_process(orc_ddcfm* d, const float* in, int count, float* out) {
+    if (d->cap < count) { free(d->a); free(d->b); d->a = (float*)malloc(sizeof(float) * 2 * count); d->b = (float*)malloc(sizeof(float) * 2 * count); d->cap = count; }
+    orc_xlator_process(d->x, in, count, d->a);
+    int m = orc_fir_process(d->f, d->a, count, d->b);
+    return orc_quad_process(d->q, d->b, m, out);
+}
+void orc_ddcfm_destroy(orc_ddcfm* d) {
+    if (!d) return;
+    orc_xlator_destroy(d->x); orc_fir_destroy(d->f); orc_quad_destroy(d->q); free(d->a); free(d->b); free(d);
+}

@@ -163,6 +163,11 @@ void orc_deemp_destroy(orc_deemp* d);
 int orc_zoom(const float* data, int fftSize, double viewOffset, double viewBandwidth, double wholeBandwidth,
              int outSize, float* out);
 
+typedef struct orc_ddcfm orc_ddcfm;          /* C3: xlator -> DecimatingFIR -> Quadrature */
+orc_ddcfm* orc_ddcfm_create(double offsetRad, const float* taps, int ntaps, int decim, double deviationRad, int precise);
+int  orc_ddcfm_process(orc_ddcfm* d, const float* in, int count, float* out);
+void orc_ddcfm_destroy(orc_ddcfm* d);
+
 /* C5 per-stream chain used as the CPU baseline: 64k BH7 spectrum (back-to-back
  * frames) + RxVFO(plan_256 + 91-tap LPF) + BroadcastFM mono. Returns audio pairs. */
 typedef struct orc_chain orc_chain;
