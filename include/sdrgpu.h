@@ -205,6 +205,10 @@ int sdrgpu_compress_dev(int device, int pcmType, const float* in, int count, uns
  * 8-byte header, payload = device bytes after it; returns complex samples written */
 int sdrgpu_decompress_dev(int device, const unsigned char* hdr, const unsigned char* payload, int nbytes, float* out, void* stream);
 
+/* recorder WAV encoders (utils/wav.cpp:296-336) of n device floats: kind 0 u8, 1 i16, 2 i24
+ * (packed LE), 3 i32, 4 f32; returns bytes written */
+int sdrgpu_wav_encode_dev(int device, int kind, const float* in, long long n, unsigned char* out, void* stream);
+
 /* ------------------------------------------------------------ ingest ---- */
 
 /* file_source / rtl_sdr / hackrf sample converters (elementwise, n scalars):

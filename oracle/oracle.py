@@ -104,6 +104,7 @@ def _load():
         "orc_ddcfm_create": (vp, [d, vp, i, i, d, i]),
         "orc_ddcfm_process": (i, [vp, vp, i, vp]),
         "orc_ddcfm_destroy": (None, [vp]),
+        "orc_wav_encode": (i, [i, vp, i, vp]),
         "orc_chain_create": (vp, [d, i, d, i]),
         "orc_chain_process": (l, [vp, vp, l, vp, l, vp]),
         "orc_chain_destroy": (None, [vp]),
@@ -406,6 +407,14 @@ def compress(pcm_type, x):
     x = np.ascontiguousarray(x, np.complex64)
     out = np.empty(8 + 8 * len(x), np.uint8)
     n = lib.orc_compress(int(pcm_type), _p(x), len(x), _p(out))
+    return out[:n]
+
+
+def wav_encode(kind, x):
+    """utils/wav.cpp:296-336 recorder encoders: kind 0 u8, 1 i16, 2 i24, 3 i32, 4 f32 -> bytes."""
+    x = np.ascontiguousarray(x, np.float32).reshape(-1)
+    out = np.empty(4 * len(x) + 4, np.uint8)
+    n = lib.orc_wav_encode(int(kind), _p(x), len(x), _p(out))
     return out[:n]
 
 

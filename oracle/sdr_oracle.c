@@ -1103,3 +1103,25 @@ void orc_ddcfm_destroy(orc_ddcfm* d) {
     if (!d) return;
     orc_xlator_destroy(d->x); orc_fir_destroy(d->f); orc_quad_destroy(d->q); free(d->a); free(d->b); free(d);
 }
+
+/* ------------------------------------------------------ recorder encoders */
+/* utils/wav.cpp:296-336 (WAV writer): kind 0 u8, 1 i16, 2 i24 (packed LE), 3 i32, 4 f32.
+ * n = sample values; returns bytes written. */
+static float orc_clampf(float v) { return (v < -1.0f) ? -1.0f : (1.0f < v) ? 1.0f : v; }   /* std::clamp */
+int orc_wav_encode(int kind, const float* in, int n, uint8_t* out) {
+    for (int i = 0; i < n; i++) {
+        const float c = orc_clampf(in[i]);
+        switch (kind) {
+        case 0: out[i] = (uint8_t)lroundf(c * (128.0f - 0.5f) - 0.5f + 128); break;
+        case 1: { int16_t v = (int16_t)lroundf(c * (32768.0f - 0.5f) - 0.5f); memcpy(out + 2 * i, &v, 2); } break;
+        case 2: {
+            int32_t v = (int32_t)lroundf(c * (8388608.0f - 0.5f) - 0.5f);
+            out[3 * i] = (uint8_t)v; out[3 * i + 1] = (uint8_t)(v >> 8); out[3 * i + 2] = (uint8_t)(v >> 16);
+        } break;
+        case 3: { int32_t v = (int32_t)lroundf((float)((double)c * (2147483648.0 - 0.5) - 0.5)); memcpy(out + 4 * i, &v, 4); } break;
+        default: memcpy(out + 4 * i, &in[i], 4); break;
+        }
+    }
+    static const int sz[] = {1, 2, 3, 4, 4};
+    return n * sz[kind < 0 || kind > 4 ? 4 : kind];
+}

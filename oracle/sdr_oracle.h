@@ -168,6 +168,9 @@ orc_ddcfm* orc_ddcfm_create(double offsetRad, const float* taps, int ntaps, int 
 int  orc_ddcfm_process(orc_ddcfm* d, const float* in, int count, float* out);
 void orc_ddcfm_destroy(orc_ddcfm* d);
 
+/* recorder WAV encoders (utils/wav.cpp:296-336): kind 0 u8, 1 i16, 2 i24, 3 i32, 4 f32 */
+int orc_wav_encode(int kind, const float* in, int n, uint8_t* out);
+
 /* C5 per-stream chain used as the CPU baseline: 64k BH7 spectrum (back-to-back
  * frames) + RxVFO(plan_256 + 91-tap LPF) + BroadcastFM mono. Returns audio pairs. */
 typedef struct orc_chain orc_chain;

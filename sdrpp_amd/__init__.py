@@ -92,6 +92,7 @@ def _load():
         "sdrgpu_zoom_destroy": (i, [vp]),
         "sdrgpu_compress_dev": (i, [i, i, vp, i, vp, vp, vp]),
         "sdrgpu_decompress_dev": (i, [i, vp, vp, i, vp, vp]),
+        "sdrgpu_wav_encode_dev": (i, [i, i, vp, ll, vp, vp]),
         "sdrgpu_frontend_create": (i, [pp, i, d, i, i, i, d, i]),
         "sdrgpu_frontend_destroy": (i, [vp]),
         "sdrgpu_frontend_configure": (i, [vp, d, i, i]),

@@ -26,7 +26,7 @@ SOURCES = [
     ("channelizer.hip", []),
     ("loops.hip", ["-ffp-contract=off"]),   # bit-exact serial recurrences
     ("frontend.hip", []),
-    ("consumers.hip", []),
+    ("consumers.hip", ["-ffp-contract=off"]),   # bit-exact encoders
 ]
 
 

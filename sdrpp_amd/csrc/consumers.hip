@@ -3,7 +3,8 @@
 //     applied to device spectrum rows so only display-width rows leave the GPU;
 //   * the IQ wire codec, SampleStreamCompressor / Decompressor
 //     (dsp/compression/sample_stream_compressor.h:26-60, sample_stream_decompressor.h:13-33).
-// Both are bit-identical to the reference arithmetic: the zoom's bin ranges are the reference's
+//   * the recorder's WAV sample encoders (utils/wav.cpp:296-336).
+// All are bit-identical to the reference arithmetic: the zoom's bin ranges are the reference's
 // own sequential double accumulation, evaluated on the host once per geometry; the codec
 // reduces the SIGNED maximum (volk_32f_index_max_32u, first index on ties -- a quirk: not
 // the magnitude) exactly and converts with the VOLK generic rounding (x * s, clamp, rintf).
@@ -78,6 +79,28 @@ __global__ void decompress16_kernel(const short* __restrict__ in, long long n, f
 __global__ void decompress8_kernel(const signed char* __restrict__ in, long long n, float isc, float* __restrict__ out) {
     const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i < n) out[i] = ((float)in[i]) * isc;                      // volk_8i_s32f_convert_32f generic
+}
+
+// ------------------------------------------------------- recorder encoders
+// utils/wav.cpp:296-336: clamp to [-1, 1], scale, offset, lroundf (half away from zero); this
+// file is compiled with -ffp-contract=off so the scale and offset round separately
+__global__ void wav_encode_kernel(int kind, const float* __restrict__ in, long long n, unsigned char* __restrict__ out) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float v = in[i];
+    const float c = (v < -1.0f) ? -1.0f : (1.0f < v) ? 1.0f : v;   // std::clamp
+    switch (kind) {
+    case 0: out[i] = (unsigned char)lroundf(c * (128.0f - 0.5f) - 0.5f + 128); break;
+    case 1: reinterpret_cast<short*>(out)[i] = (short)lroundf(c * (32768.0f - 0.5f) - 0.5f); break;
+    case 2: {
+        const int q = (int)lroundf(c * (8388608.0f - 0.5f) - 0.5f);
+        out[3 * i] = (unsigned char)q;
+        out[3 * i + 1] = (unsigned char)(q >> 8);
+        out[3 * i + 2] = (unsigned char)(q >> 16);
+    } break;
+    case 3: reinterpret_cast<int*>(out)[i] = (int)lroundf((float)((double)c * (2147483648.0 - 0.5) - 0.5)); break;
+    default: reinterpret_cast<float*>(out)[i] = v; break;
+    }
 }
 
 struct ZoomPlan {
@@ -216,4 +239,16 @@ extern "C" int sdrgpu_decompress_dev(int device, const unsigned char* hdr, const
     }
     set_error("decompress: unknown sample type %u", (unsigned)st);
     return SDRGPU_EARG;
+}
+
+// recorder WAV encoders (utils/wav.cpp:296-336) of a device buffer of n sample values:
+// kind 0 u8, 1 i16, 2 i24 (packed little-endian), 3 i32, 4 f32; returns bytes written
+extern "C" int sdrgpu_wav_encode_dev(int device, int kind, const float* in, long long n, unsigned char* out, void* stream) {
+    static const int sz[] = {1, 2, 3, 4, 4};
+    if (kind < 0 || kind > 4 || n < 0 || (n > 0 && (!in || !out))) { set_error("wav_encode: bad argument"); return SDRGPU_EARG; }
+    SDRGPU_SET_DEVICE(device);
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(wav_encode_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, kind, in, n, out);
+    SDRGPU_HIP(hipGetLastError());
+    return (int)std::min<long long>(n * sz[kind], 0x7fffffff);
 }

@@ -77,3 +77,18 @@ def test_codec_bit_exact(pcm, rng):
     yo = oracle.decompress(ref)
     assert m == len(yo) == len(x)
     assert np.array_equal(_bits(y.view(np.float32)), _bits(yo.view(np.float32)))
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
+def test_wav_encoders_bit_exact(kind, rng):
+    """Recorder WAV encoders (utils/wav.cpp:296-336) incl. out-of-range and exact-code inputs."""
+    x = np.concatenate([rng.uniform(-1.2, 1.2, 200000), [-1.0, 1.0, 0.0, -0.0, 0.5, -0.5, 1.5, -3.0],
+                        (np.arange(-128, 128) + 0.5) / 127.5 - 0.0]).astype(np.float32)
+    ref = oracle.wav_encode(kind, x)
+    d_x = torch.from_numpy(x).cuda()
+    d_o = torch.zeros(len(ref) + 16, dtype=torch.uint8, device="cuda")
+    n = sdrpp_amd.check(sdrpp_amd.lib.sdrgpu_wav_encode_dev(0, kind, ctypes.c_void_p(d_x.data_ptr()), len(x),
+                                                            ctypes.c_void_p(d_o.data_ptr()), None))
+    torch.cuda.synchronize()
+    assert n == len(ref)
+    assert np.array_equal(d_o.cpu().numpy()[:n], ref)

@@ -127,6 +127,14 @@ def test_u8_i16_roundtrip_recorder_encoder():
     f = oracle.convert(1, codes)
     enc = _lroundf(np.clip(f, -1, 1) * np.float32(32767.5) - np.float32(0.5))
     np.testing.assert_array_equal(enc, codes.astype(np.int64))
+    # the oracle's C encoder (orc_wav_encode) agrees with this restatement and round-trips i24
+    np.testing.assert_array_equal(oracle.wav_encode(1, f).view(np.int16), codes)
+    c24 = np.arange(-(1 << 23), 1 << 23, 997, dtype=np.int64)
+    b24 = np.stack([c24 & 0xff, (c24 >> 8) & 0xff, (c24 >> 16) & 0xff], axis=1).astype(np.uint8).ravel()
+    np.testing.assert_array_equal(oracle.wav_encode(2, oracle.convert(2, b24)), b24)
+    x = np.array([2.0, -2.0, 1.0, -1.0, 0.25], np.float32)
+    np.testing.assert_array_equal(oracle.wav_encode(0, x), [255, 0, 255, 0, 159])   # 0.25*127.5-0.5+128 = 159.375
+    np.testing.assert_array_equal(oracle.wav_encode(4, x).view(np.float32), x)
 
 
 def test_i24_sign_extension():
