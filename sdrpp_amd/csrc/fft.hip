@@ -31,13 +31,12 @@ __device__ __forceinline__ float db_of(float2 X) {
 // is transformed and stored, so HBM latency overlaps the LDS exchange, the math and the
 // stores of the previous tile (one register fragment in flight per thread).
 template <int L, class Frag, class Issue, class Finish, class Store>
-__device__ __forceinline__ void tile_loop(float2* lds, const float2* __restrict__ tw, int ntiles, int sF, int tF, int sL,
-                                          int tL, Issue&& issue, Finish&& finish, Store&& store) {
+__device__ __forceinline__ void tile_loop(float2* lds, const float2* __restrict__ tw, int tile, int ntiles, int sF, int tF,
+                                          int sL, int tL, Issue&& issue, Finish&& finish, Store&& store) {
     // One tile per workgroup (grid = tiles). A persistent variant with a ping-pong register
     // prefetch of the next tile was measured at the same 64k throughput with a quarter of the
     // occupancy (and spills at N1 = 1024), so the simple form is kept.
     constexpr int LS = Lds<L>::LS;
-    const int tile = blockIdx.x;
     if (tile >= ntiles) return;
     Frag fr;
     issue(fr, tile);
@@ -67,7 +66,7 @@ __global__ __launch_bounds__(S * L / 16) void fft_single_kernel(
     const int s = tid / T, t = tid % T;           // frame-contiguous mapping for load and store
     const int ntiles = (frames + S - 1) / S;
     tile_loop<L, FragW>(
-        lds, tw, ntiles, s, t, s, t,
+        lds, tw, blockIdx.x, ntiles, s, t, s, t,
         [&](FragW& fr, int tile) {
             const int f = min(tile * S + s, frames - 1);
             const float2* x = in + (long long)f * frameStride;
@@ -98,18 +97,104 @@ __global__ __launch_bounds__(S * L / 16) void fft_single_kernel(
 // two table values (W_N^(S b k1) x W_N^(c k1)) saved a little table space but added an
 // fp32 rounding: the 64k spectrum's rms dB error on a tonal signal was 2.1x pocketfft's.
 template <int L, int S>
-__global__ __launch_bounds__(S * L / 16) void fft_passA_kernel(
-    const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
-    int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull,
-    float2* __restrict__ scratch) {
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+__device__ __forceinline__ void passA_tile(
+    float2* lds, int tile, const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win,
+    int nz, int N2, int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull,
+    float2* __restrict__ scratch, int dbg) {
     const int tid = threadIdx.x;
     const int c = tid % S, t = tid / S;
     constexpr int T = L / 16;
     const int nb = N2 / S;                        // column blocks per frame
     const int ntiles = nb * frames;
+    if (dbg & 16) {   // timing ablation only: the same loads and stores, no transform
+        if (tile >= ntiles) return;
+        const int b = tile % nb;
+        const long long f = tile / nb;
+        const float2* x = in + f * frameStride;
+        float2 v[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const long long n = (long long)(t + r * T) * N2 + b * S + c;
+            const float w = (dbg & 1) ? 1.0f : win[n];
+            v[r] = make_float2(x[n].x * w, x[n].y * w);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const long long o = (long long)(t + r * T) * N2 + b * S + c;
+            const float2 t0 = (dbg & 2) ? make_float2(1.f, 0.f) : tfull[o];
+            scratch[(f << logN) + o] = cmul(v[r], t0);
+        }
+        return;
+    }
+    if constexpr (L == 256) {
+        // 256-point columns: both stages are radix 16, so the whole column is one LDS exchange.
+        // Every global read is issued up front (input, window, the exact four-step twiddles of
+        // this thread's 16 outputs and the WG's copy of the stage twiddles, which live in LDS),
+        // so the WG waits for memory once instead of three times.
+        if (tile >= ntiles) return;
+        constexpr int LS = Lds<L>::LS;
+        float2* twl = lds + S * LS;
+        const int b = tile % nb;
+        const long long f = tile / nb;
+        const int col = b * S + c;
+        // Buffer loads/stores: one wave-uniform resource per array and ONE per-lane byte offset
+        // (o0) shared by every access of the thread; the row step r * 16 * N2 rides in the
+        // scalar soffset. (Plain global accesses kept a 64-bit address pair per row live and
+        // spilled at the 4-waves/SIMD register budget.)
+        const float2* x = in + f * frameStride;
+        const unsigned o0 = (unsigned)(t * N2 + col);
+        const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)win, (short)0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc((void*)tfull, (short)0, 0x7fffffff, 0x00020000);
+        const int rowB = T * N2 * 8;   // bytes between the rows t + 16 r and t + 16 (r + 1)
+        float2 xv[16], tt[16];
+        float wv[16];
+        if (nz >= L * N2) {   // no zero padding (wave-uniform)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                xv[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, o0 * 8, r * rowB, 0));
+                wv[r] = (dbg & 1) ? 1.0f : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, o0 * 4, r * rowB / 2, 0));
+            }
+        } else {              // zero-padded tail: clamped (in-bounds) loads, then select
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const unsigned n = o0 + (unsigned)(r * T * N2);
+                const bool live = (int)n < nz;
+                const unsigned nc = live ? n : 0u;
+                const float2 xe = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, nc * 8, 0, 0));
+                const float we = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, nc * 4, 0, 0));
+                xv[r] = live ? xe : make_float2(0.0f, 0.0f);
+                wv[r] = live ? ((dbg & 1) ? 1.0f : we) : 0.0f;
+            }
+        }
+        for (int i = tid; i < L; i += S * T) twl[i] = tw[i];
+#pragma unroll
+        for (int r = 0; r < 16; r++)   // exact W_N^(n2 k1), k1 = t + 16 r: same offsets as the input rows
+            tt[r] = (dbg & 2) ? make_float2(1.f, 0.f)
+                              : __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rt, o0 * 8, r * rowB, 0));
+        float2 v[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) v[r] = make_float2(xv[r].x * wv[r], xv[r].y * wv[r]);
+        float2* seq = lds + c * LS;
+        stage_first<L>(seq, v, t);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 16; r++) v[r] = seq[pad16(t + 16 * r)];
+#pragma unroll
+        for (int r = 1; r < 16; r++) v[r] = cmul(v[r], twl[r * t]);
+        dft16(v);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(scratch + (f << logN)), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const float2 y = cmul(v[r], tt[r]);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, y), rs,
+                                                  o0 * 8, r * rowB, 0);
+        }
+        return;
+    }
     tile_loop<L, FragW>(
-        lds, tw, ntiles, c, t, c, t,
+        lds, tw, tile, ntiles, c, t, c, t,
         [&](FragW& fr, int tile) {
             const int b = tile % nb;
             const long long f = tile / nb;
@@ -121,7 +206,7 @@ __global__ __launch_bounds__(S * L / 16) void fft_passA_kernel(
                 const bool live = n < nz;
                 const long long nc = live ? n : 0;   // frame[0]: always in bounds
                 fr.x[r] = x[nc];
-                fr.w[r] = live ? win[nc] : 0.0f;
+                fr.w[r] = live ? ((dbg & 1) ? 1.0f : win[nc]) : 0.0f;
             }
         },
         [&](const FragW& fr, float2 (&v)[16]) {
@@ -131,9 +216,18 @@ __global__ __launch_bounds__(S * L / 16) void fft_passA_kernel(
         [&](int tile, int k1, float2 y) {
             const int b = tile % nb;
             const long long f = tile / nb;
-            const float2 t0 = tfull[(long long)k1 * N2 + b * S + c];   // exact W_N^(n2 k1)
+            const float2 t0 = (dbg & 2) ? make_float2(1.f, 0.f) : tfull[(long long)k1 * N2 + b * S + c];   // exact W_N^(n2 k1)
             scratch[(f << logN) + (long long)k1 * N2 + b * S + c] = cmul(y, t0);
         });
+}
+
+template <int L, int S>
+__global__ __launch_bounds__(S * L / 16) __attribute__((amdgpu_waves_per_eu(4))) void fft_passA_kernel(
+    const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
+    int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull,
+    float2* __restrict__ scratch, int dbg) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    passA_tile<L, S>(lds, blockIdx.x, in, frameStride, frames, win, nz, N2, logN, tw, tfull, scratch, dbg);
 }
 
 // ---- pass A, paired columns: S columns x N1 rows per tile, two adjacent columns per lane --
@@ -217,18 +311,18 @@ __device__ __forceinline__ void stages_rest_v(float2* seq0, const float2* twl, i
 }
 
 template <int L, int S>
-__global__ __launch_bounds__(S / 2 * L / 16) void fft_passA2_kernel(
-    const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
-    int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull, float2* __restrict__ scratch, int dbg) {
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+__device__ __forceinline__ void passA2_tile(
+    float2* lds, int tile, const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win,
+    int nz, int N2, int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull, float2* __restrict__ scratch,
+    int dbg) {
     constexpr int P = S / 2, T = L / 16, NT = P * T, LS = Lds<L>::LS;
     float2* twl = lds + S * LS;
     const int tid = threadIdx.x;
     const int cp = tid % P, t = tid / P;
     for (int i = tid; i < L; i += NT) twl[i] = tw[i];
     const int nb = N2 / S;
-    const int b = blockIdx.x % nb;
-    const long long f = blockIdx.x / nb;
+    const int b = tile % nb;
+    const long long f = tile / nb;
     const int col = b * S + 2 * cp;
     const float2* x = in + f * frameStride;
     float4 q[16];
@@ -273,14 +367,21 @@ __global__ __launch_bounds__(S / 2 * L / 16) void fft_passA2_kernel(
     });
 }
 
+template <int L, int S>
+__global__ __launch_bounds__(S / 2 * L / 16) void fft_passA2_kernel(
+    const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
+    int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull, float2* __restrict__ scratch, int dbg) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    passA2_tile<L, S>(lds, blockIdx.x, in, frameStride, frames, win, nz, N2, logN, tw, tfull, scratch, dbg);
+}
+
 // ---- pass B: S rows of length N2 per tile, dB out, transposed store -----------------
 // Stage 1 maps threads row-contiguous (coalesced row reads); the last stage maps the row
 // index fastest so the transposed dB store writes S consecutive floats per k2.
 template <int L, int S>
-__global__ __launch_bounds__(S * L / 16) void fft_passB_kernel(
-    const float2* __restrict__ scratch, int frames, int N1, int logN, const float2* __restrict__ tw,
+__device__ __forceinline__ void passB_tile(
+    float2* lds, int tile, const float2* __restrict__ scratch, int frames, int N1, int logN, const float2* __restrict__ tw,
     float* __restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
     constexpr int T = L / 16;
     const int tid = threadIdx.x;
     const int sF = tid / T, tF = tid % T;
@@ -288,7 +389,7 @@ __global__ __launch_bounds__(S * L / 16) void fft_passB_kernel(
     const int nb = N1 / S;
     const int ntiles = nb * frames;
     tile_loop<L, FragC>(
-        lds, tw, ntiles, sF, tF, sL, tL,
+        lds, tw, tile, ntiles, sF, tF, sL, tL,
         [&](FragC& fr, int tile) {
             const int b = tile % nb;
             const long long f = tile / nb;
@@ -305,6 +406,35 @@ __global__ __launch_bounds__(S * L / 16) void fft_passB_kernel(
             const long long f = tile / nb;
             out[(f << logN) + b * S + sL + (long long)N1 * k2] = db_of(y);
         });
+}
+
+template <int L, int S>
+__global__ __launch_bounds__(S * L / 16) void fft_passB_kernel(
+    const float2* __restrict__ scratch, int frames, int N1, int logN, const float2* __restrict__ tw,
+    float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    passB_tile<L, S>(lds, blockIdx.x, scratch, frames, N1, logN, tw, out);
+}
+
+// ---- merged launch: pass B of chunk c (first nB workgroups) + pass A of chunk c+1 --------
+// The two halves share nothing (pass A writes the other scratch buffer), so one launch
+// replaces two dependent kernel boundaries per chunk; the pass-B workgroups are dispatched
+// first and pass A fills the CUs as they drain. Needs equal thread counts (SA*LA == SB*LB).
+template <int LA, int SA, int LB, int SB, bool PAIRED>
+__global__ __launch_bounds__((PAIRED ? SA / 2 : SA) * LA / 16) __attribute__((amdgpu_waves_per_eu(4))) void fft_merged_kernel(
+    int nB, const float2* __restrict__ scratchB, int framesB, float* __restrict__ outB,
+    const float2* __restrict__ in, long long frameStride, int framesA, const float* __restrict__ win, int nz,
+    int logN, const float2* __restrict__ tw1, const float2* __restrict__ tw2, const float2* __restrict__ tfull,
+    float2* __restrict__ scratchA) {
+    static_assert((PAIRED ? SA / 2 : SA) * LA == SB * LB, "merged pass kernels need equal workgroup sizes");
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    if ((int)blockIdx.x < nB) {
+        passB_tile<LB, SB>(lds, blockIdx.x, scratchB, framesB, LA, logN, tw2, outB);
+    } else if constexpr (PAIRED) {
+        passA2_tile<LA, SA>(lds, blockIdx.x - nB, in, frameStride, framesA, win, nz, LB, logN, tw1, tfull, scratchA, 0);
+    } else {
+        passA_tile<LA, SA>(lds, blockIdx.x - nB, in, frameStride, framesA, win, nz, LB, logN, tw1, tfull, scratchA, 0);
+    }
 }
 
 // ---------------------------------------------------------------- host side
@@ -325,6 +455,9 @@ struct FftPlan {
     // 2.98 vs 2.39 ms per step; the concurrent passes evict each other's Infinity-Cache
     // working set), so it is off unless SDRGPU_FFT_PIPE=1.
     int pipe = 0;
+    // merged pass-B(c) + pass-A(c+1) launches (64k split): one launch boundary per chunk
+    // instead of two; 1.87 -> 1.73 ms per 2^28 samples (A/B on one box). SDRGPU_FFT_MERGE=0 off.
+    int merge = 1;
     hipStream_t s2 = nullptr;
     hipEvent_t evFork = nullptr, evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr};
     DevBuf scratch2;
@@ -364,11 +497,11 @@ static int launch_single(const FftPlan& p, const float2* in, long long stride, i
 template <int L, int S>
 static int launch_passA(const FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
     auto k = fft_passA_kernel<L, S>;
-    size_t lds = sizeof(float2) * S * Lds<L>::LS;
+    size_t lds = sizeof(float2) * (S * Lds<L>::LS + (L == 256 ? L : 0));   // + stage twiddles (256-point columns)
     SDRGPU_CHECK(set_lds(k, lds));
     const int g = (p.N2 / S) * frames;
     hipLaunchKernelGGL(k, dim3(g), dim3(S * L / 16), lds, s, in, stride, frames, p.win.as<float>(), p.nz, p.N2,
-                       p.logN, p.tw1.as<float2>(), p.tfull.as<float2>(), p.cur);
+                       p.logN, p.tw1.as<float2>(), p.tfull.as<float2>(), p.cur, p.dbg);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
@@ -397,6 +530,30 @@ static int launch_passB(const FftPlan& p, int frames, float* out, hipStream_t s)
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
+
+template <int LA, int SA, int LB, int SB, bool PAIRED>
+static int launch_merged(const FftPlan& p, const float2* scratchB, int framesB, float* outB, const float2* in,
+                         long long stride, int framesA, float2* scratchA, hipStream_t s) {
+    auto k = fft_merged_kernel<LA, SA, LB, SB, PAIRED>;
+    size_t lds = sizeof(float2) * std::max(SA * Lds<LA>::LS + ((PAIRED || LA == 256) ? LA : 0), SB * Lds<LB>::LS);
+    SDRGPU_CHECK(set_lds(k, lds));
+    const int nB = (LA / SB) * framesB, nA = (LB / SA) * framesA;
+    hipLaunchKernelGGL(k, dim3(nB + nA), dim3(SB * LB / 16), lds, s, nB, scratchB, framesB, outB, in, stride, framesA,
+                       p.win.as<float>(), p.nz, p.logN, p.tw1.as<float2>(), p.tw2.as<float2>(), p.tfull.as<float2>(),
+                       scratchA);
+    SDRGPU_HIP(hipGetLastError());
+    return SDRGPU_OK;
+}
+
+// merged pass B (chunk c) + pass A (chunk c+1) launches: the 64k split (256 x 256, one-column
+// pass A). The 1M split's merged form (paired pass A, pass B at 8 rows to match its 512
+// threads) measured 12% SLOWER (2.68 vs 2.39 ms per 256 frames): pass B loses half its
+// occupancy to pass A's 147 KB of LDS, so the 1M transform keeps separate launches.
+static int dispatch_merged(const FftPlan& p, const float2* scratchB, int framesB, float* outB, const float2* in,
+                           long long stride, int framesA, float2* scratchA, hipStream_t s) {
+    return launch_merged<256, 16, 256, 16, false>(p, scratchB, framesB, outB, in, stride, framesA, scratchA, s);
+}
+static bool merged_supported(const FftPlan& p, bool paired) { return !paired && p.N1 == 256 && p.N2 == 256 && p.sa == 16; }
 
 static int dispatch_single(const FftPlan& p, const float2* in, long long stride, int frames, float* out, hipStream_t s) {
     switch (p.N) {
@@ -506,13 +663,15 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         if (rc >= 0) rc = make_twiddles(p.tw2, p.N2);
 
         // chunk so the pass-A -> pass-B intermediate (+ the input it came from) stays
-        // resident in the Infinity Cache: 64 MB of intermediate per chunk
-        long long chunkMB = 64;
+        // resident in the Infinity Cache: 128 MB of intermediate per chunk (64 and 192-256 MB
+        // measured 2-5% slower for 64k with merged launches; 1M: 2.32 vs 2.39 ms at 64 MB)
+        long long chunkMB = 128;
         if (const char* e = getenv("SDRGPU_FFT_CHUNK_MB")) chunkMB = std::max(1, atoi(e));
         if (const char* e = getenv("SDRGPU_FFT_SA")) p.sa = atoi(e);
         if (const char* e = getenv("SDRGPU_FFT_SB")) p.sb = atoi(e);
         if (const char* e = getenv("SDRGPU_FFT_DEBUG")) p.dbg = atoi(e);
         if (const char* e = getenv("SDRGPU_FFT_PIPE")) p.pipe = atoi(e);
+        if (const char* e = getenv("SDRGPU_FFT_MERGE")) p.merge = atoi(e);
         p.chunkFrames = std::max(1, (int)((chunkMB << 20) / ((long long)fftSize * 8)));
         // paired-column pass A: +13% on the 1M transform (N1 = 1024), but slower than the
         // one-column kernel at N1 = 256 (64k: 2.05-2.10 vs 1.86 ms per 2^28 samples, A/B on
@@ -533,7 +692,6 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
                 rc = SDRGPU_EHIP;
             }
         }
-        if (rc >= 0) rc = p.scratch.ensure((size_t)p.chunkFrames * fftSize * sizeof(float2));
     }
     if (rc >= 0 && hipStreamCreateWithFlags(&p.own, hipStreamNonBlocking) != hipSuccess) {
         set_error("fft_create: hipStreamCreate failed");
@@ -575,6 +733,26 @@ extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long f
     // 16-B loads need an even frame stride and a 16-B aligned base
     const bool paired = p.sa2 > 0 && (frameStride % 2) == 0 && ((uintptr_t)in & 15) == 0;
     const int nchunks = (frames + p.chunkFrames - 1) / p.chunkFrames;
+    // the intermediate grows with the largest chunk seen (a single-frame drop-in plan holds 0.5 MB)
+    SDRGPU_CHECK(p.scratch.ensure((size_t)std::min(p.chunkFrames, frames) * p.N * sizeof(float2)));
+    if (p.merge && nchunks > 1 && merged_supported(p, paired)) {
+        // A(0); [B(c-1) + A(c)] for c = 1..; B(last). Scratch alternates between two buffers.
+        SDRGPU_CHECK(p.scratch2.ensure(p.scratch.bytes));
+        float2* sc[2] = {p.scratch.as<float2>(), p.scratch2.as<float2>()};
+        p.cur = sc[0];
+        if (paired) SDRGPU_CHECK(dispatch_passA2(p, x, frameStride, std::min(p.chunkFrames, frames), s));
+        else SDRGPU_CHECK(dispatch_passA(p, x, frameStride, std::min(p.chunkFrames, frames), s));
+        for (int c = 1; c < nchunks; c++) {
+            const int fB = (c - 1) * p.chunkFrames, nfB = p.chunkFrames;
+            const int fA = c * p.chunkFrames, nfA = std::min(p.chunkFrames, frames - fA);
+            SDRGPU_CHECK(dispatch_merged(p, sc[(c - 1) & 1], nfB, out + (long long)fB * p.N,
+                                         x + (long long)fA * frameStride, frameStride, nfA, sc[c & 1], s));
+        }
+        const int fL = (nchunks - 1) * p.chunkFrames;
+        p.cur = sc[(nchunks - 1) & 1];
+        SDRGPU_CHECK(dispatch_passB(p, frames - fL, out + (long long)fL * p.N, s));
+        return frames;
+    }
     const bool pipe = p.pipe && nchunks > 1;
     if (pipe) {
         if (!p.s2) {
