@@ -64,13 +64,24 @@ class C5:
         self.bytes_per_sample = 8 + 4 + 8 / 256 + 8 / 256   # ~12.06 B
         self.kernel_bytes = 12.0 * self.B                   # spectrum pair: 8 B in + 4 B dB out per sample
         self.kernel_name = "spectrum (fft_passA + fft_passB, N=65536)"
+        self.pieces = max(1, int(os.environ.get("BENCH_C5_PIECES", "1")))
 
-    def dominant(self, x, s):
-        self.fft.execute_dev(x.data_ptr(), self.N, self.frames, self.spectra.data_ptr(), s)
-
-    def rest(self, x, s):
-        m = self.vfo.process_dev(x.data_ptr(), self.B, self.ifbuf.data_ptr(), s)
-        self.wfm.process_dev(self.ifbuf.data_ptr(), m, self.audio.data_ptr(), s)
+    def run(self, x, s, timed_call):
+        # the batch is pushed through the chain in `pieces` blocks, each through the spectrum and
+        # then the VFO, as the reference's splitter feeds both paths block by block
+        # (iq_frontend.cpp:15-52); pieces > 1 lets the VFO re-read a block the spectrum just read
+        P = self.pieces
+        fpp = self.frames // P
+        m_if = m_au = 0
+        for k in range(P):
+            f0 = k * fpp
+            nf = fpp if k < P - 1 else self.frames - f0
+            xp = x.data_ptr() + 8 * f0 * self.N
+            timed_call(lambda: self.fft.execute_dev(xp, self.N, nf, self.spectra.data_ptr() + 4 * f0 * self.N, s))
+            m = self.vfo.process_dev(xp, nf * self.N, self.ifbuf.data_ptr() + 8 * m_if, s)
+            a = self.wfm.process_dev(self.ifbuf.data_ptr() + 8 * m_if, m, self.audio.data_ptr() + 8 * m_au, s)
+            m_if += m
+            m_au += a
 
     def gather_src(self):
         return self.spectra[-16 * self.N:]
@@ -146,6 +157,11 @@ class C4:
 
     def gather_src(self):
         return self.out[:2 * 16 * self.M]
+
+
+def _run_generic(wl, x, s, timed_call):
+    timed_call(lambda: wl.dominant(x, s))
+    wl.rest(x, s)
 
 
 def _timed(fn, blk, seconds):
@@ -255,6 +271,8 @@ def main():
     gather_bufs = None
     if world > 1 and rank == 0:
         gather_bufs = [torch.empty_like(wl.gather_src()) for _ in range(world)]
+    gather_stage = torch.empty_like(wl.gather_src()) if world > 1 else None
+    pending = [None]   # the in-flight gather (async work handle)
 
     ev = []
     # One stream for the whole step. Forking the spectrum and the VFO chain onto two streams
@@ -263,28 +281,49 @@ def main():
     # spectrum kernels' event/rocprof durations stretch by the overlap, so the roofline
     # numbers would stop describing the kernel.
     def step(timed):
+        evs = []
+
+        def timed_call(fn):   # HIP events around the dominant kernel's launches, on their stream
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            fn()
+            if timed:
+                e1.record(stream)
+                evs.append((e0, e1))
+        if hasattr(wl, "run"):
+            wl.run(x, stream.cuda_stream, timed_call)
+        else:
+            _run_generic(wl, x, stream.cuda_stream, timed_call)
         if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        wl.dominant(x, stream.cuda_stream)
-        if timed:
-            e1.record(stream)
-            ev.append((e0, e1))
-        wl.rest(x, stream.cuda_stream)
+            ev.append(evs)
         if world > 1:
-            shard.gather_spectra(wl.gather_src(), gather_bufs)
+            # RCCL gather of this step's latest spectra, overlapped with the next step: the rows
+            # are snapshotted into a staging buffer (the next step overwrites them) and the
+            # collective runs on the process group's stream; it is waited on one step later
+            if pending[0] is not None:
+                pending[0].wait()
+            gather_stage.copy_(wl.gather_src())
+            pending[0], _ = shard.gather_spectra_async(gather_stage, gather_bufs)
+
+    def drain():
+        if pending[0] is not None:
+            pending[0].wait()
+            pending[0] = None
 
     for _ in range(a.warmup):
         step(False)
+    drain()
     torch.cuda.synchronize()
     shard.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step(True)
+    drain()   # the last step's gather is inside the timed region
     torch.cuda.synchronize()
     shard.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / max(len(ev), 1)
+    kern_ms = sum(sum(e0.elapsed_time(e1) for e0, e1 in evs) for evs in ev) / max(len(ev), 1)
     elapsed, kern_ms = shard.max_over_ranks([elapsed, kern_ms], device="cuda")
 
     if rank == 0:

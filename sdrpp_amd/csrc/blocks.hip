@@ -245,6 +245,122 @@ __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
     }
 }
 
+// ------------------------------------------------ MFMA FIR (complex data x real taps)
+// With Qp = ceil(ntaps / D) taps per phase (C3: 256 taps / 8 = 32), each phase's correlation
+//   y_p[m] = sum_q g_p[q] u_p[m + q],   u_p[n] = span[n D + p],   g_p[q] = h[q D + p]
+// is a Toeplitz product and runs on the f32 matrix cores (v_mfma_f32_16x16x4_f32: exact fp32
+// FMA chains at the vector-FMA peak, one VGPR per operand, no VALU issue):
+//   Y[i][j] += sum_k A[i][k] B[k][j],   A[i][k] = u_p[o + 16 i + k],   B[k][j] = g_p[k - j]
+// (zero outside [0, Qp)), so the 16 x 16 accumulator holds outputs o + 16 i + j and k runs over
+// [0, 16 + Qp - 1) in steps of 4 (1.47x the essential MACs at Qp = 32). Re and im are two
+// accumulators sharing B. A wave owns 256 consecutive outputs, a workgroup MF_TM = 1024.
+// LDS: the span phase-major with one pad row per 16 (X[p][r + r / 16]: the 16 rows of one A
+// load fall in distinct banks), and B as gz[p][t] = g_p[t - 15], t < 64 (host-built).
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+constexpr int MF_TM = 1024;                 // outputs per workgroup tile (4 waves x 256)
+constexpr int MF_KS = 12;                   // k steps of 4: k < 48 >= 16 + Qp - 1 for Qp <= 32
+constexpr int MF_ROWS = MF_TM + 4 * MF_KS;  // span rows per phase
+constexpr int MF_GZ = 64;                   // gz entries per phase
+
+template <bool XL, bool QUAD>
+__global__ __launch_bounds__(256) void fir_mfma_kernel(FirArgs a) {
+    constexpr int PF = 36, NT = 256, QOFF = QUAD ? 1 : 0;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float2* X = reinterpret_cast<float2*>(smem);
+    float* gz = reinterpret_cast<float*>(smem + a.tapsLdsOff);
+    const int tid = threadIdx.x, tile = blockIdx.x;
+    const int D = a.D, RSP = a.RSP, dsh = a.dshift;   // D a power of two dividing NT (host-checked)
+    {
+        const float* __restrict__ g = reinterpret_cast<const float*>(a.taps);
+        for (int i = tid; i < D * MF_GZ; i += NT) gz[i] = g[i];
+    }
+    auto lds_index = [&](int sx) {
+        const int r = sx >> dsh, p = sx & (D - 1);
+        return p * RSP + r + (r >> 4);
+    };
+    const int mFirst = tile * a.TMS - QOFF;
+    const long long b0 = (long long)a.offset0 + (long long)mFirst * D;
+    const int span = MF_ROWS * D;
+    const bool interior = (b0 >= a.H) && (b0 + span <= (long long)a.H + a.count);
+    int sxRest = tid;
+    if (interior) {
+        const float2* __restrict__ src = reinterpret_cast<const float2*>(a.in) + (b0 - a.H);
+        float2 pf[PF];
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            const int sx = tid + u * NT;
+            if (sx < span) pf[u] = src[sx];
+        }
+        if constexpr (XL) {
+            const float2 ph0 = nco_tab(a.phi, a.plo, b0 - a.H + tid);
+            const float2* __restrict__ S = a.nstep;
+#pragma unroll
+            for (int u = 0; u < PF; u++) pf[u] = cmulf(pf[u], cmulf(ph0, S[u]));
+        }
+        // slot u: phase tid % D fixed, row advancing by NT / D (+ its pad rows)
+        int idx = lds_index(tid);
+        const int inc = (NT >> dsh) + (NT >> dsh) / 16;
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            if (tid + u * NT < span) X[idx] = pf[u];
+            idx += inc;
+        }
+        sxRest = tid + PF * NT;
+    }
+    for (int sx = sxRest; sx < span; sx += NT) X[lds_index(sx)] = fir_fetch<float2, XL>(a, b0 + sx);
+    __syncthreads();
+
+    const int lane = tid & 63, o = (tid >> 6) * 256;
+    const int i = lane & 15, kk = lane >> 4;   // A row i / B column j = i, k offset kk
+    f32x4_t cre = {0.f, 0.f, 0.f, 0.f}, cim = {0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < D; p++) {
+        const float2* Xp = X + p * RSP;
+        const float* gp = gz + p * MF_GZ + 15 - i + kk;   // B[k0 + kk][i] = g_p[k0 + kk - i]
+        const int r0 = o + 16 * i + kk;
+#pragma unroll
+        for (int s = 0; s < MF_KS; s++) {
+            const int r = r0 + 4 * s;
+            const float2 xa = Xp[r + (r >> 4)];
+            const float bb = gp[4 * s];
+            cre = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.x, bb, cre, 0, 0, 0);
+            cim = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.y, bb, cim, 0, 0, 0);
+        }
+    }
+    // accumulator element e of this lane: row (lane >> 4) * 4 + e, column lane & 15
+    if constexpr (QUAD) {
+        // FM quadrature (demod/quadrature.h:41-56) on the tile's outputs staged in LDS (the span
+        // is dead once every wave has passed the barrier); output 0 of the tile only supplies y[m-1]
+        float2* Y = X;
+        const float2 din0 = a.din[0];
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 4; e++) Y[o + 16 * (kk * 4 + e) + i] = make_float2(cre[e], cim[e]);
+        __syncthreads();
+        float* out = reinterpret_cast<float*>(a.out);
+#pragma unroll
+        for (int e = 0; e < MF_TM / NT; e++) {
+            const int ml = tid + e * NT;
+            const int m = mFirst + ml;
+            if (ml >= QOFF && m >= 0 && m < a.M) {
+                const float2 y = Y[ml];
+                const float2 prev = (m == 0) ? din0 : Y[ml - 1];
+                const float br = prev.x, bi = -prev.y;
+                const float re = (y.x * br) - (y.y * bi);
+                const float im = (y.y * br) + (y.x * bi);
+                out[m] = atan2f(im, re) * a.invDev;
+                if (m == a.M - 1) a.dinNext[0] = y;
+            }
+        }
+    } else {
+        float2* out = reinterpret_cast<float2*>(a.out);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int m = mFirst + o + 16 * (kk * 4 + e) + i;
+            if (m < a.M && m < (tile + 1) * a.TMS) out[m] = make_float2(cre[e], cim[e]);
+        }
+    }
+}
+
 template <typename DT, bool XL>
 __global__ void fir_hist_kernel(const DT* __restrict__ hist, const DT* __restrict__ in, DT* __restrict__ next, int H,
                                 int count, const float2* __restrict__ phi, const float2* __restrict__ plo) {
@@ -430,6 +546,7 @@ struct FirBlock : Block {
         if (const char* e = getenv("SDRGPU_FIR_NT")) forceNT = atoi(e);
         if (const char* e = getenv("SDRGPU_FIR_K")) forceK = atoi(e);
         if (const char* e = getenv("SDRGPU_FIR_LDS_KB")) ldsCap = std::max(8, atoi(e));
+        if (const char* e = getenv("SDRGPU_FIR_MFMA")) useMfma = atoi(e);
         SDRGPU_CHECK(init_stream());
         SDRGPU_CHECK(set_taps(t, n));
         return SDRGPU_OK;
@@ -478,7 +595,52 @@ struct FirBlock : Block {
             }
         SDRGPU_CHECK(taps.ensure(sizeof(float) * pq.size()));
         SDRGPU_HIP(hipMemcpy(taps.p, pq.data(), sizeof(float) * pq.size(), hipMemcpyHostToDevice));
+        // matrix-core path (fir_mfma_kernel): complex data, real taps, 16..32 taps per phase,
+        // D a power of two <= 16 (the span's load slots advance by whole pad groups)
+        const int Qr = (ntaps + D - 1) / D;
+        mf = in_dtype == SDRGPU_C64 && ttype == SDRGPU_F32 && !stereo && (D & (D - 1)) == 0 && D <= 16 &&
+             Qr <= 32 && (Qr >= 16 || useMfma == 2) && useMfma != 0;
+        if (mf) {
+            std::vector<float> g((size_t)D * MF_GZ, 0.0f);   // gz[p][t] = h[(t - 15) D + p]
+            for (int p = 0; p < D; p++)
+                for (int t = 15; t < MF_GZ; t++) {
+                    const int j = (t - 15) * D + p;
+                    if (t - 15 < Qr && j < ntaps) g[(size_t)p * MF_GZ + t] = host_taps[j];
+                }
+            SDRGPU_CHECK(gzTaps.ensure(sizeof(float) * g.size()));
+            SDRGPU_HIP(hipMemcpy(gzTaps.p, g.data(), sizeof(float) * g.size(), hipMemcpyHostToDevice));
+        }
         return SDRGPU_OK;
+    }
+    bool mf = false;        // fir_mfma_kernel selected for the current taps / decimation
+    int useMfma = 1;        // SDRGPU_FIR_MFMA (tuning): 0 off, 1 auto, 2 also below 16 taps per phase
+    DevBuf gzTaps;
+    template <bool XL, bool QD>
+    int launch_mfma(FirArgs& a, int tiles, size_t lds, hipStream_t s) {
+        auto k = fir_mfma_kernel<XL, QD>;
+        SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(k, dim3(tiles), dim3(256), lds, s, a);
+        SDRGPU_HIP(hipGetLastError());
+        return SDRGPU_OK;
+    }
+    int run_mfma(const void* in, int count, void* out, int M, hipStream_t s) {
+        FirArgs a{};
+        a.hist = hist[cur].p; a.in = in; a.taps = gzTaps.p; a.out = out;
+        a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
+        a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>();
+        a.ntaps = ntaps; a.H = ntaps - 1; a.count = count; a.D = D; a.offset0 = offset; a.M = M;
+        a.TMS = quad ? MF_TM - 1 : MF_TM;
+        a.RSP = MF_ROWS + MF_ROWS / 16 + 1;
+        a.dshift = __builtin_ctz((unsigned)D);
+        a.invDev = invDev;
+        a.nstep = xl ? nco.step_for(256) : nullptr;
+        const size_t xb = sizeof(float2) * (size_t)D * a.RSP;
+        a.tapsLdsOff = (int)((xb + 15) / 16 * 16);
+        const size_t lds = a.tapsLdsOff + sizeof(float) * D * MF_GZ;
+        const int tiles = (M + a.TMS - 1) / a.TMS;
+        a.ntiles = tiles;
+        if (xl) return quad ? launch_mfma<true, true>(a, tiles, lds, s) : launch_mfma<true, false>(a, tiles, lds, s);
+        return quad ? launch_mfma<false, true>(a, tiles, lds, s) : launch_mfma<false, false>(a, tiles, lds, s);
     }
     int out_count(int count) override { return count > offset ? (count - offset + D - 1) / D : 0; }
     int reset() override {
@@ -533,7 +695,9 @@ struct FirBlock : Block {
         const int M = out_count(count);
         const int H = ntaps - 1;
         if (xl && count > 0) SDRGPU_CHECK(nco.prepare(count, s));
-        if (M > 0) {
+        if (M > 0 && mf) {
+            SDRGPU_CHECK(run_mfma(in, count, out, M, s));
+        } else if (M > 0) {
             int K = choose_k();
             // LDS budget: span (TM + Q + K rows) * D elements + taps; shrink K, then the
             // tile's thread count, until it fits (large decimations: plan_8192 stage 0)

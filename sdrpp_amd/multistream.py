@@ -42,6 +42,17 @@ class StreamShard:
         dist.gather(local_rows, out_list if self.rank == 0 else None, dst=0)
         return out_list if self.rank == 0 else None
 
+    def gather_spectra_async(self, local_rows, out_list=None):
+        """Start the rank-0 gather and return (work, out_list); work.wait() before `local_rows`
+        or `out_list` are touched again. Over RCCL the collective runs on the process group's
+        own stream, so it overlaps the rest of the chain instead of serialising behind it."""
+        if self.world == 1:
+            return None, [local_rows]
+        if self.rank == 0 and out_list is None:
+            out_list = [torch.empty_like(local_rows) for _ in range(self.world)]
+        work = dist.gather(local_rows, out_list if self.rank == 0 else None, dst=0, async_op=True)
+        return work, (out_list if self.rank == 0 else None)
+
     def max_over_ranks(self, values, device=None):
         t = torch.tensor(values, dtype=torch.float64, device=device)
         if self.world > 1:

@@ -23,11 +23,14 @@ def _worker(rank, world, port, q):
     assert sh.seed() == 0xACE1 + rank and sh.vfo_offset() == 2.5e6 + 1e5 * rank
     rows = torch.full((4, 8), float(rank)) + torch.arange(8, dtype=torch.float32)   # "spectra" of this stream
     got = sh.gather_spectra(rows)
+    work, got2 = sh.gather_spectra_async(rows * 2)   # bench.py's overlapped form
+    work.wait()
     t = sh.max_over_ranks([1.0 + rank, 5.0 - rank])
     sh.barrier()
     if rank == 0:
         ok = len(got) == world and all(torch.equal(got[r], torch.full((4, 8), float(r)) + torch.arange(8.0))
                                         for r in range(world))
+        ok = ok and len(got2) == world and all(torch.equal(got2[r], 2 * got[r]) for r in range(world))
         q.put((ok, t))
     sh.close()
 
