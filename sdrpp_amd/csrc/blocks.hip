@@ -257,14 +257,15 @@ __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
 // LDS: the span phase-major with one pad row per 16 (X[p][r + r / 16]: the 16 rows of one A
 // load fall in distinct banks), and B as gz[p][t] = g_p[t - 15], t < 64 (host-built).
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
-constexpr int MF_TM = 1024;                 // outputs per workgroup tile (4 waves x 256)
 constexpr int MF_KS = 12;                   // k steps of 4: k < 48 >= 16 + Qp - 1 for Qp <= 32
-constexpr int MF_ROWS = MF_TM + 4 * MF_KS;  // span rows per phase
 constexpr int MF_GZ = 64;                   // gz entries per phase
+constexpr int mf_rows(int nw) { return 256 * nw + 4 * MF_KS; }   // span rows per phase
 
-template <bool XL, bool QUAD>
-__global__ __launch_bounds__(256) void fir_mfma_kernel(FirArgs a) {
-    constexpr int PF = 36, NT = 256, QOFF = QUAD ? 1 : 0;
+template <int NW, bool XL, bool QUAD>   // NW waves per workgroup, 256 outputs each
+__global__ __launch_bounds__(64 * NW) void fir_mfma_kernel(FirArgs a) {
+    constexpr int NT = 64 * NW, MF_TM = 256 * NW, MF_ROWS = mf_rows(NW);
+    constexpr int PF = (MF_ROWS * 8 + NT - 1) / NT;    // load slots per thread for D <= 8
+    constexpr int QOFF = QUAD ? 1 : 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float2* X = reinterpret_cast<float2*>(smem);
     float* gz = reinterpret_cast<float*>(smem + a.tapsLdsOff);
@@ -547,6 +548,7 @@ struct FirBlock : Block {
         if (const char* e = getenv("SDRGPU_FIR_K")) forceK = atoi(e);
         if (const char* e = getenv("SDRGPU_FIR_LDS_KB")) ldsCap = std::max(8, atoi(e));
         if (const char* e = getenv("SDRGPU_FIR_MFMA")) useMfma = atoi(e);
+        if (const char* e = getenv("SDRGPU_FIR_MFMA_NW")) mfNW = atoi(e);
         SDRGPU_CHECK(init_stream());
         SDRGPU_CHECK(set_taps(t, n));
         return SDRGPU_OK;
@@ -596,9 +598,9 @@ struct FirBlock : Block {
         SDRGPU_CHECK(taps.ensure(sizeof(float) * pq.size()));
         SDRGPU_HIP(hipMemcpy(taps.p, pq.data(), sizeof(float) * pq.size(), hipMemcpyHostToDevice));
         // matrix-core path (fir_mfma_kernel): complex data, real taps, 16..32 taps per phase,
-        // D a power of two <= 16 (the span's load slots advance by whole pad groups)
+        // D a power of two <= 8 (with 128 threads, a load slot advances by whole 16-row pad groups)
         const int Qr = (ntaps + D - 1) / D;
-        mf = in_dtype == SDRGPU_C64 && ttype == SDRGPU_F32 && !stereo && (D & (D - 1)) == 0 && D <= 16 &&
+        mf = in_dtype == SDRGPU_C64 && ttype == SDRGPU_F32 && !stereo && (D & (D - 1)) == 0 && D <= 8 &&
              Qr <= 32 && (Qr >= 16 || useMfma == 2) && useMfma != 0;
         if (mf) {
             std::vector<float> g((size_t)D * MF_GZ, 0.0f);   // gz[p][t] = h[(t - 15) D + p]
@@ -615,15 +617,18 @@ struct FirBlock : Block {
     bool mf = false;        // fir_mfma_kernel selected for the current taps / decimation
     int useMfma = 1;        // SDRGPU_FIR_MFMA (tuning): 0 off, 1 auto, 2 also below 16 taps per phase
     DevBuf gzTaps;
-    template <bool XL, bool QD>
+    template <int NW, bool XL, bool QD>
     int launch_mfma(FirArgs& a, int tiles, size_t lds, hipStream_t s) {
-        auto k = fir_mfma_kernel<XL, QD>;
+        auto k = fir_mfma_kernel<NW, XL, QD>;
         SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(k, dim3(tiles), dim3(256), lds, s, a);
+        hipLaunchKernelGGL(k, dim3(tiles), dim3(64 * NW), lds, s, a);
         SDRGPU_HIP(hipGetLastError());
         return SDRGPU_OK;
     }
-    int run_mfma(const void* in, int count, void* out, int M, hipStream_t s) {
+    int mfNW = 4;           // SDRGPU_FIR_MFMA_NW (tuning): waves (x 256 outputs) per workgroup, 4 or 2 (2: 4 WG/CU, measured 13% slower on C3)
+    template <int NW>
+    int run_mfma_nw(const void* in, int count, void* out, int M, hipStream_t s) {
+        constexpr int MF_TM = 256 * NW, MF_ROWS = mf_rows(NW);
         FirArgs a{};
         a.hist = hist[cur].p; a.in = in; a.taps = gzTaps.p; a.out = out;
         a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
@@ -633,14 +638,17 @@ struct FirBlock : Block {
         a.RSP = MF_ROWS + MF_ROWS / 16 + 1;
         a.dshift = __builtin_ctz((unsigned)D);
         a.invDev = invDev;
-        a.nstep = xl ? nco.step_for(256) : nullptr;
+        a.nstep = xl ? nco.step_for(64 * NW) : nullptr;
         const size_t xb = sizeof(float2) * (size_t)D * a.RSP;
         a.tapsLdsOff = (int)((xb + 15) / 16 * 16);
         const size_t lds = a.tapsLdsOff + sizeof(float) * D * MF_GZ;
         const int tiles = (M + a.TMS - 1) / a.TMS;
         a.ntiles = tiles;
-        if (xl) return quad ? launch_mfma<true, true>(a, tiles, lds, s) : launch_mfma<true, false>(a, tiles, lds, s);
-        return quad ? launch_mfma<false, true>(a, tiles, lds, s) : launch_mfma<false, false>(a, tiles, lds, s);
+        if (xl) return quad ? launch_mfma<NW, true, true>(a, tiles, lds, s) : launch_mfma<NW, true, false>(a, tiles, lds, s);
+        return quad ? launch_mfma<NW, false, true>(a, tiles, lds, s) : launch_mfma<NW, false, false>(a, tiles, lds, s);
+    }
+    int run_mfma(const void* in, int count, void* out, int M, hipStream_t s) {
+        return mfNW == 4 ? run_mfma_nw<4>(in, count, out, M, s) : run_mfma_nw<2>(in, count, out, M, s);
     }
     int out_count(int count) override { return count > offset ? (count - offset + D - 1) / D : 0; }
     int reset() override {
