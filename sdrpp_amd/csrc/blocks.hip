@@ -75,6 +75,7 @@ struct FirArgs {
     int simple;         // D | NT and K | NT/D: constant LDS stride per load slot
     const float2* nstep;  // XL: e^{i w u NT}, u < NCO_PF, for this launch's NT
     float invDev;
+    int gzs;            // MFMA phase-split: gz entries per phase
 };
 
 // FIR tile kernel: one tile of NT*K outputs per workgroup.
@@ -362,6 +363,101 @@ __global__ __launch_bounds__(64 * NW) void fir_mfma_kernel(FirArgs a) {
     }
 }
 
+// Phase-split variant for larger decimations (VFO stage 1: D = 32, 143 taps -> Qp = 5): a tile
+// is 256 outputs, the four waves split the D phases (wave w takes p = w, w + 4, ...), each
+// accumulating the whole 16 x 16 output block over its phases with k < 4 * ks (ks = ceil((15 + Qp)
+// / 4) steps), and the four partial blocks are summed through LDS. Small tiles keep the span in
+// LDS for D up to 32 (75 KB at D = 32, 2 workgroups per CU) and for D = 8 let 7 share a CU.
+template <bool XL, bool QUAD>
+__global__ __launch_bounds__(256) void fir_mfma_ps_kernel(FirArgs a) {
+    constexpr int NT = 256, TM = 256, PF = 36, QOFF = QUAD ? 1 : 0;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float2* X = reinterpret_cast<float2*>(smem);
+    float* gz = reinterpret_cast<float*>(smem + a.tapsLdsOff);
+    const int tid = threadIdx.x, tile = blockIdx.x;
+    const int D = a.D, RSP = a.RSP, dsh = a.dshift, ks = a.Q;   // a.Q carries ks here
+    {
+        const float* __restrict__ g = reinterpret_cast<const float*>(a.taps);
+        for (int i = tid; i < D * a.gzs; i += NT) gz[i] = g[i];
+    }
+    auto lds_index = [&](int sx) {
+        const int r = sx >> dsh, p = sx & (D - 1);
+        return p * RSP + r + (r >> 4);
+    };
+    const int rows = TM + 4 * ks;
+    const int span = rows * D;
+    const int mFirst = tile * a.TMS - QOFF;
+    const long long b0 = (long long)a.offset0 + (long long)mFirst * D;
+    const bool interior = (b0 >= a.H) && (b0 + span <= (long long)a.H + a.count);
+    int sxRest = tid;
+    if (interior) {
+        const float2* __restrict__ src = reinterpret_cast<const float2*>(a.in) + (b0 - a.H);
+        float2 pf[PF];
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            const int sx = tid + u * NT;
+            if (sx < span) pf[u] = src[sx];
+        }
+        if constexpr (XL) {
+            const float2 ph0 = nco_tab(a.phi, a.plo, b0 - a.H + tid);
+            const float2* __restrict__ S = a.nstep;
+#pragma unroll
+            for (int u = 0; u < PF; u++) pf[u] = cmulf(pf[u], cmulf(ph0, S[u]));
+        }
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            const int sx = tid + u * NT;
+            if (sx < span) X[lds_index(sx)] = pf[u];
+        }
+        sxRest = tid + PF * NT;
+    }
+    for (int sx = sxRest; sx < span; sx += NT) X[lds_index(sx)] = fir_fetch<float2, XL>(a, b0 + sx);
+    __syncthreads();
+
+    const int lane = tid & 63, w = tid >> 6;
+    const int i = lane & 15, kk = lane >> 4;   // A row i / B column j = i, k offset kk
+    f32x4_t cre = {0.f, 0.f, 0.f, 0.f}, cim = {0.f, 0.f, 0.f, 0.f};
+    for (int p = w; p < D; p += 4) {
+        const float2* Xp = X + p * RSP;
+        const float* gp = gz + p * a.gzs + 15 - i + kk;   // B[k0 + kk][i] = g_p[k0 + kk - i]
+        const int r0 = 16 * i + kk;
+#pragma unroll
+        for (int s = 0; s < MF_KS; s++) {   // unrolled so the operand reads are issued ahead
+            if (s < ks) {
+                const int r = r0 + 4 * s;
+                const float2 xa = Xp[r + (r >> 4)];
+                const float bb = gp[4 * s];
+                cre = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.x, bb, cre, 0, 0, 0);
+                cim = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.y, bb, cim, 0, 0, 0);
+            }
+        }
+    }
+    // partial blocks of the four waves -> LDS (the span is dead after the barrier), summed per output
+    float2* P = X;
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 4; e++) P[w * TM + 16 * (kk * 4 + e) + i] = make_float2(cre[e], cim[e]);
+    __syncthreads();
+    auto ysum = [&](int ml) {
+        const float2 q0 = P[ml], q1 = P[TM + ml], q2 = P[2 * TM + ml], q3 = P[3 * TM + ml];
+        return make_float2((q0.x + q1.x) + (q2.x + q3.x), (q0.y + q1.y) + (q2.y + q3.y));
+    };
+    const int ml = tid, m = mFirst + ml;
+    if constexpr (QUAD) {
+        if (ml >= QOFF && m >= 0 && m < a.M) {
+            const float2 y = ysum(ml);
+            const float2 prev = (m == 0) ? a.din[0] : ysum(ml - 1);
+            const float br = prev.x, bi = -prev.y;
+            const float re = (y.x * br) - (y.y * bi);
+            const float im = (y.y * br) + (y.x * bi);
+            reinterpret_cast<float*>(a.out)[m] = atan2f(im, re) * a.invDev;
+            if (m == a.M - 1) a.dinNext[0] = y;
+        }
+    } else {
+        if (m < a.M && m < (tile + 1) * a.TMS) reinterpret_cast<float2*>(a.out)[m] = ysum(ml);
+    }
+}
+
 template <typename DT, bool XL>
 __global__ void fir_hist_kernel(const DT* __restrict__ hist, const DT* __restrict__ in, DT* __restrict__ next, int H,
                                 int count, const float2* __restrict__ phi, const float2* __restrict__ plo) {
@@ -549,6 +645,7 @@ struct FirBlock : Block {
         if (const char* e = getenv("SDRGPU_FIR_LDS_KB")) ldsCap = std::max(8, atoi(e));
         if (const char* e = getenv("SDRGPU_FIR_MFMA")) useMfma = atoi(e);
         if (const char* e = getenv("SDRGPU_FIR_MFMA_NW")) mfNW = atoi(e);
+        if (const char* e = getenv("SDRGPU_FIR_MFMA_PS")) usePS = atoi(e);
         SDRGPU_CHECK(init_stream());
         SDRGPU_CHECK(set_taps(t, n));
         return SDRGPU_OK;
@@ -600,14 +697,20 @@ struct FirBlock : Block {
         // matrix-core path (fir_mfma_kernel): complex data, real taps, 16..32 taps per phase,
         // D a power of two <= 8 (with 128 threads, a load slot advances by whole 16-row pad groups)
         const int Qr = (ntaps + D - 1) / D;
-        mf = in_dtype == SDRGPU_C64 && ttype == SDRGPU_F32 && !stereo && (D & (D - 1)) == 0 && D <= 8 &&
-             Qr <= 32 && (Qr >= 16 || useMfma == 2) && useMfma != 0;
-        if (mf) {
-            std::vector<float> g((size_t)D * MF_GZ, 0.0f);   // gz[p][t] = h[(t - 15) D + p]
+        const bool cplx = in_dtype == SDRGPU_C64 && ttype == SDRGPU_F32 && !stereo && (D & (D - 1)) == 0 && Qr <= 32 &&
+                          useMfma != 0;
+        mf = cplx && D <= 8 && (Qr >= 16 || useMfma == 2);
+        // phase-split tiles for the larger decimations (and on request for the others)
+        mfps = cplx && !mf && D >= 4 && D <= 32 && (usePS != 0);
+        if (usePS == 2 && cplx && D >= 4 && D <= 32) { mfps = true; mf = false; }
+        if (mf || mfps) {
+            // gz[p][t] = h[(t - 15) D + p], gzs entries per phase (t < 15 + 4 ks suffice)
+            gzs = mf ? MF_GZ : 16 + 4 * ((15 + Qr + 3) / 4);
+            std::vector<float> g((size_t)D * gzs, 0.0f);
             for (int p = 0; p < D; p++)
-                for (int t = 15; t < MF_GZ; t++) {
+                for (int t = 15; t < gzs; t++) {
                     const int j = (t - 15) * D + p;
-                    if (t - 15 < Qr && j < ntaps) g[(size_t)p * MF_GZ + t] = host_taps[j];
+                    if (t - 15 < Qr && j < ntaps) g[(size_t)p * gzs + t] = host_taps[j];
                 }
             SDRGPU_CHECK(gzTaps.ensure(sizeof(float) * g.size()));
             SDRGPU_HIP(hipMemcpy(gzTaps.p, g.data(), sizeof(float) * g.size(), hipMemcpyHostToDevice));
@@ -615,6 +718,41 @@ struct FirBlock : Block {
         return SDRGPU_OK;
     }
     bool mf = false;        // fir_mfma_kernel selected for the current taps / decimation
+    bool mfps = false;      // fir_mfma_ps_kernel selected
+    int gzs = MF_GZ;
+    int usePS = 1;          // SDRGPU_FIR_MFMA_PS (tuning): 0 off, 1 auto (D >= 4 where fir_mfma_kernel is not used), 2 force
+    template <bool XL, bool QD>
+    int launch_mfma_ps(FirArgs& a, int tiles, size_t lds, hipStream_t s) {
+        auto k = fir_mfma_ps_kernel<XL, QD>;
+        SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(k, dim3(tiles), dim3(256), lds, s, a);
+        SDRGPU_HIP(hipGetLastError());
+        return SDRGPU_OK;
+    }
+    int run_mfma_ps(const void* in, int count, void* out, int M, hipStream_t s) {
+        FirArgs a{};
+        a.hist = hist[cur].p; a.in = in; a.taps = gzTaps.p; a.out = out;
+        a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
+        a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>();
+        a.ntaps = ntaps; a.H = ntaps - 1; a.count = count; a.D = D; a.offset0 = offset; a.M = M;
+        const int Qr = (ntaps + D - 1) / D;
+        a.Q = (15 + Qr + 3) / 4;                        // k steps
+        const int rows = 256 + 4 * a.Q;
+        a.RSP = (rows + rows / 16) | 1;                 // odd: the D phases of one load slot in distinct banks
+        a.TMS = quad ? 255 : 256;
+        a.dshift = __builtin_ctz((unsigned)D);
+        a.invDev = invDev;
+        a.nstep = xl ? nco.step_for(256) : nullptr;
+        const size_t xb = std::max(sizeof(float2) * (size_t)D * a.RSP, sizeof(float2) * 4 * 256);   // span / partials
+        a.tapsLdsOff = (int)((xb + 15) / 16 * 16);
+        a.gzs = gzs;
+        const size_t lds = a.tapsLdsOff + sizeof(float) * D * gzs;   // D = 32, Qp = 5: 79.6 KB, 2 per CU
+        if (lds > 150 * 1024) { set_error("fir: MFMA tile does not fit (D %d)", D); return SDRGPU_EARG; }
+        const int tiles = (M + a.TMS - 1) / a.TMS;
+        a.ntiles = tiles;
+        if (xl) return quad ? launch_mfma_ps<true, true>(a, tiles, lds, s) : launch_mfma_ps<true, false>(a, tiles, lds, s);
+        return quad ? launch_mfma_ps<false, true>(a, tiles, lds, s) : launch_mfma_ps<false, false>(a, tiles, lds, s);
+    }
     int useMfma = 1;        // SDRGPU_FIR_MFMA (tuning): 0 off, 1 auto, 2 also below 16 taps per phase
     DevBuf gzTaps;
     template <int NW, bool XL, bool QD>
@@ -705,6 +843,8 @@ struct FirBlock : Block {
         if (xl && count > 0) SDRGPU_CHECK(nco.prepare(count, s));
         if (M > 0 && mf) {
             SDRGPU_CHECK(run_mfma(in, count, out, M, s));
+        } else if (M > 0 && mfps) {
+            SDRGPU_CHECK(run_mfma_ps(in, count, out, M, s));
         } else if (M > 0) {
             int K = choose_k();
             // LDS budget: span (TM + Q + K rows) * D elements + taps; shrink K, then the
