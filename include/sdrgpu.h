@@ -214,9 +214,27 @@ int sdrgpu_wav_encode_dev(int device, int kind, const float* in, long long n, un
 /* file_source / rtl_sdr / hackrf sample converters (elementwise, n scalars):
  * kind 0 u8 (b-128+0.5f)/127.5f, 1 i16 (s+0.5f)/32767.5f, 2 i24 packed LE,
  * 3 i32 ((v+0.5)/(2^31-0.5) in double), 4 f64 -> f32, 5 i8 x*(1/128) */
-enum { SDRGPU_CONV_U8 = 0, SDRGPU_CONV_I16, SDRGPU_CONV_I24, SDRGPU_CONV_I32, SDRGPU_CONV_F64, SDRGPU_CONV_I8 };
+enum { SDRGPU_CONV_U8 = 0, SDRGPU_CONV_I16, SDRGPU_CONV_I24, SDRGPU_CONV_I32, SDRGPU_CONV_F64, SDRGPU_CONV_I8,
+       SDRGPU_CONV_F32 /* 32-bit IEEE float copied as it is (WAV IEEE_FLOAT 32) */ };
 int sdrgpu_convert_dev(int device, int kind, const void* in, long long n, float* out, void* stream);
 int sdrgpu_convert(int device, int kind, const void* in, long long n, float* out);      /* host buffers */
+/* one-channel file_source WAV (main.cpp:294-430): n samples -> n complex_t with I = Q = the
+ * converted sample (any SDRGPU_CONV_* kind) */
+int sdrgpu_convert_mono_dev(int device, int kind, const void* in, long long n, void* out, void* stream);
+int sdrgpu_convert_mono(int device, int kind, const void* in, long long n, void* out);   /* host buffers */
+
+/* file_source WavReader (source_modules/file_source/src/wavreader.h:34-226): RIFF / RF64 WAVE,
+ * fmt PCM / IEEE_FLOAT / EXTENSIBLE (by SubFormat), samples = [data offset, end of file) */
+typedef struct sdrgpu_wav sdrgpu_wav;
+int sdrgpu_wav_open(sdrgpu_wav** h, const char* path);
+int sdrgpu_wav_info(sdrgpu_wav* h, int* format, int* channels, int* bits, double* sampleRate, long long* sampleCount);
+/* converter kind (SDRGPU_CONV_*) for the file's (format, bits) as worker_1ch / worker_2ch pick it
+ * (main.cpp:316-560); < 0 = unsupported (error) */
+int sdrgpu_wav_kind(sdrgpu_wav* h);
+int sdrgpu_wav_block_size(sdrgpu_wav* h);                      /* min(fs / 200, 1e6) frames */
+int sdrgpu_wav_read(sdrgpu_wav* h, void* out, int maxFrames);   /* raw frames; 0 at the end */
+int sdrgpu_wav_seek(sdrgpu_wav* h, long long frame);
+int sdrgpu_wav_close(sdrgpu_wav* h);
 
 #ifdef __cplusplus
 }

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("SDRGPU_LIB_PATH") or os.path.join(_HERE, "lib", "libs
 
 F32, C64 = 0, 1
 WIN_RECTANGULAR, WIN_HAMMING, WIN_HANN, WIN_BLACKMAN, WIN_NUTTALL, WIN_BH4, WIN_BH7 = range(7)
-CONV_U8, CONV_I16, CONV_I24, CONV_I32, CONV_F64, CONV_I8 = range(6)
+CONV_U8, CONV_I16, CONV_I24, CONV_I32, CONV_F64, CONV_I8, CONV_F32 = range(7)
 
 
 class SdrGpuError(RuntimeError):
@@ -122,6 +122,16 @@ def _load():
         "sdrgpu_block_destroy": (i, [vp]),
         "sdrgpu_convert_dev": (i, [i, i, vp, ll, vp, vp]),
         "sdrgpu_convert": (i, [i, i, vp, ll, vp]),
+        "sdrgpu_convert_mono_dev": (i, [i, i, vp, ll, vp, vp]),
+        "sdrgpu_convert_mono": (i, [i, i, vp, ll, vp]),
+        "sdrgpu_wav_open": (i, [pp, ctypes.c_char_p]),
+        "sdrgpu_wav_info": (i, [vp, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(d),
+                                ctypes.POINTER(ll)]),
+        "sdrgpu_wav_kind": (i, [vp]),
+        "sdrgpu_wav_block_size": (i, [vp]),
+        "sdrgpu_wav_read": (i, [vp, vp, i]),
+        "sdrgpu_wav_seek": (i, [vp, ll]),
+        "sdrgpu_wav_close": (i, [vp]),
     }
     alt = bool(os.environ.get("SDRGPU_LIB_PATH"))
     for name, (res, args) in sig.items():

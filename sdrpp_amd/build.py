@@ -27,6 +27,7 @@ SOURCES = [
     ("loops.hip", ["-ffp-contract=off"]),   # bit-exact serial recurrences
     ("frontend.hip", []),
     ("consumers.hip", ["-ffp-contract=off"]),   # bit-exact encoders
+    ("file_source.cpp", []),
 ]
 
 

@@ -559,24 +559,32 @@ __global__ void poly_kernel(const DT* __restrict__ hist, const DT* __restrict__ 
 }
 
 // ------------------------------------------------------------ converters
-__global__ void convert_kernel(int kind, const void* __restrict__ in, long long n, float* __restrict__ out) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    float r;
+__device__ __forceinline__ float convert_one(int kind, const void* __restrict__ in, long long i) {
     switch (kind) {
-    case SDRGPU_CONV_U8: r = (((const uint8_t*)in)[i] - 128 + 0.5f) / (128.0f - 0.5f); break;
-    case SDRGPU_CONV_I16: r = (((const int16_t*)in)[i] + 0.5f) / (32768.0f - 0.5f); break;
+    case SDRGPU_CONV_U8: return (((const uint8_t*)in)[i] - 128 + 0.5f) / (128.0f - 0.5f);
+    case SDRGPU_CONV_I16: return (((const int16_t*)in)[i] + 0.5f) / (32768.0f - 0.5f);
     case SDRGPU_CONV_I24: {
         const uint8_t* p = (const uint8_t*)in + 3 * i;
         int32_t v = (int32_t)((uint32_t)(p[0] | (p[1] << 8) | (p[2] << 16)) << 8) >> 8;
-        r = (v + 0.5f) / (8388608.0f - 0.5f);
-        break;
+        return (v + 0.5f) / (8388608.0f - 0.5f);
     }
-    case SDRGPU_CONV_I32: r = (float)((((const int32_t*)in)[i] + 0.5) / (2147483648.0 - 0.5)); break;
-    case SDRGPU_CONV_F64: r = (float)((const double*)in)[i]; break;
-    default: r = ((float)((const int8_t*)in)[i]) * (float)(1.0 / 128.0f); break;
+    case SDRGPU_CONV_I32: return (float)((((const int32_t*)in)[i] + 0.5) / (2147483648.0 - 0.5));
+    case SDRGPU_CONV_F64: return (float)((const double*)in)[i];
+    case SDRGPU_CONV_I8: return ((float)((const int8_t*)in)[i]) * (float)(1.0 / 128.0f);
+    default: return ((const float*)in)[i];   // SDRGPU_CONV_F32: IEEE float samples as they are
     }
-    out[i] = r;
+}
+__global__ void convert_kernel(int kind, const void* __restrict__ in, long long n, float* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = convert_one(kind, in, i);
+}
+// one-channel WAV (file_source worker_1ch, main.cpp:294-430): I = Q = the converted sample
+__global__ void convert_mono_kernel(int kind, const void* __restrict__ in, long long n, float2* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float v = convert_one(kind, in, i);
+    out[i] = make_float2(v, v);
 }
 
 // ================================================================ host blocks
@@ -1458,7 +1466,7 @@ extern "C" int sdrgpu_block_destroy(sdrgpu_block* h) {
 }
 
 extern "C" int sdrgpu_convert_dev(int device, int kind, const void* in, long long n, float* out, void* stream) {
-    if (kind < SDRGPU_CONV_U8 || kind > SDRGPU_CONV_I8 || n < 0 || (n > 0 && (!in || !out))) {
+    if (kind < SDRGPU_CONV_U8 || kind > SDRGPU_CONV_F32 || n < 0 || (n > 0 && (!in || !out))) {
         set_error("convert: bad argument");
         return SDRGPU_EARG;
     }
@@ -1469,9 +1477,36 @@ extern "C" int sdrgpu_convert_dev(int device, int kind, const void* in, long lon
     return (int)std::min<long long>(n, 0x7fffffff);
 }
 
+extern "C" int sdrgpu_convert_mono_dev(int device, int kind, const void* in, long long n, void* out, void* stream) {
+    if (kind < SDRGPU_CONV_U8 || kind > SDRGPU_CONV_F32 || n < 0 || (n > 0 && (!in || !out))) {
+        set_error("convert_mono: bad argument");
+        return SDRGPU_EARG;
+    }
+    SDRGPU_SET_DEVICE(device);
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(convert_mono_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, kind, in, n,
+                       (float2*)out);
+    SDRGPU_HIP(hipGetLastError());
+    return (int)std::min<long long>(n, 0x7fffffff);
+}
+
+extern "C" int sdrgpu_convert_mono(int device, int kind, const void* in, long long n, void* out) {
+    static const int isz[] = {1, 2, 3, 4, 8, 1, 4};
+    if (kind < SDRGPU_CONV_U8 || kind > SDRGPU_CONV_F32 || n < 0) { set_error("convert_mono: bad argument"); return SDRGPU_EARG; }
+    if (n == 0) return 0;
+    SDRGPU_SET_DEVICE(device);
+    DevBuf din, dout;
+    SDRGPU_CHECK(din.ensure((size_t)n * isz[kind]));
+    SDRGPU_CHECK(dout.ensure((size_t)n * sizeof(float2)));
+    SDRGPU_HIP(hipMemcpy(din.p, in, (size_t)n * isz[kind], hipMemcpyHostToDevice));
+    SDRGPU_CHECK(sdrgpu_convert_mono_dev(device, kind, din.p, n, dout.p, nullptr));
+    SDRGPU_HIP(hipMemcpy(out, dout.p, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost));
+    return (int)std::min<long long>(n, 0x7fffffff);
+}
+
 extern "C" int sdrgpu_convert(int device, int kind, const void* in, long long n, float* out) {
-    static const int isz[] = {1, 2, 3, 4, 8, 1};
-    if (kind < SDRGPU_CONV_U8 || kind > SDRGPU_CONV_I8 || n < 0) { set_error("convert: bad argument"); return SDRGPU_EARG; }
+    static const int isz[] = {1, 2, 3, 4, 8, 1, 4};
+    if (kind < SDRGPU_CONV_U8 || kind > SDRGPU_CONV_F32 || n < 0) { set_error("convert: bad argument"); return SDRGPU_EARG; }
     if (n == 0) return 0;
     SDRGPU_SET_DEVICE(device);
     void* din = nullptr;

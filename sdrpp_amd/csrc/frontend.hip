@@ -36,7 +36,7 @@ struct VfoSlot {
     PinnedBuf pin;
     int n = 0;
 };
-const int kConvSize[] = {1, 2, 3, 4, 8, 1};   // bytes per real value of SDRGPU_CONV_U8..I8
+const int kConvSize[] = {1, 2, 3, 4, 8, 1, 4};   // bytes per real value of SDRGPU_CONV_U8..F32
 }  // namespace
 
 struct sdrgpu_frontend {
@@ -290,7 +290,7 @@ static int fe_preproc(sdrgpu_frontend* f, const float2* in, int n, hipStream_t s
 // Returns the number of spectrum rows produced; rows and VFO outputs stay on the device.
 extern "C" int sdrgpu_frontend_push_dev(sdrgpu_frontend* f, const void* in, int count, int kind, void* stream) {
     NEED_FE(f);
-    if (count < 0 || (count > 0 && !in) || kind < -1 || kind > SDRGPU_CONV_I8) { set_error("frontend_push: bad argument"); return SDRGPU_EARG; }
+    if (count < 0 || (count > 0 && !in) || kind < -1 || kind > SDRGPU_CONV_F32) { set_error("frontend_push: bad argument"); return SDRGPU_EARG; }
     SDRGPU_SET_DEVICE(f->device);
     hipStream_t s = stream ? (hipStream_t)stream : f->s;
     const float2* x = (const float2*)in;
@@ -309,7 +309,7 @@ extern "C" int sdrgpu_frontend_push_dev(sdrgpu_frontend* f, const void* in, int 
 // frontend's stream; synchronises so the host can read the results.
 extern "C" int sdrgpu_frontend_push(sdrgpu_frontend* f, const void* in, int count, int kind) {
     NEED_FE(f);
-    if (count < 0 || (count > 0 && !in) || kind < -1 || kind > SDRGPU_CONV_I8) { set_error("frontend_push: bad argument"); return SDRGPU_EARG; }
+    if (count < 0 || (count > 0 && !in) || kind < -1 || kind > SDRGPU_CONV_F32) { set_error("frontend_push: bad argument"); return SDRGPU_EARG; }
     SDRGPU_SET_DEVICE(f->device);
     const size_t bytes = (size_t)count * (kind < 0 ? sizeof(float2) : 2 * kConvSize[kind]);
     if (count > 0) {

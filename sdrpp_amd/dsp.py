@@ -230,6 +230,73 @@ def convert(kind, x, device=0):
     return out
 
 
+def convert_mono(kind, x, device=0):
+    """One-channel file_source ingest (main.cpp:294-430): n samples -> complex64 with I = Q."""
+    x = np.ascontiguousarray(x)
+    n = x.size if kind != 2 else x.size // 3
+    out = np.empty(n, dtype=np.complex64)
+    check(lib.sdrgpu_convert_mono(device, int(kind), _fptr(x), n, _fptr(out)))
+    return out
+
+
+_CONV_BYTES = (1, 2, 3, 4, 8, 1, 4)
+_CONV_VIEW = (np.uint8, np.int16, np.uint8, np.int32, np.float64, np.int8, np.float32)   # (i24: packed bytes)
+
+
+class WavFile:
+    """file_source's WavReader (C++ in libsdrgpu: sdrgpu_wav_*, wavreader.h:34-226) with the
+    worker's framing: ``read()`` returns the next raw block of block_size frames (fs / 200), as
+    bytes, and ``samples(block)`` converts it on the GPU to complex64 exactly as worker_1ch /
+    worker_2ch do (main.cpp:294-560)."""
+
+    def __init__(self, path, device=0):
+        self._h = _make(lib.sdrgpu_wav_open, str(path).encode())
+        f, c, b, sr, n = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_double(), ctypes.c_longlong()
+        check(lib.sdrgpu_wav_info(self._h, ctypes.byref(f), ctypes.byref(c), ctypes.byref(b), ctypes.byref(sr),
+                                  ctypes.byref(n)))
+        self.format, self.channels, self.bits = f.value, c.value, b.value
+        self.sample_rate, self.sample_count = sr.value, n.value
+        self.device = device
+        self.kind = check(lib.sdrgpu_wav_kind(self._h))
+        self.block_size = check(lib.sdrgpu_wav_block_size(self._h))
+        self.frame_bytes = self.channels * _CONV_BYTES[self.kind]
+
+    def read(self, max_frames=None):
+        n = self.block_size if max_frames is None else int(max_frames)
+        buf = np.empty(n * self.frame_bytes, np.uint8)
+        got = check(lib.sdrgpu_wav_read(self._h, _fptr(buf), n))
+        return buf[:got * self.frame_bytes]
+
+    def samples(self, raw):
+        if raw.size == 0:
+            return np.empty(0, np.complex64)
+        typed = raw.view(_CONV_VIEW[self.kind])
+        if self.channels == 1:
+            return convert_mono(self.kind, typed, self.device)
+        return convert(self.kind, typed, self.device).view(np.complex64)
+
+    def blocks(self):
+        while True:
+            raw = self.read()
+            if raw.size == 0:
+                return
+            yield raw
+
+    def seek(self, frame):
+        check(lib.sdrgpu_wav_seek(self._h, int(frame)))
+
+    def close(self):
+        if self._h:
+            lib.sdrgpu_wav_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 # ---- host-side design functions (no GPU) ----------------------------------
 def create_window(wtype, size, centered=True):
     w = np.empty(size, dtype=np.float32)

@@ -18,6 +18,7 @@
 #include "dsp/demod/am.h"
 #include "dsp/demod/ssb.h"
 #include "dsp/loop/agc.h"
+#include "dsp/filter/deephasis.h"
 #include "sdr_oracle.h"
 
 static int failures = 0;
@@ -166,6 +167,19 @@ int main() {
         CHECK(std::memcmp(c.data(), d.data(), sizeof(float) * n) == 0, "DCBlocker->AGC not bit-exact");
         std::printf("DCBlocker<float> -> AGC<float>: bit-exact %s\n", std::memcmp(c.data(), d.data(), sizeof(float) * n) == 0 ? "yes" : "NO");
         orc_dcb_destroy(od); orc_agc_destroy(og);
+
+        // Deemphasis<float> over two blocks vs the reference recurrence (filter/deephasis.h:58-65, 91-94)
+        dsp::filter::Deemphasis<float> de(&fdummy, 50e-6, 48000.0);
+        std::vector<float> e(n), g(n);
+        de.process(n / 3, c.data(), e.data());
+        de.process(n - n / 3, c.data() + n / 3, e.data() + n / 3);
+        const double tau = 50e-6, fsr = 48000.0;
+        const float dt = 1.0f / fsr;
+        const float alpha = dt / (tau + dt);
+        float last = 0;
+        for (int i = 0; i < n; i++) { g[i] = (alpha * c[i]) + ((1 - alpha) * last); last = g[i]; }
+        CHECK(std::memcmp(e.data(), g.data(), sizeof(float) * n) == 0, "Deemphasis not bit-exact");
+        std::printf("Deemphasis<float>: bit-exact %s\n", std::memcmp(e.data(), g.data(), sizeof(float) * n) == 0 ? "yes" : "NO");
     }
     std::printf(failures ? "FAILED (%d)\n" : "ALL OK\n", failures);
     return failures ? 1 : 0;
