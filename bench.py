@@ -123,7 +123,7 @@ class C3:
         self.out = torch.empty(B // 8 + 64, dtype=torch.float32, device="cuda")
         self.bytes_per_sample = 8 + 4 / 8
         self.kernel_bytes = self.bytes_per_sample * B
-        self.kernel_name = "fir_kernel<xlator+256-tap/8+quadrature>"
+        self.kernel_name = "fir_mfma_kernel<4,XL,QUAD> (xlator + 256-tap FIR /8 on f32 MFMA + quadrature)"
 
     def dominant(self, x, s):
         self.ddc.process_dev(x.data_ptr(), self.B, self.out.data_ptr(), s)
@@ -277,9 +277,9 @@ def main():
     ev = []
     # One stream for the whole step. Forking the spectrum and the VFO chain onto two streams
     # (the reference runs them on separate block threads, iq_frontend.cpp:49,115) was
-    # measured: the step time does not change (both are HBM-bound; 2.95 vs 2.97 ms) but the
-    # spectrum kernels' event/rocprof durations stretch by the overlap, so the roofline
-    # numbers would stop describing the kernel.
+    # measured twice: the step time does not change (2.95 vs 2.97 ms; with the MFMA VFO stage
+    # 2.265 vs 2.261 ms) but the spectrum's event/rocprof durations stretch by the overlap
+    # (1.58 -> 1.89 ms), so the roofline numbers would stop describing the kernel.
     def step(timed):
         evs = []
 
