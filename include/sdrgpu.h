@@ -146,8 +146,14 @@ int sdrgpu_demod_agc_set_enabled(sdrgpu_block* h, int which, int enabled);
 int sdrgpu_demod_agc_set_attack_decay(sdrgpu_block* h, double attack, double decay);
 /* demod::BroadcastFM with the stereo decoder (broadcast_fm.h:34-60, 144-215): quadrature ->
  * pilot band-pass (complex taps) -> PLL (loop/pll.h) -> L+R / L-R matrix -> audio low-pass;
- * stereo_t out. stereo = 0 gives the mono path (= sdrgpu_wfm_create). RDS output: not provided. */
+ * stereo_t out. stereo = 0 gives the mono path (= sdrgpu_wfm_create). */
 int sdrgpu_broadcast_fm_create(sdrgpu_block** h, int device, double deviation, double samplerate, int stereo, int lowPass);
+/* RDS branch (broadcast_fm.h:121-127, 164-171, 193-203): setRDSOut; when on, every process call
+ * also produces complex_t RDS baseband = RationalResampler(fs -> 5 kHz)(FrequencyXlator(-57 kHz)(MPX)),
+ * read with rds_dev (device pointer + count of the last call) or read_rds (host copy) */
+int sdrgpu_broadcast_fm_set_rds(sdrgpu_block* h, int enabled);
+int sdrgpu_broadcast_fm_rds_dev(sdrgpu_block* h, const void** out, int* n);
+int sdrgpu_broadcast_fm_read_rds(sdrgpu_block* h, void* out, int max);
 /* filter::Deemphasis<T> (filter/deephasis.h:57-93): dtype F32 (float) or C64 (stereo_t);
  * serial recurrence, bit-identical to the reference arithmetic */
 int sdrgpu_deemphasis_create(sdrgpu_block** h, int device, int dtype, double tau, double samplerate);

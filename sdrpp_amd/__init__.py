@@ -123,6 +123,9 @@ def _load():
         "sdrgpu_convert_dev": (i, [i, i, vp, ll, vp, vp]),
         "sdrgpu_convert": (i, [i, i, vp, ll, vp]),
         "sdrgpu_convert_mono_dev": (i, [i, i, vp, ll, vp, vp]),
+        "sdrgpu_broadcast_fm_set_rds": (i, [vp, i]),
+        "sdrgpu_broadcast_fm_rds_dev": (i, [vp, pp, ctypes.POINTER(i)]),
+        "sdrgpu_broadcast_fm_read_rds": (i, [vp, vp, i]),
         "sdrgpu_convert_mono": (i, [i, i, vp, ll, vp]),
         "sdrgpu_wav_open": (i, [pp, ctypes.c_char_p]),
         "sdrgpu_wav_info": (i, [vp, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(d),

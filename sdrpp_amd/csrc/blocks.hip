@@ -1325,6 +1325,18 @@ extern "C" int sdrgpu_polyphase_resampler_create(sdrgpu_block** h, int device, i
     return wrap(h, p, p->setup(device, dtype, interp, decim, taps, ntaps));
 }
 
+// FrequencyXlator(w) -> RationalResampler<complex_t>(inSr -> outSr) with the xlator fused into the
+// first decimation stage (BroadcastFM's RDS branch, broadcast_fm.h:164-171)
+namespace sdrgpu {
+Block* make_xlate_resample_block(int dev, double inSr, double outSr, double w, int* rc) {
+    auto* c = new ChainBlock();
+    c->device = dev; c->in_dtype = c->out_dtype = SDRGPU_C64;
+    *rc = c->init_stream();
+    if (*rc >= 0) *rc = build_rational(c, dev, SDRGPU_C64, inSr, outSr, true, w);
+    return c;
+}
+}  // namespace sdrgpu
+
 extern "C" int sdrgpu_rational_resampler_create(sdrgpu_block** h, int device, int dtype, double inSr, double outSr) {
     if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
     auto* c = new ChainBlock();

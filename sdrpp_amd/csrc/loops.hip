@@ -465,9 +465,27 @@ Block* make_xlator_block(int dev, double offsetRad, int* rc);
 // BroadcastFM (demod/broadcast_fm.h:34-60, 144-215): quadrature -> [stereo: pilot band-pass
 // (complex, 305 taps at 240 kS/s) -> PLL -> matrix] -> audio low-pass -> stereo_t
 Block* make_quad_block(int dev, double deviationRad, int* rc);
+Block* make_xlate_resample_block(int dev, double inSr, double outSr, double w, int* rc);
 struct BroadcastFmBlock : Block {
     bool stereo = true, lowPass = true;
     std::unique_ptr<Block> quad, pilot, audio;
+    // RDS branch (broadcast_fm.h:164-171, 193-203): MPX as complex -> FrequencyXlator(-57 kHz) ->
+    // RationalResampler<complex_t>(fs -> 5 kHz); off unless set_rds(true) (setRDSOut)
+    bool rds = false;
+    double fs = 0.0;
+    std::unique_ptr<Block> rdsChain;
+    DevBuf rdsIn, rdsOut;
+    int rdsN = 0;
+    int set_rds(bool on) {
+        rds = on;
+        rdsN = 0;
+        if (on && !rdsChain) {
+            int rc;
+            rdsChain.reset(make_xlate_resample_block(device, fs, 5000.0, hz_to_rads(-57000.0, fs), &rc));
+            if (rc < 0) { rdsChain.reset(); rds = false; return rc; }
+        }
+        return SDRGPU_OK;
+    }
     PllParams pp{};
     float initPhase = 0.0f, initFreq = 0.0f;
     int delay = 0;
@@ -479,6 +497,7 @@ struct BroadcastFmBlock : Block {
         out_dtype = SDRGPU_C64;
         stereo = st;
         lowPass = lp;
+        fs = samplerate;
         SDRGPU_CHECK(init_stream());
         int rc;
         quad.reset(make_quad_block(dev, hz_to_rads(deviation, samplerate), &rc));
@@ -522,6 +541,7 @@ struct BroadcastFmBlock : Block {
         SDRGPU_CHECK(quad->reset());
         SDRGPU_CHECK(pilot->reset());
         SDRGPU_CHECK(audio->reset());
+        if (rdsChain) SDRGPU_CHECK(rdsChain->reset());
         const float2 st = make_float2(initPhase, initFreq);
         SDRGPU_HIP(hipMemcpy(pllState.p, &st, sizeof(st), hipMemcpyHostToDevice));
         SDRGPU_HIP(hipMemset(hist[cur].p, 0, sizeof(float) * delay));
@@ -529,6 +549,7 @@ struct BroadcastFmBlock : Block {
     }
     int run(const void* in, int count, void* out, hipStream_t s) override {
         if (count < 0) { set_error("broadcast_fm: negative count"); return SDRGPU_EARG; }
+        rdsN = 0;
         if (count == 0) return 0;
         SDRGPU_SET_DEVICE(device);
         SDRGPU_CHECK(mpx.ensure(sizeof(float) * count));
@@ -554,6 +575,21 @@ struct BroadcastFmBlock : Block {
             hipLaunchKernelGGL(mono_to_stereo_kernel, g, b, 0, s, mpx.as<float>(), lr.as<float2>(), count);
         }
         SDRGPU_HIP(hipGetLastError());
+        if (rds && rdsChain) {
+            // the undelayed MPX as complex (the stereo path already holds it in cplx)
+            const float2* c = cplx.as<float2>();
+            if (!stereo) {
+                SDRGPU_CHECK(rdsIn.ensure(sizeof(float2) * count));
+                hipLaunchKernelGGL(real_to_complex_kernel, g, b, 0, s, mpx.as<float>(), rdsIn.as<float2>(), count);
+                SDRGPU_HIP(hipGetLastError());
+                c = rdsIn.as<float2>();
+            }
+            const int want = rdsChain->out_count(count);
+            if (want < 0) return want;
+            SDRGPU_CHECK(rdsOut.ensure(sizeof(float2) * (size_t)std::max(want, 1)));
+            rdsN = rdsChain->run(c, count, rdsOut.p, s);
+            if (rdsN < 0) return rdsN;
+        }
         return audio->run(lr.p, count, out, s);
     }
 };
@@ -734,12 +770,36 @@ extern "C" int sdrgpu_dc_blocker_set_rate(sdrgpu_block* h, double rate) {
     return SDRGPU_OK;
 }
 
-// demod::BroadcastFM (broadcast_fm.h), stereo decoder included (RDS output: not provided)
+// demod::BroadcastFM (broadcast_fm.h), stereo decoder and RDS branch included
 extern "C" int sdrgpu_broadcast_fm_create(sdrgpu_block** h, int device, double deviation, double samplerate, int stereo,
                                           int lowPass) {
     if (!h || !(samplerate > 0)) { set_error("broadcast_fm_create: bad argument"); return SDRGPU_EARG; }
     auto* w = new BroadcastFmBlock();
     return wrap_block(h, w, w->setup(device, deviation, samplerate, stereo != 0, lowPass != 0));
+}
+extern "C" int sdrgpu_broadcast_fm_set_rds(sdrgpu_block* h, int enabled) {   // setRDSOut (broadcast_fm.h:121-127)
+    auto* w = h ? dynamic_cast<BroadcastFmBlock*>(h->impl) : nullptr;
+    if (!w) { set_error("not a broadcast_fm block"); return SDRGPU_EARG; }
+    SDRGPU_SET_DEVICE(w->device);
+    return w->set_rds(enabled != 0);
+}
+// RDS samples (complex_t at 5 kS/s) of the last process call: device pointer and count
+extern "C" int sdrgpu_broadcast_fm_rds_dev(sdrgpu_block* h, const void** out, int* n) {
+    auto* w = h ? dynamic_cast<BroadcastFmBlock*>(h->impl) : nullptr;
+    if (!w) { set_error("not a broadcast_fm block"); return SDRGPU_EARG; }
+    if (out) *out = w->rdsOut.p;
+    if (n) *n = w->rds ? w->rdsN : 0;
+    return w->rds ? w->rdsN : 0;
+}
+extern "C" int sdrgpu_broadcast_fm_read_rds(sdrgpu_block* h, void* out, int max) {   // host copy (waits for the block)
+    auto* w = h ? dynamic_cast<BroadcastFmBlock*>(h->impl) : nullptr;
+    if (!w || (!out && max > 0)) { set_error("broadcast_fm_read_rds: bad argument"); return SDRGPU_EARG; }
+    const int n = std::min(max, w->rds ? w->rdsN : 0);
+    if (n <= 0) return 0;
+    SDRGPU_SET_DEVICE(w->device);
+    SDRGPU_HIP(hipDeviceSynchronize());
+    SDRGPU_HIP(hipMemcpy(out, w->rdsOut.p, sizeof(float2) * (size_t)n, hipMemcpyDeviceToHost));
+    return n;
 }
 
 // filter::Deemphasis<T> (deephasis.h): dtype F32 (float) or C64 (stereo_t)

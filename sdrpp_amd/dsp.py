@@ -176,12 +176,28 @@ class BroadcastFM(Block):
     """dsp::demod::BroadcastFM (demod/broadcast_fm.h:144-215); stereo_t out. stereo=False is
     the mono path (the C5 bench chain); stereo=True adds the pilot PLL stereo decoder."""
 
-    def __init__(self, deviation, samplerate, low_pass=True, device=0, stereo=False):
-        if stereo:
-            h = _make(lib.sdrgpu_broadcast_fm_create, device, float(deviation), float(samplerate), 1, int(low_pass))
+    def __init__(self, deviation, samplerate, low_pass=True, device=0, stereo=False, rds=False):
+        if stereo or rds:   # the RDS branch lives in the full BroadcastFM block (mono or stereo)
+            h = _make(lib.sdrgpu_broadcast_fm_create, device, float(deviation), float(samplerate), int(stereo),
+                      int(low_pass))
         else:
             h = _make(lib.sdrgpu_wfm_create, device, float(deviation), float(samplerate), int(low_pass))
         super().__init__(h, np.complex64, STEREO)
+        if rds:
+            self.set_rds(True)
+
+    def set_rds(self, enabled):
+        """setRDSOut (broadcast_fm.h:121-127)."""
+        check(lib.sdrgpu_broadcast_fm_set_rds(self._h, int(bool(enabled))))
+
+    def rds_output(self):
+        """RDS baseband (complex64, 5 kS/s) produced by the last process() call."""
+        n = ctypes.c_int()
+        check(lib.sdrgpu_broadcast_fm_rds_dev(self._h, None, ctypes.byref(n)))
+        out = np.empty(n.value, np.complex64)
+        if n.value:
+            check(lib.sdrgpu_broadcast_fm_read_rds(self._h, _fptr(out), n.value))
+        return out
 
 
 class FFTSpectrum:

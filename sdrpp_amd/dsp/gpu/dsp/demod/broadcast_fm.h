@@ -1,9 +1,11 @@
 // GPU-backed dsp::demod::BroadcastFM -- drop-in for core/src/dsp/demod/broadcast_fm.h:
 //  stereo: quadrature -> pilot band-pass -> PLL -> L+R / L-R matrix -> audio low-pass
 //          (broadcast_fm.h:144-191, sdrgpu_broadcast_fm_create);
-//  mono:   quadrature -> 15 kHz low-pass -> LRToStereo (:193-211, sdrgpu_wfm_create).
-// The RDS branch feeds the RDS decoder module (out of scope): rdsOut = true reports an error
-// and produces no RDS samples; the audio path is unaffected.
+//  mono:   quadrature -> 15 kHz low-pass -> LRToStereo (:193-211, sdrgpu_wfm_create);
+//  RDS:    MPX -> FrequencyXlator(-57 kHz) -> RationalResampler(fs -> 5 kHz) into rdsOut
+//          (:164-171, 193-203; sdrgpu_broadcast_fm_set_rds / _read_rds).
+// As in the reference, the constructor does not pass rdsOut on to init() (:23): use init() or
+// setRDSOut() to enable the RDS branch.
 #pragma once
 #include "../processor.h"
 #include "../sdrgpu_handle.h"
@@ -15,7 +17,7 @@ public:
     BroadcastFM() {}
     BroadcastFM(stream<complex_t>* in, double deviation, double samplerate, bool stereo = true, bool lowPass = true,
                 bool rdsOut = false) {
-        init(in, deviation, samplerate, stereo, lowPass, rdsOut);
+        init(in, deviation, samplerate, stereo, lowPass);   // (reference: rdsOut is dropped here)
     }
     virtual void init(stream<complex_t>* in, double deviation, double samplerate, bool stereo = true, bool lowPass = true,
                       bool rdsOut = false) {
@@ -44,15 +46,22 @@ public:
     }
     inline int process(int count, complex_t* in, stereo_t* out, int& rdsOutCount, complex_t* rdsout = nullptr) {
         rdsOutCount = 0;
-        return _h.process(in, count, out, "wfm");
+        const int n = _h.process(in, count, out, "wfm");
+        if (n >= 0 && _rdsOut && rdsout) {
+            const int r = sdrgpu_broadcast_fm_read_rds(_h.h, rdsout, STREAM_BUFFER_SIZE);
+            if (!gpu::ok(r, "broadcast_fm_read_rds")) return -1;
+            rdsOutCount = r;
+        }
+        return n;
     }
     int run() override {
         int count = base_type::_in->read();
         if (count < 0) return -1;
         int rds = 0;
-        int n = process(count, base_type::_in->readBuf, base_type::out.writeBuf, rds);
+        int n = process(count, base_type::_in->readBuf, base_type::out.writeBuf, rds, rdsOut.writeBuf);
         base_type::_in->flush();
         if (n < 0 || !base_type::out.swap(count)) return -1;
+        if (rds && _rdsOut && !rdsOut.swap(rds)) return -1;
         return count;
     }
     stream<complex_t> rdsOut;
@@ -66,10 +75,13 @@ protected:
         base_type::tempStart();
     }
     void rebuild() {
-        if (_rdsOut) std::fprintf(stderr, "[sdrgpu] BroadcastFM: RDS output is not provided by the GPU path\n");
         sdrgpu_block* h = nullptr;
-        if (_stereo) gpu::ok(sdrgpu_broadcast_fm_create(&h, gpu::device(), _deviation, _samplerate, 1, _lowPass), "broadcast_fm_create");
-        else gpu::ok(sdrgpu_wfm_create(&h, gpu::device(), _deviation, _samplerate, _lowPass), "wfm_create");
+        if (_stereo || _rdsOut) {
+            gpu::ok(sdrgpu_broadcast_fm_create(&h, gpu::device(), _deviation, _samplerate, _stereo, _lowPass), "broadcast_fm_create");
+            if (h && _rdsOut) gpu::ok(sdrgpu_broadcast_fm_set_rds(h, 1), "broadcast_fm_set_rds");
+        } else {
+            gpu::ok(sdrgpu_wfm_create(&h, gpu::device(), _deviation, _samplerate, _lowPass), "wfm_create");
+        }
         _h.reset(h);
     }
     double _deviation = 0, _samplerate = 0;

@@ -168,6 +168,20 @@ int main() {
         std::printf("DCBlocker<float> -> AGC<float>: bit-exact %s\n", std::memcmp(c.data(), d.data(), sizeof(float) * n) == 0 ? "yes" : "NO");
         orc_dcb_destroy(od); orc_agc_destroy(og);
 
+        // BroadcastFM with the RDS branch (init(..., rdsOut = true)): 5 kS/s complex baseband per block
+        {
+            dsp::demod::BroadcastFM bfm;
+            bfm.init(&dummy, 100000, 240000, true, true, true);
+            std::vector<dsp::stereo_t> aud(n);
+            std::vector<dsp::complex_t> rds(n);
+            int rdsCount = -1;
+            const int a1 = bfm.process(n, ifx.data(), aud.data(), rdsCount, rds.data());
+            double e = 0;
+            for (int i = 0; i < rdsCount; i++) e += (double)rds[i].re * rds[i].re + (double)rds[i].im * rds[i].im;
+            CHECK(a1 == n && std::abs(rdsCount - (int)((long long)n * 5000 / 240000)) <= 2 && e > 0, "BroadcastFM RDS: audio %d rds %d", a1, rdsCount);
+            std::printf("BroadcastFM stereo + RDS: %d audio, %d RDS samples\n", a1, rdsCount);
+        }
+
         // Deemphasis<float> over two blocks vs the reference recurrence (filter/deephasis.h:58-65, 91-94)
         dsp::filter::Deemphasis<float> de(&fdummy, 50e-6, 48000.0);
         std::vector<float> e(n), g(n);

@@ -259,6 +259,38 @@ def test_wfm_mono_vs_oracle(rng):
         np.testing.assert_array_equal(yg["l"], yg["r"])
 
 
+@pytest.mark.parametrize("stereo", [False, True])
+def test_broadcast_fm_rds_branch(stereo):
+    """BroadcastFM's RDS output (broadcast_fm.h:164-171, 193-203): MPX -> FrequencyXlator(-57 kHz)
+    -> RationalResampler(240 k -> 5 k), over ragged blocks, vs the oracle's quadrature, xlator and
+    rational resampler on the same input; the audio path is unchanged by the branch."""
+    fs = 240000.0
+    n = 60000
+    t = np.arange(n) / fs
+    bits = np.sign(np.sin(2 * np.pi * 1187.5 * t + 0.3))
+    mpx = 0.45 * np.sin(2 * np.pi * 1000 * t) + 0.1 * np.sin(2 * np.pi * 19000 * t) + 0.05 * bits * np.cos(2 * np.pi * 57000 * t)
+    x = np.exp(1j * 2 * np.pi * 75000 / fs * np.cumsum(mpx)).astype(np.complex64)
+    g = dsp.BroadcastFM(100000, fs, True, stereo=stereo, rds=True)
+    plain = dsp.BroadcastFM(100000, fs, True, stereo=stereo, rds=False) if stereo else None
+    got, audio = [], []
+    for a, b in [(0, 7001), (7001, 7002), (7002, 33333), (33333, n)]:
+        audio.append(g.process(x[a:b]))
+        got.append(g.rds_output())
+        if plain is not None:
+            np.testing.assert_array_equal(audio[-1].view(np.float32), plain.process(x[a:b]).view(np.float32))
+    got = np.concatenate(got)
+    mp = oracle.Quadrature(2 * np.pi * 100000 / fs).process(x)
+    ref = oracle.RationalResampler(fs, 5000.0, True).process(oracle.Xlator(2 * np.pi * -57000 / fs).process(mp.astype(np.complex64)))
+    assert len(got) == len(ref) > 1000
+    # cascade bar (DESIGN.md, FIR / resamplers): 5e-5 of the input scale, here the MPX peak; the
+    # quadrature's atan2f last bits (device vs host libm) and the NCO enter the same way
+    err = np.abs(got - ref).max()
+    assert err <= 5e-5 * np.abs(mp).max(), (err, np.abs(mp).max())
+    g.set_rds(False)
+    g.process(x[:1000])
+    assert g.rds_output().size == 0
+
+
 def test_fm_nfm_vs_oracle(rng):
     for lp, hp in [(True, False), (False, True), (True, True), (False, False)]:
         g = dsp.FM(48000, 12500, lp, hp)
