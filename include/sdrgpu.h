@@ -211,6 +211,19 @@ int sdrgpu_compress_dev(int device, int pcmType, const float* in, int count, uns
  * 8-byte header, payload = device bytes after it; returns complex samples written */
 int sdrgpu_decompress_dev(int device, const unsigned char* hdr, const unsigned char* payload, int nbytes, float* out, void* stream);
 
+/* WaterFall::pushFFT consumers (gui/widgets/waterfall.cpp), device buffers, bit-exact:
+ *  colormap: zoomed dB -> waterfall pixels, pallet[(int)(((clamp(v) - min) / (max - min)) * (res - 1))] (:903-910);
+ *  fft_smooth_hold: per column over nrows rows in order, smoothing (smooth = row*alpha + smooth*beta,
+ *    row <- smooth; :918-925) then hold (hold[i] = max(row[i], hold[i] - speed), i >= 1; :952-957);
+ *  vfo_signal_info: calculateVFOSignalInfo per raw row -> strength (in-band max) and snr (max minus
+ *    side-band mean) (:563-601) */
+int sdrgpu_colormap_dev(int device, const float* in, long long n, float wfMin, float wfMax, const unsigned* pallet, int res,
+                        unsigned* out, void* stream);
+int sdrgpu_fft_smooth_hold_dev(int device, float* rows, int nrows, int width, int smoothing, float alpha, float beta,
+                               float* smooth, int holdOn, float holdSpeed, float* hold, void* stream);
+int sdrgpu_vfo_signal_info_dev(int device, const float* rows, int nrows, int fftSize, double wholeBandwidth,
+                               double centerOffset, double bandwidth, float* strength, float* snr, void* stream);
+
 /* recorder WAV encoders (utils/wav.cpp:296-336) of n device floats: kind 0 u8, 1 i16, 2 i24
  * (packed LE), 3 i32, 4 f32; returns bytes written */
 int sdrgpu_wav_encode_dev(int device, int kind, const float* in, long long n, unsigned char* out, void* stream);

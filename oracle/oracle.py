@@ -101,6 +101,9 @@ def _load():
         "orc_deemp_process": (i, [vp, vp, i, vp]),
         "orc_deemp_destroy": (None, [vp]),
         "orc_zoom": (i, [vp, i, d, d, d, i, vp]),
+        "orc_colormap": (None, [vp, ctypes.c_long, ctypes.c_float, ctypes.c_float, vp, i, vp]),
+        "orc_fft_smooth_hold": (None, [vp, i, i, i, ctypes.c_float, ctypes.c_float, vp, i, ctypes.c_float, vp]),
+        "orc_vfo_signal_info": (None, [vp, i, d, d, d, vp, vp]),
         "orc_ddcfm_create": (vp, [d, vp, i, i, d, i]),
         "orc_ddcfm_process": (i, [vp, vp, i, vp]),
         "orc_ddcfm_destroy": (None, [vp]),
@@ -400,6 +403,34 @@ def zoom(row, view_offset, view_bw, whole_bw, out_size):
     out = np.empty(out_size, np.float32)
     lib.orc_zoom(_p(row), len(row), float(view_offset), float(view_bw), float(whole_bw), int(out_size), _p(out))
     return out
+
+
+def colormap(x, wf_min, wf_max, pallet):
+    """waterfall.cpp:903-910: dB -> pallet entries."""
+    x = np.ascontiguousarray(x, np.float32)
+    pallet = np.ascontiguousarray(pallet, np.uint32)
+    out = np.empty(x.shape, np.uint32)
+    lib.orc_colormap(_p(x), x.size, float(wf_min), float(wf_max), _p(pallet), len(pallet), _p(out))
+    return out
+
+
+def fft_smooth_hold(rows, smoothing, alpha, beta, smooth, hold_on, hold_speed, hold):
+    """waterfall.cpp:918-925, 952-957 over consecutive rows; returns (rows, smooth, hold) updated."""
+    rows = np.array(rows, np.float32, copy=True, order="C")
+    smooth = np.array(smooth, np.float32, copy=True)
+    hold = np.array(hold, np.float32, copy=True)
+    lib.orc_fft_smooth_hold(_p(rows), rows.shape[0], rows.shape[1], int(smoothing), float(alpha), float(beta), _p(smooth),
+                            int(hold_on), float(hold_speed), _p(hold))
+    return rows, smooth, hold
+
+
+def vfo_signal_info(line, whole_bw, center_offset, bandwidth):
+    """WaterFall::calculateVFOSignalInfo (waterfall.cpp:563-601) -> (strength, snr)."""
+    line = np.ascontiguousarray(line, np.float32)
+    st, sn = ctypes.c_float(), ctypes.c_float()
+    lib.orc_vfo_signal_info(_p(line), len(line), float(whole_bw), float(center_offset), float(bandwidth),
+                            ctypes.byref(st), ctypes.byref(sn))
+    return st.value, sn.value
 
 
 def compress(pcm_type, x):

@@ -1082,6 +1082,64 @@ int orc_zoom(const float* data, int fftSize, double viewOffset, double viewBandw
     return outSize;
 }
 
+/* ------------------------------------------- WaterFall::pushFFT consumers */
+/* colormap of zoomed rows into the waterfall framebuffer (gui/widgets/waterfall.cpp:903-910) */
+void orc_colormap(const float* in, long n, float wfMin, float wfMax, const unsigned* pallet, int res, unsigned* out) {
+    const float dataRange = wfMax - wfMin;
+    for (long j = 0; j < n; j++) {
+        float v = in[j];
+        v = v < wfMin ? wfMin : (wfMax < v ? wfMax : v);   /* std::clamp<float> */
+        const float pixel = (v - wfMin) / dataRange;
+        const int id = (int)(pixel * (res - 1));
+        out[j] = pallet[id];
+    }
+}
+
+/* FFT smoothing then FFT hold on consecutive zoomed rows (waterfall.cpp:918-925, 952-957):
+ * row <- smooth = row*alpha + smooth*beta (three volk roundings); hold[i] = max(row[i], hold[i]-speed), i >= 1 */
+void orc_fft_smooth_hold(float* rows, int nrows, int width, int smoothing, float alpha, float beta, float* smooth,
+                         int holdOn, float holdSpeed, float* hold) {
+    for (int r = 0; r < nrows; r++) {
+        float* latest = rows + (long)r * width;
+        if (smoothing) {
+            for (int i = 0; i < width; i++) {
+                const float a = latest[i] * alpha;
+                const float b = smooth[i] * beta;
+                smooth[i] = b + a;
+                latest[i] = smooth[i];
+            }
+        }
+        if (holdOn) {
+            for (int i = 1; i < width; i++) {
+                const float h = hold[i] - holdSpeed;
+                hold[i] = (latest[i] < h) ? h : latest[i];   /* std::max<float>(latest, hold - speed) */
+            }
+        }
+    }
+}
+
+/* WaterFall::calculateVFOSignalInfo (waterfall.cpp:563-601) on one raw dB row. The reference's max
+ * loop runs to i <= vfoMaxOffset, which reads one past the row when vfoMaxOffset == fftSize; here that
+ * bin is skipped (a conscious fix: it cannot change the result of a correct read). */
+void orc_vfo_signal_info(const float* line, int fftSize, double wholeBandwidth, double centerOffset, double bandwidth,
+                         float* strength, float* snr) {
+    const double minSide = centerOffset - bandwidth, minF = centerOffset - (bandwidth / 2.0);
+    const double maxF = centerOffset + (bandwidth / 2.0), maxSide = centerOffset + bandwidth;
+#define OFS(f) ({ double v_ = (((f) / (wholeBandwidth / 2.0)) * (double)(fftSize / 2)) + (fftSize / 2); int i_ = (int)v_; \
+                  i_ < 0 ? 0 : (i_ > fftSize ? fftSize : i_); })
+    const int a0 = OFS(minSide), a1 = OFS(minF), b0 = OFS(maxF), b1 = OFS(maxSide);
+#undef OFS
+    double avg = 0;
+    int cnt = 0;
+    for (int i = a0; i < a1; i++) { avg += line[i]; cnt++; }
+    for (int i = b0 + 1; i < b1; i++) { avg += line[i]; cnt++; }
+    avg /= (double)cnt;
+    float mx = -INFINITY;
+    for (int i = a1; i <= b0 && i < fftSize; i++) if (line[i] > mx) mx = line[i];
+    *strength = mx;
+    *snr = mx - avg;
+}
+
 /* ----------------------------------------------------- C3 chain (CPU baseline) */
 /* FrequencyXlator -> DecimatingFIR<complex_t, float> -> Quadrature, one block at a time
  * (the three reference blocks back to back; precise = 0: VOLK-style fp32 rotator and dots) */

@@ -163,6 +163,13 @@ void orc_deemp_destroy(orc_deemp* d);
 int orc_zoom(const float* data, int fftSize, double viewOffset, double viewBandwidth, double wholeBandwidth,
              int outSize, float* out);
 
+/* WaterFall::pushFFT consumers (gui/widgets/waterfall.cpp) */
+void orc_colormap(const float* in, long n, float wfMin, float wfMax, const unsigned* pallet, int res, unsigned* out);
+void orc_fft_smooth_hold(float* rows, int nrows, int width, int smoothing, float alpha, float beta, float* smooth,
+                         int holdOn, float holdSpeed, float* hold);
+void orc_vfo_signal_info(const float* line, int fftSize, double wholeBandwidth, double centerOffset, double bandwidth,
+                         float* strength, float* snr);
+
 typedef struct orc_ddcfm orc_ddcfm;          /* C3: xlator -> DecimatingFIR -> Quadrature */
 orc_ddcfm* orc_ddcfm_create(double offsetRad, const float* taps, int ntaps, int decim, double deviationRad, int precise);
 int  orc_ddcfm_process(orc_ddcfm* d, const float* in, int count, float* out);

@@ -124,6 +124,9 @@ def _load():
         "sdrgpu_convert": (i, [i, i, vp, ll, vp]),
         "sdrgpu_convert_mono_dev": (i, [i, i, vp, ll, vp, vp]),
         "sdrgpu_broadcast_fm_set_rds": (i, [vp, i]),
+        "sdrgpu_colormap_dev": (i, [i, vp, ll, ctypes.c_float, ctypes.c_float, vp, i, vp, vp]),
+        "sdrgpu_fft_smooth_hold_dev": (i, [i, vp, i, i, i, ctypes.c_float, ctypes.c_float, vp, i, ctypes.c_float, vp, vp]),
+        "sdrgpu_vfo_signal_info_dev": (i, [i, vp, i, i, d, d, d, vp, vp, vp]),
         "sdrgpu_broadcast_fm_rds_dev": (i, [vp, pp, ctypes.POINTER(i)]),
         "sdrgpu_broadcast_fm_read_rds": (i, [vp, vp, i]),
         "sdrgpu_convert_mono": (i, [i, i, vp, ll, vp]),

@@ -30,6 +30,75 @@ __global__ void zoom_kernel(const float* __restrict__ rows, int fftSize, int nro
     out[(size_t)r * outSize + o] = m;
 }
 
+// ----------------------------------------------- WaterFall::pushFFT consumers
+// colormap (waterfall.cpp:903-910): one pixel per thread, IEEE division, no contraction
+__global__ void colormap_kernel(const float* __restrict__ in, long long n, float wfMin, float wfMax,
+                                const unsigned* __restrict__ pallet, int res, unsigned* __restrict__ out) {
+    const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const float dataRange = wfMax - wfMin;
+    float v = in[j];
+    v = v < wfMin ? wfMin : (wfMax < v ? wfMax : v);   // std::clamp<float>
+    const float pixel = (v - wfMin) / dataRange;
+    out[j] = pallet[(int)(pixel * (res - 1))];
+}
+
+// FFT smoothing + hold (waterfall.cpp:918-925, 952-957): one column per thread, rows in order
+__global__ void smooth_hold_kernel(float* __restrict__ rows, int nrows, int width, int smoothing, float alpha, float beta,
+                                   float* __restrict__ smooth, int holdOn, float holdSpeed, float* __restrict__ hold) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= width) return;
+    float sm = smoothing ? smooth[i] : 0.0f;
+    float h = holdOn ? hold[i] : 0.0f;
+    for (int r = 0; r < nrows; r++) {
+        float v = rows[(size_t)r * width + i];
+        if (smoothing) {
+            const float a = v * alpha;   // volk_32f_s32f_multiply_32f (latest)
+            const float b = sm * beta;   // volk_32f_s32f_multiply_32f (smoothingBuf)
+            sm = b + a;                  // volk_32f_x2_add_32f(smoothingBuf, latest, smoothingBuf)
+            v = sm;
+            rows[(size_t)r * width + i] = v;
+        }
+        if (holdOn && i >= 1) {
+            const float hs = h - holdSpeed;
+            h = (v < hs) ? hs : v;       // std::max<float>(latestFFT[i], latestFFTHold[i] - fftHoldSpeed)
+        }
+    }
+    if (smoothing) smooth[i] = sm;
+    if (holdOn) hold[i] = h;
+}
+
+// WaterFall::calculateVFOSignalInfo (waterfall.cpp:563-601): one workgroup per raw dB row; the
+// side-band mean is a double sum (exact, so order-free, while it fits 53 bits) and the in-band max
+__global__ void vfo_info_kernel(const float* __restrict__ rows, int fftSize, int a0, int a1, int b0, int b1,
+                                float* __restrict__ strength, float* __restrict__ snr) {
+    __shared__ double ssum[256];
+    __shared__ float smax[256];
+    const float* line = rows + (size_t)blockIdx.x * fftSize;
+    const int tid = threadIdx.x;
+    double acc = 0.0;
+    float mx = -INFINITY;
+    for (int i = a0 + tid; i < a1; i += 256) acc += line[i];
+    for (int i = b0 + 1 + tid; i < b1; i += 256) acc += line[i];
+    for (int i = a1 + tid; i <= b0 && i < fftSize; i += 256) mx = line[i] > mx ? line[i] : mx;
+    ssum[tid] = acc;
+    smax[tid] = mx;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) {
+            ssum[tid] += ssum[tid + o];
+            smax[tid] = smax[tid + o] > smax[tid] ? smax[tid + o] : smax[tid];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const int cnt = (a1 > a0 ? a1 - a0 : 0) + (b1 > b0 + 1 ? b1 - b0 - 1 : 0);
+        const double avg = ssum[0] / (double)cnt;
+        strength[blockIdx.x] = smax[0];
+        snr[blockIdx.x] = smax[0] - avg;
+    }
+}
+
 // ---------------------------------------------------------------- codec
 __global__ void signed_max_kernel(const float* __restrict__ x, long long n, unsigned* __restrict__ bits) {
     // max over floats as an order-preserving unsigned key (exact; NaN-free input)
@@ -176,6 +245,52 @@ extern "C" int sdrgpu_zoom_execute_dev(sdrgpu_zoom* z, const float* rows, int nr
 extern "C" int sdrgpu_zoom_destroy(sdrgpu_zoom* z) {
     delete z;
     return SDRGPU_OK;
+}
+
+extern "C" int sdrgpu_colormap_dev(int device, const float* in, long long n, float wfMin, float wfMax, const unsigned* pallet,
+                                   int res, unsigned* out, void* stream) {
+    if (n < 0 || (n > 0 && (!in || !pallet || !out)) || res < 1) { set_error("colormap: bad argument"); return SDRGPU_EARG; }
+    SDRGPU_SET_DEVICE(device);
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(colormap_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, in, n, wfMin, wfMax,
+                       pallet, res, out);
+    SDRGPU_HIP(hipGetLastError());
+    return (int)std::min<long long>(n, 0x7fffffff);
+}
+
+extern "C" int sdrgpu_fft_smooth_hold_dev(int device, float* rows, int nrows, int width, int smoothing, float alpha, float beta,
+                                          float* smooth, int holdOn, float holdSpeed, float* hold, void* stream) {
+    if (nrows < 0 || width < 1 || (nrows > 0 && !rows) || (smoothing && !smooth) || (holdOn && !hold)) {
+        set_error("fft_smooth_hold: bad argument");
+        return SDRGPU_EARG;
+    }
+    SDRGPU_SET_DEVICE(device);
+    if (nrows == 0) return 0;
+    hipLaunchKernelGGL(smooth_hold_kernel, dim3((width + 255) / 256), dim3(256), 0, (hipStream_t)stream, rows, nrows, width,
+                       smoothing, alpha, beta, smooth, holdOn, holdSpeed, hold);
+    SDRGPU_HIP(hipGetLastError());
+    return nrows;
+}
+
+extern "C" int sdrgpu_vfo_signal_info_dev(int device, const float* rows, int nrows, int fftSize, double wholeBandwidth,
+                                          double centerOffset, double bandwidth, float* strength, float* snr, void* stream) {
+    if (nrows < 0 || fftSize < 2 || !(wholeBandwidth > 0) || (nrows > 0 && (!rows || !strength || !snr))) {
+        set_error("vfo_signal_info: bad argument");
+        return SDRGPU_EARG;
+    }
+    SDRGPU_SET_DEVICE(device);
+    if (nrows == 0) return 0;
+    // the reference's bin offsets, in its double arithmetic (waterfall.cpp:567-574)
+    auto ofs = [&](double f) {
+        const int i = (int)(((f / (wholeBandwidth / 2.0)) * (double)(fftSize / 2)) + (fftSize / 2));
+        return std::clamp<int>(i, 0, fftSize);
+    };
+    const int a0 = ofs(centerOffset - bandwidth), a1 = ofs(centerOffset - (bandwidth / 2.0));
+    const int b0 = ofs(centerOffset + (bandwidth / 2.0)), b1 = ofs(centerOffset + bandwidth);
+    hipLaunchKernelGGL(vfo_info_kernel, dim3(nrows), dim3(256), 0, (hipStream_t)stream, rows, fftSize, a0, a1, b0, b1,
+                       strength, snr);
+    SDRGPU_HIP(hipGetLastError());
+    return nrows;
 }
 
 // SampleStreamCompressor::process on a device block of `count` complex samples. pcmType:

@@ -92,3 +92,68 @@ def test_wav_encoders_bit_exact(kind, rng):
     torch.cuda.synchronize()
     assert n == len(ref)
     assert np.array_equal(d_o.cpu().numpy()[:n], ref)
+
+
+# ------------------------------------------------ WaterFall::pushFFT consumers (§8f rank 3)
+def _vp(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def test_waterfall_colormap_bit_exact(rng):
+    """waterfall.cpp:903-910 on zoomed rows: clamped to [min, max], pallet index by truncation;
+    values on, inside and outside the range, with the reference's 1e6-entry pallet size."""
+    res = 1000000
+    pallet = rng.integers(0, 2 ** 32, size=res, dtype=np.uint32)
+    x = rng.uniform(-160, 20, 300 * 1024).astype(np.float32)
+    x[:8] = [-150.0, 0.0, -150.0000001, 1e30, -1e30, -75.0, -0.0, 5.0]
+    wf_min, wf_max = np.float32(-150.0), np.float32(0.0)
+    d_x, d_p = torch.from_numpy(x).cuda(), torch.from_numpy(pallet.view(np.int32)).cuda()
+    d_o = torch.empty(x.size, dtype=torch.int32, device="cuda")
+    sdrpp_amd.check(sdrpp_amd.lib.sdrgpu_colormap_dev(0, _vp(d_x), x.size, float(wf_min), float(wf_max), _vp(d_p), res,
+                                                      _vp(d_o), None))
+    torch.cuda.synchronize()
+    assert np.array_equal(d_o.cpu().numpy().view(np.uint32), oracle.colormap(x, wf_min, wf_max, pallet))
+
+
+@pytest.mark.parametrize("smoothing,hold_on", [(True, True), (True, False), (False, True)])
+def test_waterfall_smoothing_and_hold_bit_exact(smoothing, hold_on, rng):
+    """waterfall.cpp:918-925, 952-957: per-column IIR smoothing across rows and FFT hold (from
+    column 1), state carried across calls (two batches of rows)."""
+    w = 2000
+    alpha, beta, speed = np.float32(0.3), np.float32(0.7), np.float32(0.25)
+    smooth0 = rng.uniform(-100, 0, w).astype(np.float32)
+    hold0 = rng.uniform(-100, 0, w).astype(np.float32)
+    rows = rng.uniform(-120, 10, (37, w)).astype(np.float32)
+    ref_rows, ref_s, ref_h = oracle.fft_smooth_hold(rows, smoothing, alpha, beta, smooth0, hold_on, speed, hold0)
+    d_rows = torch.from_numpy(rows.copy()).cuda()
+    d_s, d_h = torch.from_numpy(smooth0.copy()).cuda(), torch.from_numpy(hold0.copy()).cuda()
+    for a, b in [(0, 10), (10, 37)]:
+        sdrpp_amd.check(sdrpp_amd.lib.sdrgpu_fft_smooth_hold_dev(
+            0, ctypes.c_void_p(d_rows.data_ptr() + 4 * a * w), b - a, w, int(smoothing), float(alpha), float(beta), _vp(d_s),
+            int(hold_on), float(speed), _vp(d_h), None))
+    torch.cuda.synchronize()
+    assert np.array_equal(_bits(d_rows.cpu().numpy()), _bits(ref_rows))
+    if smoothing:
+        assert np.array_equal(_bits(d_s.cpu().numpy()), _bits(ref_s))
+    if hold_on:
+        assert np.array_equal(_bits(d_h.cpu().numpy()), _bits(ref_h))
+
+
+@pytest.mark.parametrize("vfo", [(100e3, 50e3), (-1.1e6, 200e3), (1.19e6, 40e3), (0.0, 1e3), (0.0, 2.4e6)])
+def test_vfo_signal_info_matches_reference(vfo, rng):
+    """WaterFall::calculateVFOSignalInfo (waterfall.cpp:563-601) per raw row: in-band max and SNR
+    against the side-band mean, including VFOs at the band edge (clamped offsets) and a bandwidth
+    with no side bins (mean 0/0 = NaN, as in the reference)."""
+    fft, whole = 8192, 2.4e6
+    rows = rng.uniform(-130, -20, (9, fft)).astype(np.float32)
+    d_rows = torch.from_numpy(rows).cuda()
+    d_st = torch.empty(9, device="cuda")
+    d_sn = torch.empty(9, device="cuda")
+    sdrpp_amd.check(sdrpp_amd.lib.sdrgpu_vfo_signal_info_dev(0, _vp(d_rows), 9, fft, whole, vfo[0], vfo[1], _vp(d_st),
+                                                             _vp(d_sn), None))
+    torch.cuda.synchronize()
+    st, sn = d_st.cpu().numpy(), d_sn.cpu().numpy()
+    for r in range(9):
+        rs, rn = oracle.vfo_signal_info(rows[r], whole, vfo[0], vfo[1])
+        assert np.array_equal(_bits(np.float32(st[r])), _bits(np.float32(rs)))
+        assert (np.isnan(sn[r]) and np.isnan(rn)) or np.float32(sn[r]) == np.float32(rn), (r, sn[r], rn)
