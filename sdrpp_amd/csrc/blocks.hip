@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <memory>
 #include <numeric>
+#include <type_traits>
 #include "sdrgpu_internal.h"
 
 namespace sdrgpu {
@@ -458,6 +459,100 @@ __global__ __launch_bounds__(256) void fir_mfma_ps_kernel(FirArgs a) {
     }
 }
 
+// Row-streaming decimating FIR for D = 32 (VFO stage 1: 143 taps -> QP = 5 taps per phase), no
+// LDS. Lane p of each 32-lane half owns phase p. A half-wave walks a segment of RS outputs row by
+// row: row r is the 32 samples buf[b0 + 32 r .. + 31], one 256-B coalesced load per half. The
+// lane keeps the QP - 1 open partial sums of its phase in registers (output o takes row o + q
+// with tap h[32 q + p]), so every row costs QP complex x real FMAs and closes one per-phase
+// partial. Every 32 closed outputs the 32 per-phase partials are summed across the half by a
+// five-step xor transpose-reduce (ds_swizzle), which leaves output 32 blk + p in lane p.
+// Each sample is read once (plus QP - 1 halo rows per segment).
+constexpr int ROWS_RS = 128;   // outputs per half-wave segment
+constexpr int ROWS_STEP = 256;  // e^{i w 32 u} table length (>= ROWS_RS + QP - 1)
+template <int QP, bool XL>
+__global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
+    const int lane = threadIdx.x & 63, p = lane & 31, hf = lane >> 5;
+    const long long seg = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + hf;
+    const long long mseg = seg * ROWS_RS;
+    if (mseg >= a.M) return;   // (the cross-lane steps stay inside one 32-lane half)
+    const float* __restrict__ taps = reinterpret_cast<const float*>(a.taps);   // [p][Q]
+    float h[QP];
+#pragma unroll
+    for (int q = 0; q < QP; q++) h[q] = taps[p * a.Q + q];
+    constexpr int NR = ROWS_RS + QP - 1;
+    const long long b0 = (long long)a.offset0 + mseg * 32;
+    const bool interior = (b0 >= a.H) && (b0 + 32LL * NR <= (long long)a.H + a.count);
+    const float2* __restrict__ src = reinterpret_cast<const float2*>(a.in) + (b0 - a.H) + p;
+    float2 ph0 = make_float2(1.f, 0.f);
+    if constexpr (XL) {
+        if (interior) ph0 = nco_tab(a.phi, a.plo, b0 - a.H + p);
+    }
+    float2* __restrict__ out = reinterpret_cast<float2*>(a.out);
+    // interior segments load unconditionally (all 32 row loads of a block in flight); the few
+    // segments touching the history or the end of the call fetch element-wise
+    auto body = [&](auto fast) {
+        constexpr bool F = decltype(fast)::value;
+        auto row = [&](int r) -> float2 {
+            if constexpr (F) {
+                float2 x = src[32 * r];
+                if constexpr (XL) x = cmulf(x, cmulf(ph0, a.nstep[r]));   // wave-uniform e^{i w 32 r}
+                return x;
+            } else {
+                return fir_fetch<float2, XL>(a, b0 + 32LL * r + p);
+            }
+        };
+        float2 P[QP];   // P[k], k >= 1: the open partial of output (r - k) before row r
+#pragma unroll
+        for (int k = 0; k < QP; k++) P[k] = make_float2(0.f, 0.f);
+        auto step = [&](float2 x) -> float2 {
+            float2 done = P[QP - 1];
+            mac(done, x, h[QP - 1]);
+#pragma unroll
+            for (int k = QP - 1; k >= 2; k--) {
+                P[k] = P[k - 1];
+                mac(P[k], x, h[k - 1]);
+            }
+            P[1] = make_float2(x.x * h[0], x.y * h[0]);
+            return done;
+        };
+        {
+            float2 pro[QP - 1];
+#pragma unroll
+            for (int r = 0; r < QP - 1; r++) pro[r] = row(r);
+#pragma unroll
+            for (int r = 0; r < QP - 1; r++) (void)step(pro[r]);
+        }
+        for (int blk = 0; blk < ROWS_RS / 32; blk++) {
+            float2 v[32];
+#pragma unroll
+            for (int i = 0; i < 32; i++) v[i] = row(QP - 1 + 32 * blk + i);
+#pragma unroll
+            for (int i = 0; i < 32; i++) v[i] = step(v[i]);
+#define SDRGPU_RED_STEP(DX, NV)                                                                   \
+            {                                                                                     \
+                const bool up = (p & (DX)) != 0;                                                  \
+                _Pragma("unroll") for (int i = 0; i < (NV); i++) {                                \
+                    const float2 snd = up ? v[i] : v[i + (NV)];                                   \
+                    const float2 keep = up ? v[i + (NV)] : v[i];                                  \
+                    const float rx = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(snd.x), ((DX) << 10) | 0x1F)); \
+                    const float ry = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(snd.y), ((DX) << 10) | 0x1F)); \
+                    v[i] = make_float2(keep.x + rx, keep.y + ry);                                 \
+                }                                                                                 \
+            }
+            SDRGPU_RED_STEP(16, 16)
+            SDRGPU_RED_STEP(8, 8)
+            SDRGPU_RED_STEP(4, 4)
+            SDRGPU_RED_STEP(2, 2)
+            SDRGPU_RED_STEP(1, 1)
+#undef SDRGPU_RED_STEP
+            const long long m = mseg + 32 * blk + p;
+            if (m < a.M) out[m] = v[0];
+        }
+    };
+    if (interior) body(std::true_type{});
+    else body(std::false_type{});
+}
+
 template <typename DT, bool XL>
 __global__ void fir_hist_kernel(const DT* __restrict__ hist, const DT* __restrict__ in, DT* __restrict__ next, int H,
                                 int count, const float2* __restrict__ phi, const float2* __restrict__ plo) {
@@ -489,6 +584,7 @@ struct Nco {
     PhaseAcc phase;     // phase of the next input sample
     DevBuf plo, phi;
     DevBuf step;        // [3][NCO_PF]: e^{i w u NT}, NT = 64, 128, 256 (fp64 -> float)
+    DevBuf rstep;       // [ROWS_STEP]: e^{i w 32 u} (fir_rows_kernel's row step)
     const float2* step_for(int NT) const { return step.as<float2>() + (NT == 64 ? 0 : NT == 128 ? 1 : 2) * NCO_PF; }
     int set_w(double w_) {
         w = w_;
@@ -502,6 +598,13 @@ struct Nco {
                 }
             SDRGPU_CHECK(step.ensure(sizeof(float2) * st.size()));
             SDRGPU_HIP(hipMemcpy(step.p, st.data(), sizeof(float2) * st.size(), hipMemcpyHostToDevice));
+            std::vector<float2> rs(ROWS_STEP);
+            for (int u = 0; u < ROWS_STEP; u++) {
+                const double a = std::fmod(w * (double)u * 32.0, 2.0 * M_PI);
+                rs[u] = make_float2((float)std::cos(a), (float)std::sin(a));
+            }
+            SDRGPU_CHECK(rstep.ensure(sizeof(float2) * rs.size()));
+            SDRGPU_HIP(hipMemcpy(rstep.p, rs.data(), sizeof(float2) * rs.size(), hipMemcpyHostToDevice));
         }
         std::vector<float2> t(NCO_LO);
         for (int k = 0; k < NCO_LO; k++) {
@@ -654,6 +757,7 @@ struct FirBlock : Block {
         if (const char* e = getenv("SDRGPU_FIR_MFMA")) useMfma = atoi(e);
         if (const char* e = getenv("SDRGPU_FIR_MFMA_NW")) mfNW = atoi(e);
         if (const char* e = getenv("SDRGPU_FIR_MFMA_PS")) usePS = atoi(e);
+        if (const char* e = getenv("SDRGPU_FIR_ROWS")) useRows = atoi(e);
         SDRGPU_CHECK(init_stream());
         SDRGPU_CHECK(set_taps(t, n));
         return SDRGPU_OK;
@@ -711,6 +815,9 @@ struct FirBlock : Block {
         // phase-split tiles for the larger decimations (and on request for the others)
         mfps = cplx && !mf && D >= 4 && D <= 32 && (usePS != 0);
         if (usePS == 2 && cplx && D >= 4 && D <= 32) { mfps = true; mf = false; }
+        // row-streaming kernel for D = 32 with <= 8 taps per phase (VFO stage 1), ahead of the MFMA tiles
+        rowsk = in_dtype == SDRGPU_C64 && ttype == SDRGPU_F32 && !stereo && !quad && D == 32 && Qr >= 2 && Qr <= 8 &&
+                useRows != 0;
         if (mf || mfps) {
             // gz[p][t] = h[(t - 15) D + p], gzs entries per phase (t < 15 + 4 ks suffice)
             gzs = mf ? MF_GZ : 16 + 4 * ((15 + Qr + 3) / 4);
@@ -727,6 +834,35 @@ struct FirBlock : Block {
     }
     bool mf = false;        // fir_mfma_kernel selected for the current taps / decimation
     bool mfps = false;      // fir_mfma_ps_kernel selected
+    bool rowsk = false;     // fir_rows_kernel selected
+    int useRows = 1;        // SDRGPU_FIR_ROWS (tuning): 0 off, 1 auto
+    template <int QP>
+    int launch_rows(FirArgs& a, int blocks, hipStream_t s) {
+        if (xl) hipLaunchKernelGGL((fir_rows_kernel<QP, true>), dim3(blocks), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((fir_rows_kernel<QP, false>), dim3(blocks), dim3(256), 0, s, a);
+        SDRGPU_HIP(hipGetLastError());
+        return SDRGPU_OK;
+    }
+    int run_rows(const void* in, int count, void* out, int M, hipStream_t s) {
+        FirArgs a{};
+        a.hist = hist[cur].p; a.in = in; a.taps = taps.p; a.out = out;
+        a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>();
+        a.ntaps = ntaps; a.H = ntaps - 1; a.count = count; a.D = D; a.Q = Q; a.offset0 = offset; a.M = M;
+        a.nstep = xl ? nco.rstep.as<float2>() : nullptr;
+        const long long segs = ((long long)M + ROWS_RS - 1) / ROWS_RS;
+        const int blocks = (int)((segs + 7) / 8);   // 4 waves x 2 half-wave segments
+        switch ((ntaps + D - 1) / D) {
+        case 2: return launch_rows<2>(a, blocks, s);
+        case 3: return launch_rows<3>(a, blocks, s);
+        case 4: return launch_rows<4>(a, blocks, s);
+        case 5: return launch_rows<5>(a, blocks, s);
+        case 6: return launch_rows<6>(a, blocks, s);
+        case 7: return launch_rows<7>(a, blocks, s);
+        case 8: return launch_rows<8>(a, blocks, s);
+        }
+        set_error("fir: rows kernel needs 2..8 taps per phase");
+        return SDRGPU_EARG;
+    }
     int gzs = MF_GZ;
     int usePS = 1;          // SDRGPU_FIR_MFMA_PS (tuning): 0 off, 1 auto (D >= 4 where fir_mfma_kernel is not used), 2 force
     template <bool XL, bool QD>
@@ -849,7 +985,9 @@ struct FirBlock : Block {
         const int M = out_count(count);
         const int H = ntaps - 1;
         if (xl && count > 0) SDRGPU_CHECK(nco.prepare(count, s));
-        if (M > 0 && mf) {
+        if (M > 0 && rowsk) {
+            SDRGPU_CHECK(run_rows(in, count, out, M, s));
+        } else if (M > 0 && mf) {
             SDRGPU_CHECK(run_mfma(in, count, out, M, s));
         } else if (M > 0 && mfps) {
             SDRGPU_CHECK(run_mfma_ps(in, count, out, M, s));
