@@ -467,7 +467,9 @@ __global__ __launch_bounds__(256) void fir_mfma_ps_kernel(FirArgs a) {
 // partial. Every 32 closed outputs the 32 per-phase partials are summed across the half by a
 // five-step xor transpose-reduce (ds_swizzle), which leaves output 32 blk + p in lane p.
 // Each sample is read once (plus QP - 1 halo rows per segment).
-constexpr int ROWS_RS = 128;   // outputs per half-wave segment
+// Segments of 64 or 256 outputs measured the same as 128; forcing 4 waves per SIMD (128 VGPRs)
+// spills and ran 10% slower.
+constexpr int ROWS_RS = 128;    // outputs per half-wave segment
 constexpr int ROWS_STEP = 256;  // e^{i w 32 u} table length (>= ROWS_RS + QP - 1)
 template <int QP, bool XL>
 __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
@@ -484,6 +486,8 @@ __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
     const bool interior = (b0 >= a.H) && (b0 + 32LL * NR <= (long long)a.H + a.count);
     const float2* __restrict__ src = reinterpret_cast<const float2*>(a.in) + (b0 - a.H) + p;
     float2 ph0 = make_float2(1.f, 0.f);
+    // the row-step table through the constant address space: scalar (SMEM) loads
+    const __attribute__((address_space(4))) float* nstep = (const __attribute__((address_space(4))) float*)a.nstep;
     if constexpr (XL) {
         if (interior) ph0 = nco_tab(a.phi, a.plo, b0 - a.H + p);
     }
@@ -495,7 +499,7 @@ __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
         auto row = [&](int r) -> float2 {
             if constexpr (F) {
                 float2 x = src[32 * r];
-                if constexpr (XL) x = cmulf(x, cmulf(ph0, a.nstep[r]));   // wave-uniform e^{i w 32 r}
+                if constexpr (XL) x = cmulf(x, cmulf(ph0, make_float2(nstep[2 * r], nstep[2 * r + 1])));   // wave-uniform e^{i w 32 r}
                 return x;
             } else {
                 return fir_fetch<float2, XL>(a, b0 + 32LL * r + p);

@@ -90,7 +90,7 @@ def test_fft_aes17_fixture():
 # ----------------------------------------------------------------------- FIR
 @pytest.mark.parametrize("ntaps,decim,cplx", [(1, 1, True), (91, 1, True), (228, 1, False), (256, 8, True),
                                                 (143, 32, True), (27, 4, True), (69, 2, False), (726, 128, True),
-                                                (5, 3, True)])
+                                                (5, 3, True), (33, 32, True), (256, 32, True), (200, 32, True)])
 def test_fir_vs_oracle(ntaps, decim, cplx, rng):
     taps = rng.standard_normal(ntaps).astype(np.float32) / ntaps
     g = dsp.FIR(taps, decim, cplx)
@@ -101,6 +101,22 @@ def test_fir_vs_oracle(ntaps, decim, cplx, rng):
         yg = g.process(x)
         assert len(yg) == len(yo), (n, len(yg), len(yo))
         assert_close_c(yg, yo, fir_atol(taps, x) if n else 0, f"fir {ntaps}/{decim}")
+
+
+def test_fir_rows_kernel_tap_change(rng):
+    # D = 32 runs on the row-streaming kernel (2..8 taps per phase); a setTaps across a
+    # taps-per-phase boundary keeps the history (fir.h:31-52) and resets the phase
+    t1 = rng.standard_normal(143).astype(np.float32) / 143
+    t2 = rng.standard_normal(230).astype(np.float32) / 230
+    g, o = dsp.FIR(t1, 32, True), oracle.FIR(t1, 32, True)
+    for taps in (t1, t2, t1):
+        g.set_taps(taps)
+        o.set_taps(taps)
+        for n in [40000, 333, 70001]:
+            x = iq(rng, n)
+            yg, yo = g.process(x), o.process(x)
+            assert len(yg) == len(yo)
+            assert_close_c(yg, yo, fir_atol(taps, x), "rows FIR tap change")
 
 
 def test_fir_complex_taps(rng):
