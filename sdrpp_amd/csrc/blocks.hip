@@ -459,31 +459,37 @@ __global__ __launch_bounds__(256) void fir_mfma_ps_kernel(FirArgs a) {
     }
 }
 
-// Row-streaming decimating FIR for D = 32 (VFO stage 1: 143 taps -> QP = 5 taps per phase), no
-// LDS. Lane p of each 32-lane half owns phase p. A half-wave walks a segment of RS outputs row by
-// row: row r is the 32 samples buf[b0 + 32 r .. + 31], one 256-B coalesced load per half. The
-// lane keeps the QP - 1 open partial sums of its phase in registers (output o takes row o + q
-// with tap h[32 q + p]), so every row costs QP complex x real FMAs and closes one per-phase
-// partial. Every 32 closed outputs the 32 per-phase partials are summed across the half by a
-// five-step xor transpose-reduce (ds_swizzle), which leaves output 32 blk + p in lane p.
-// Each sample is read once (plus QP - 1 halo rows per segment).
-// Segments of 64 or 256 outputs measured the same as 128; forcing 4 waves per SIMD (128 VGPRs)
-// spills and ran 10% slower.
-constexpr int ROWS_RS = 128;    // outputs per half-wave segment
-constexpr int ROWS_STEP = 256;  // e^{i w 32 u} table length (>= ROWS_RS + QP - 1)
-template <int QP, bool XL>
+// Row-streaming decimating FIR, no LDS (D = 32: VFO stage 1, 143 taps -> QP = 5 taps per phase;
+// D = 8: C3, 256 taps -> QP = 32, with the FM quadrature fused on the outputs). Lane p of each
+// D-lane group owns phase p. A group walks a segment of RS outputs row by row: row r is the D
+// samples buf[b0 + D r .. + D - 1], one coalesced 8D-byte load per group. The lane keeps the
+// QP - 1 open partial sums of its phase in registers (output o takes row o + q with tap
+// h[D q + p]), so every row costs QP complex x real FMAs and closes one per-phase partial.
+// Every D closed outputs the D per-phase partials are summed across the group by a log2(D)-step
+// xor transpose-reduce (ds_swizzle), which leaves output D blk + p in lane p. Each sample is
+// read once (plus QP - 1 halo rows per segment). With QUAD a segment starts one output early
+// (that output only feeds y[m - 1] of the next) and stores RS - 1 outputs.
+// D = 32: segments of 64 or 256 outputs measured the same as 128; forcing 4 waves per SIMD
+// (128 VGPRs) spills and ran 10% slower; loading batch t + 1 while batch t computes (2 waves per
+// SIMD) was no faster. D = 8 (C3) measured equal to fir_mfma_kernel (0.84 vs 0.85 ms), so it
+// runs only on request (SDRGPU_FIR_ROWS=2).
+constexpr int ROWS_STEP = 512;  // e^{i w D u} table length (>= RS + QP - 1)
+template <int D> constexpr int rows_rs() { return D == 32 ? 128 : 256; }
+template <int D, int QP, bool XL, bool QUAD>
 __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
-    const int lane = threadIdx.x & 63, p = lane & 31, hf = lane >> 5;
-    const long long seg = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + hf;
-    const long long mseg = seg * ROWS_RS;
-    if (mseg >= a.M) return;   // (the cross-lane steps stay inside one 32-lane half)
+    constexpr int RS = rows_rs<D>(), NG = 64 / D, QOFF = QUAD ? 1 : 0;
+    constexpr int BT = QP > 16 ? 16 : 32;   // rows per load batch (register budget at QP = 32)
+    const int lane = threadIdx.x & 63, p = lane & (D - 1), g = lane / D;
+    const long long seg = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * NG + g;
+    const long long mseg = seg * (RS - QOFF) - QOFF;   // output of local index 0
+    if (mseg + QOFF >= a.M) return;   // (the cross-lane steps stay inside one D-lane group)
     const float* __restrict__ taps = reinterpret_cast<const float*>(a.taps);   // [p][Q]
     float h[QP];
 #pragma unroll
-    for (int q = 0; q < QP; q++) h[q] = taps[p * a.Q + q];
-    constexpr int NR = ROWS_RS + QP - 1;
-    const long long b0 = (long long)a.offset0 + mseg * 32;
-    const bool interior = (b0 >= a.H) && (b0 + 32LL * NR <= (long long)a.H + a.count);
+    for (int q = 0; q < QP; q++) h[q] = q < a.Q ? taps[p * a.Q + q] : 0.0f;
+    constexpr int NR = RS + QP - 1;
+    const long long b0 = (long long)a.offset0 + mseg * D;
+    const bool interior = (b0 >= a.H) && (b0 + (long long)D * NR <= (long long)a.H + a.count);
     const float2* __restrict__ src = reinterpret_cast<const float2*>(a.in) + (b0 - a.H) + p;
     float2 ph0 = make_float2(1.f, 0.f);
     // the row-step table through the constant address space: scalar (SMEM) loads
@@ -491,19 +497,19 @@ __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
     if constexpr (XL) {
         if (interior) ph0 = nco_tab(a.phi, a.plo, b0 - a.H + p);
     }
-    float2* __restrict__ out = reinterpret_cast<float2*>(a.out);
-    // interior segments load unconditionally (all 32 row loads of a block in flight); the few
-    // segments touching the history or the end of the call fetch element-wise
+    float2* __restrict__ out2 = reinterpret_cast<float2*>(a.out);
+    float* __restrict__ outf = reinterpret_cast<float*>(a.out);
+    // interior segments load unconditionally (32 row loads in flight); the few segments touching
+    // the history or the end of the call fetch element-wise
     auto body = [&](auto fast) {
         constexpr bool F = decltype(fast)::value;
-        auto row = [&](int r) -> float2 {
-            if constexpr (F) {
-                float2 x = src[32 * r];
-                if constexpr (XL) x = cmulf(x, cmulf(ph0, make_float2(nstep[2 * r], nstep[2 * r + 1])));   // wave-uniform e^{i w 32 r}
-                return x;
-            } else {
-                return fir_fetch<float2, XL>(a, b0 + 32LL * r + p);
-            }
+        auto row = [&](int r) -> float2 {   // raw row sample (the slow path applies the xlator itself)
+            if constexpr (F) return src[D * r];
+            else return fir_fetch<float2, XL>(a, b0 + (long long)D * r + p);
+        };
+        auto xlate = [&](float2 x, int r) -> float2 {   // fused xlator of the fast path: e^{i w D r}
+            if constexpr (F && XL) x = cmulf(x, cmulf(ph0, make_float2(nstep[2 * r], nstep[2 * r + 1])));
+            return x;
         };
         float2 P[QP];   // P[k], k >= 1: the open partial of output (r - k) before row r
 #pragma unroll
@@ -519,38 +525,64 @@ __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
             P[1] = make_float2(x.x * h[0], x.y * h[0]);
             return done;
         };
-        {
-            float2 pro[QP - 1];
+        for (int r0 = 0; r0 < QP - 1; r0 += 8) {   // prologue: rows 0 .. QP - 2 close no output
+            float2 pro[8];
 #pragma unroll
-            for (int r = 0; r < QP - 1; r++) pro[r] = row(r);
+            for (int r = 0; r < 8; r++) pro[r] = (r0 + r < QP - 1) ? row(r0 + r) : make_float2(0.f, 0.f);
 #pragma unroll
-            for (int r = 0; r < QP - 1; r++) (void)step(pro[r]);
+            for (int r = 0; r < 8; r++)
+                if (r0 + r < QP - 1) (void)step(xlate(pro[r], r0 + r));
         }
-        for (int blk = 0; blk < ROWS_RS / 32; blk++) {
-            float2 v[32];
+        float2 ylast = make_float2(0.f, 0.f);   // QUAD: the group's previous output
+#pragma unroll 1
+        for (int bt = 0; bt < RS / BT; bt++) {
+            float2 v[BT];
 #pragma unroll
-            for (int i = 0; i < 32; i++) v[i] = row(QP - 1 + 32 * blk + i);
+            for (int i = 0; i < BT; i++) v[i] = row(QP - 1 + BT * bt + i);   // BT row loads in flight
 #pragma unroll
-            for (int i = 0; i < 32; i++) v[i] = step(v[i]);
-#define SDRGPU_RED_STEP(DX, NV)                                                                   \
-            {                                                                                     \
-                const bool up = (p & (DX)) != 0;                                                  \
-                _Pragma("unroll") for (int i = 0; i < (NV); i++) {                                \
-                    const float2 snd = up ? v[i] : v[i + (NV)];                                   \
-                    const float2 keep = up ? v[i + (NV)] : v[i];                                  \
-                    const float rx = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(snd.x), ((DX) << 10) | 0x1F)); \
-                    const float ry = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(snd.y), ((DX) << 10) | 0x1F)); \
-                    v[i] = make_float2(keep.x + rx, keep.y + ry);                                 \
-                }                                                                                 \
-            }
-            SDRGPU_RED_STEP(16, 16)
-            SDRGPU_RED_STEP(8, 8)
-            SDRGPU_RED_STEP(4, 4)
-            SDRGPU_RED_STEP(2, 2)
-            SDRGPU_RED_STEP(1, 1)
+            for (int i = 0; i < BT; i++) v[i] = step(xlate(v[i], QP - 1 + BT * bt + i));
+#pragma unroll
+            for (int kb = 0; kb < BT / D; kb++) {
+                float2* w = v + kb * D;
+#define SDRGPU_RED_STEP(DX)                                                                        \
+                if constexpr (D > (DX)) {                                                          \
+                    const bool up = (p & (DX)) != 0;                                               \
+                    _Pragma("unroll") for (int i = 0; i < (DX); i++) {                             \
+                        const float2 snd = up ? w[i] : w[i + (DX)];                                \
+                        const float2 keep = up ? w[i + (DX)] : w[i];                               \
+                        const float rx = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(snd.x), ((DX) << 10) | 0x1F)); \
+                        const float ry = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(snd.y), ((DX) << 10) | 0x1F)); \
+                        w[i] = make_float2(keep.x + rx, keep.y + ry);                              \
+                    }                                                                              \
+                }
+                SDRGPU_RED_STEP(16)
+                SDRGPU_RED_STEP(8)
+                SDRGPU_RED_STEP(4)
+                SDRGPU_RED_STEP(2)
+                SDRGPU_RED_STEP(1)
 #undef SDRGPU_RED_STEP
-            const long long m = mseg + 32 * blk + p;
-            if (m < a.M) out[m] = v[0];
+                const float2 y = w[0];
+                const int j = BT * bt + kb * D + p;   // local output index
+                const long long m = mseg + j;
+                if constexpr (QUAD) {
+                    // y[m - 1]: lane p - 1 of the group, or the group's last output of the previous block
+                    const int srcl = (lane & ~(D - 1)) + ((p + D - 1) & (D - 1));
+                    float2 prev = make_float2(__shfl(y.x, srcl), __shfl(y.y, srcl));
+                    if (p == 0) prev = ylast;
+                    const int lastl = (lane & ~(D - 1)) + D - 1;
+                    ylast = make_float2(__shfl(y.x, lastl), __shfl(y.y, lastl));
+                    if (m == 0) prev = a.din[0];
+                    if (j >= QOFF && m >= 0 && m < a.M) {
+                        const float br = prev.x, bi = -prev.y;
+                        const float re = (y.x * br) - (y.y * bi);
+                        const float im = (y.y * br) + (y.x * bi);
+                        outf[m] = atan2f(im, re) * a.invDev;
+                        if (m == a.M - 1) a.dinNext[0] = y;
+                    }
+                } else {
+                    if (m < a.M) out2[m] = y;
+                }
+            }
         }
     };
     if (interior) body(std::true_type{});
@@ -588,7 +620,8 @@ struct Nco {
     PhaseAcc phase;     // phase of the next input sample
     DevBuf plo, phi;
     DevBuf step;        // [3][NCO_PF]: e^{i w u NT}, NT = 64, 128, 256 (fp64 -> float)
-    DevBuf rstep;       // [ROWS_STEP]: e^{i w 32 u} (fir_rows_kernel's row step)
+    DevBuf rstep;       // [2][ROWS_STEP]: e^{i w D u}, D = 8, 32 (fir_rows_kernel's row step)
+    const float2* rstep_for(int D) const { return rstep.as<float2>() + (D == 8 ? 0 : ROWS_STEP); }
     const float2* step_for(int NT) const { return step.as<float2>() + (NT == 64 ? 0 : NT == 128 ? 1 : 2) * NCO_PF; }
     int set_w(double w_) {
         w = w_;
@@ -602,11 +635,12 @@ struct Nco {
                 }
             SDRGPU_CHECK(step.ensure(sizeof(float2) * st.size()));
             SDRGPU_HIP(hipMemcpy(step.p, st.data(), sizeof(float2) * st.size(), hipMemcpyHostToDevice));
-            std::vector<float2> rs(ROWS_STEP);
-            for (int u = 0; u < ROWS_STEP; u++) {
-                const double a = std::fmod(w * (double)u * 32.0, 2.0 * M_PI);
-                rs[u] = make_float2((float)std::cos(a), (float)std::sin(a));
-            }
+            std::vector<float2> rs(2 * ROWS_STEP);
+            for (int k = 0; k < 2; k++)
+                for (int u = 0; u < ROWS_STEP; u++) {
+                    const double a = std::fmod(w * (double)u * (k ? 32.0 : 8.0), 2.0 * M_PI);
+                    rs[k * ROWS_STEP + u] = make_float2((float)std::cos(a), (float)std::sin(a));
+                }
             SDRGPU_CHECK(rstep.ensure(sizeof(float2) * rs.size()));
             SDRGPU_HIP(hipMemcpy(rstep.p, rs.data(), sizeof(float2) * rs.size(), hipMemcpyHostToDevice));
         }
@@ -820,8 +854,8 @@ struct FirBlock : Block {
         mfps = cplx && !mf && D >= 4 && D <= 32 && (usePS != 0);
         if (usePS == 2 && cplx && D >= 4 && D <= 32) { mfps = true; mf = false; }
         // row-streaming kernel for D = 32 with <= 8 taps per phase (VFO stage 1), ahead of the MFMA tiles
-        rowsk = in_dtype == SDRGPU_C64 && ttype == SDRGPU_F32 && !stereo && !quad && D == 32 && Qr >= 2 && Qr <= 8 &&
-                useRows != 0;
+        rowsk = in_dtype == SDRGPU_C64 && ttype == SDRGPU_F32 && !stereo && rows_qp(D, Qr) > 0 &&
+                !(quad && D == 32) && (useRows == 2 || (useRows == 1 && D == 32));
         if (mf || mfps) {
             // gz[p][t] = h[(t - 15) D + p], gzs entries per phase (t < 15 + 4 ks suffice)
             gzs = mf ? MF_GZ : 16 + 4 * ((15 + Qr + 3) / 4);
@@ -839,32 +873,51 @@ struct FirBlock : Block {
     bool mf = false;        // fir_mfma_kernel selected for the current taps / decimation
     bool mfps = false;      // fir_mfma_ps_kernel selected
     bool rowsk = false;     // fir_rows_kernel selected
-    int useRows = 1;        // SDRGPU_FIR_ROWS (tuning): 0 off, 1 auto
-    template <int QP>
-    int launch_rows(FirArgs& a, int blocks, hipStream_t s) {
-        if (xl) hipLaunchKernelGGL((fir_rows_kernel<QP, true>), dim3(blocks), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((fir_rows_kernel<QP, false>), dim3(blocks), dim3(256), 0, s, a);
+    int useRows = 1;        // SDRGPU_FIR_ROWS (tuning): 0 off, 1 auto (D = 32), 2 also D = 8
+    template <int D, int QP, bool QD>
+    int launch_rows(FirArgs& a, hipStream_t s) {
+        constexpr int RS = rows_rs<D>();
+        const int q = QD ? 1 : 0;
+        const long long segs = ((long long)a.M + q + (RS - q) - 1) / (RS - q);
+        const int blocks = (int)((segs + 4 * (64 / D) - 1) / (4 * (64 / D)));   // 4 waves x 64/D groups
+        if (xl) hipLaunchKernelGGL((fir_rows_kernel<D, QP, true, QD>), dim3(blocks), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((fir_rows_kernel<D, QP, false, QD>), dim3(blocks), dim3(256), 0, s, a);
         SDRGPU_HIP(hipGetLastError());
         return SDRGPU_OK;
+    }
+    // taps per phase of the rows kernel: D = 32 exact (2..8), D = 8 padded to 16, 24 or 32
+    static int rows_qp(int D, int Qr) {
+        if (D == 32) return (Qr >= 2 && Qr <= 8) ? Qr : 0;
+        if (D == 8) return Qr < 2 ? 0 : Qr <= 16 ? 16 : Qr <= 24 ? 24 : Qr <= 32 ? 32 : 0;
+        return 0;
     }
     int run_rows(const void* in, int count, void* out, int M, hipStream_t s) {
         FirArgs a{};
         a.hist = hist[cur].p; a.in = in; a.taps = taps.p; a.out = out;
+        a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
         a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>();
         a.ntaps = ntaps; a.H = ntaps - 1; a.count = count; a.D = D; a.Q = Q; a.offset0 = offset; a.M = M;
-        a.nstep = xl ? nco.rstep.as<float2>() : nullptr;
-        const long long segs = ((long long)M + ROWS_RS - 1) / ROWS_RS;
-        const int blocks = (int)((segs + 7) / 8);   // 4 waves x 2 half-wave segments
-        switch ((ntaps + D - 1) / D) {
-        case 2: return launch_rows<2>(a, blocks, s);
-        case 3: return launch_rows<3>(a, blocks, s);
-        case 4: return launch_rows<4>(a, blocks, s);
-        case 5: return launch_rows<5>(a, blocks, s);
-        case 6: return launch_rows<6>(a, blocks, s);
-        case 7: return launch_rows<7>(a, blocks, s);
-        case 8: return launch_rows<8>(a, blocks, s);
+        a.invDev = invDev;
+        a.nstep = xl ? nco.rstep_for(D) : nullptr;
+        const int qp = rows_qp(D, (ntaps + D - 1) / D);
+        if (D == 32 && !quad) {
+            switch (qp) {
+            case 2: return launch_rows<32, 2, false>(a, s);
+            case 3: return launch_rows<32, 3, false>(a, s);
+            case 4: return launch_rows<32, 4, false>(a, s);
+            case 5: return launch_rows<32, 5, false>(a, s);
+            case 6: return launch_rows<32, 6, false>(a, s);
+            case 7: return launch_rows<32, 7, false>(a, s);
+            case 8: return launch_rows<32, 8, false>(a, s);
+            }
+        } else if (D == 8) {
+            switch (qp) {
+            case 16: return quad ? launch_rows<8, 16, true>(a, s) : launch_rows<8, 16, false>(a, s);
+            case 24: return quad ? launch_rows<8, 24, true>(a, s) : launch_rows<8, 24, false>(a, s);
+            case 32: return quad ? launch_rows<8, 32, true>(a, s) : launch_rows<8, 32, false>(a, s);
+            }
         }
-        set_error("fir: rows kernel needs 2..8 taps per phase");
+        set_error("fir: rows kernel does not take (D %d, ntaps %d)", D, ntaps);
         return SDRGPU_EARG;
     }
     int gzs = MF_GZ;

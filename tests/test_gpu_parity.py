@@ -254,6 +254,29 @@ def test_ddc_fm_c3(rng):
         assert np.mean(np.abs(yg - yo) < 1e-3) > 0.999
 
 
+@pytest.mark.parametrize("ntaps,quad", [(256, True), (256, False), (150, False), (190, True)])
+def test_rows_kernel_d8_on_request(ntaps, quad, rng, monkeypatch):
+    # fir_rows_kernel at D = 8 (taps per phase padded to 16/24/32, optional fused quadrature) is
+    # selected only with SDRGPU_FIR_ROWS=2 (read at block creation); check it against the oracle
+    monkeypatch.setenv("SDRGPU_FIR_ROWS", "2")
+    fs = 61.44e6
+    taps = dsp.low_pass(3.0e6, 912000.0, fs) if ntaps == 256 else (rng.standard_normal(ntaps) / ntaps).astype(np.float32)
+    w = 2 * np.pi * (-1.5e6 / fs)
+    dev = 2 * np.pi * 100e3 / (fs / 8)
+    g = dsp.DDCFM(w, taps, 8, dev) if quad else dsp.FIR(taps, 8)
+    ox, of, oq = oracle.Xlator(w), oracle.FIR(taps, 8), oracle.Quadrature(dev)
+    for n in [307200, 12345, 8, 500000]:
+        x = iq(rng, n)
+        if quad:
+            yo, yg = oq.process(of.process(ox.process(x))), g.process(x)
+            assert len(yg) == len(yo)
+            assert np.mean(np.abs(yg - yo) < 1e-3) > 0.999
+        else:
+            yo, yg = of.process(x), g.process(x)
+            assert len(yg) == len(yo)
+            assert_close_c(yg, yo, fir_atol(taps, x), "rows FIR D=8")
+
+
 def test_fm_tone_demod_amplitude():
     # 1 kHz tone FM-modulated at 75 kHz deviation, demodulated with dev 100 kHz -> amplitude 0.75
     fs = 240000.0
