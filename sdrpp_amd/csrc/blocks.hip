@@ -1642,15 +1642,24 @@ extern "C" int sdrgpu_block_process(sdrgpu_block* h, const void* in, int count, 
     SDRGPU_CHECK(b->pin_out.ensure(outB));
     SDRGPU_CHECK(b->dev_in.ensure(inB));
     SDRGPU_CHECK(b->dev_out.ensure(outB));
+    // buffers registered with sdrgpu_host_register are DMA'd directly; others go through the
+    // handle's pinned staging buffers
+    const bool inPinned = host_pinned(in, (size_t)count * esize(b->in_dtype));
+    const bool outPinned = host_pinned(out, (size_t)mExp * esize(b->out_dtype));
     if (count > 0) {
-        std::memcpy(b->pin_in.p, in, (size_t)count * esize(b->in_dtype));
-        SDRGPU_HIP(hipMemcpyAsync(b->dev_in.p, b->pin_in.p, (size_t)count * esize(b->in_dtype), hipMemcpyHostToDevice, b->own));
+        const void* src = in;
+        if (!inPinned) {
+            std::memcpy(b->pin_in.p, in, (size_t)count * esize(b->in_dtype));
+            src = b->pin_in.p;
+        }
+        SDRGPU_HIP(hipMemcpyAsync(b->dev_in.p, src, (size_t)count * esize(b->in_dtype), hipMemcpyHostToDevice, b->own));
     }
     int m = b->run(b->dev_in.p, count, b->dev_out.p, b->own);
     if (m < 0) return m;
-    if (m > 0) SDRGPU_HIP(hipMemcpyAsync(b->pin_out.p, b->dev_out.p, (size_t)m * esize(b->out_dtype), hipMemcpyDeviceToHost, b->own));
+    void* dst = (outPinned && m <= mExp) ? out : b->pin_out.p;
+    if (m > 0) SDRGPU_HIP(hipMemcpyAsync(dst, b->dev_out.p, (size_t)m * esize(b->out_dtype), hipMemcpyDeviceToHost, b->own));
     SDRGPU_HIP(hipStreamSynchronize(b->own));
-    if (m > 0) std::memcpy(out, b->pin_out.p, (size_t)m * esize(b->out_dtype));
+    if (m > 0 && dst != out) std::memcpy(out, b->pin_out.p, (size_t)m * esize(b->out_dtype));
     return m;
 }
 

@@ -1,4 +1,6 @@
 // C ABI: runtime helpers and the host-side design entry points of libsdrgpu.
+#include <map>
+#include <mutex>
 #include "sdrgpu_internal.h"
 
 namespace sdrgpu { const char* last_error(); }
@@ -47,11 +49,34 @@ extern "C" int sdrgpu_stream_synchronize(void* stream) {
     SDRGPU_HIP(hipStreamSynchronize((hipStream_t)stream));
     return SDRGPU_OK;
 }
+// Registered (page-locked) host ranges. The host-buffer process calls DMA straight from / to
+// a registered buffer and stage through their own pinned buffers otherwise.
+namespace {
+std::mutex g_pinMtx;
+std::map<uintptr_t, size_t> g_pinned;   // start -> bytes
+}  // namespace
+namespace sdrgpu {
+bool host_pinned(const void* p, size_t bytes) {
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_pinMtx);
+    auto it = g_pinned.upper_bound(a);
+    if (it == g_pinned.begin()) return false;
+    --it;
+    return a >= it->first && a + bytes <= it->first + it->second;
+}
+}  // namespace sdrgpu
 extern "C" int sdrgpu_host_register(void* ptr, size_t bytes) {
+    if (!ptr || bytes == 0) { set_error("host_register: empty range"); return SDRGPU_EARG; }
     SDRGPU_HIP(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    std::lock_guard<std::mutex> lk(g_pinMtx);
+    g_pinned[(uintptr_t)ptr] = bytes;
     return SDRGPU_OK;
 }
 extern "C" int sdrgpu_host_unregister(void* ptr) {
+    {
+        std::lock_guard<std::mutex> lk(g_pinMtx);
+        g_pinned.erase((uintptr_t)ptr);
+    }
     SDRGPU_HIP(hipHostUnregister(ptr));
     return SDRGPU_OK;
 }

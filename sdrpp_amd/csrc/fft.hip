@@ -797,10 +797,18 @@ extern "C" int sdrgpu_fft_logmag(sdrgpu_fft* h, const void* in, float* out) {
     SDRGPU_CHECK(p.pin_in.ensure(inB));
     SDRGPU_CHECK(p.dev_in.ensure(inB));
     SDRGPU_CHECK(p.dev_out.ensure(outB));
-    std::memcpy(p.pin_in.p, in, inB);
-    SDRGPU_HIP(hipMemcpyAsync(p.dev_in.p, p.pin_in.p, inB, hipMemcpyHostToDevice, p.own));
+    // registered host buffers (sdrgpu_host_register) are DMA'd directly, others staged
+    const void* src = in;
+    if (!host_pinned(in, inB)) {
+        std::memcpy(p.pin_in.p, in, inB);
+        src = p.pin_in.p;
+    }
+    SDRGPU_HIP(hipMemcpyAsync(p.dev_in.p, src, inB, hipMemcpyHostToDevice, p.own));
     SDRGPU_CHECK(sdrgpu_fft_execute_dev(h, p.dev_in.p, p.nz, 1, p.dev_out.as<float>(), p.own));
-    if (out) {
+    if (out && host_pinned(out, outB)) {
+        SDRGPU_HIP(hipMemcpyAsync(out, p.dev_out.p, outB, hipMemcpyDeviceToHost, p.own));
+        SDRGPU_HIP(hipStreamSynchronize(p.own));
+    } else if (out) {
         SDRGPU_CHECK(p.pin_out.ensure(outB));
         SDRGPU_HIP(hipMemcpyAsync(p.pin_out.p, p.dev_out.p, outB, hipMemcpyDeviceToHost, p.own));
         SDRGPU_HIP(hipStreamSynchronize(p.own));

@@ -8,6 +8,7 @@
 #include "../../include/sdrgpu.h"
 
 namespace sdrgpu {
+bool host_pinned(const void* p, size_t bytes);   // inside a sdrgpu_host_register range (capi.cpp)
 
 void set_error(const char* fmt, ...);
 

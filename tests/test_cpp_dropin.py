@@ -9,9 +9,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "build", "test_dropin")
 
 
-def _build():
+def _build(pinned=False):
+    """pinned: built with SDRGPU_PIN_STREAMS, so every dsp::stream buffer is registered with
+    sdrgpu_host_register and the blocks DMA straight from / into the stream buffers."""
     os.makedirs(os.path.dirname(BIN), exist_ok=True)
-    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-pthread",
+    binp = BIN + ("_pinned" if pinned else "")
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-pthread"] + (["-DSDRGPU_PIN_STREAMS"] if pinned else []) + [
            "-I", os.path.join(ROOT, "sdrpp_amd", "dsp", "gpu"),
            "-I", os.path.join(ROOT, "sdrpp_amd", "dsp", "runtime"),
            "-I", os.path.join(ROOT, "sdrpp_amd", "dsp", "runtime", "dsp", "buffer"),   # resolves "../processor.h"
@@ -20,19 +23,21 @@ def _build():
            "-L", os.path.join(ROOT, "sdrpp_amd", "lib"), "-lsdrgpu",
            "-L", os.path.join(ROOT, "oracle"), "-lsdr_oracle",
            "-Wl,-rpath," + os.path.join(ROOT, "sdrpp_amd", "lib") + ":" + os.path.join(ROOT, "oracle"),
-           "-o", BIN]
+           "-o", binp]
     subprocess.check_call(cmd)
+    return binp
 
 
-def test_dropin_compiles():
-    _build()
-    assert os.path.exists(BIN)
+@pytest.mark.parametrize("pinned", [False, True])
+def test_dropin_compiles(pinned):
+    assert os.path.exists(_build(pinned))
 
 
 @pytest.mark.gpu
-def test_dropin_runs_on_gpu():
-    _build()
-    r = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
+@pytest.mark.parametrize("pinned", [False, True])
+def test_dropin_runs_on_gpu(pinned):
+    b = _build(pinned)
+    r = subprocess.run([b], capture_output=True, text=True, timeout=300)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ALL OK" in r.stdout

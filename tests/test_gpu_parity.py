@@ -277,6 +277,35 @@ def test_rows_kernel_d8_on_request(ntaps, quad, rng, monkeypatch):
             assert_close_c(yg, yo, fir_atol(taps, x), "rows FIR D=8")
 
 
+def test_registered_host_buffers_dma_directly(rng):
+    # sdrgpu_host_register'ed in/out buffers take the direct-DMA path of the host process calls
+    # (no staging copy); the results are identical to the staged path
+    import ctypes
+    lib = sdrpp_amd.lib
+    taps = dsp.low_pass(3.0e6, 912000.0, 61.44e6)
+    x = iq(rng, 300000)
+    ref = dsp.FIR(taps, 8).process(x)
+    xin = np.ascontiguousarray(x)
+    yout = np.zeros(len(ref) + 16, dtype=np.complex64)
+    for a in (xin, yout):
+        assert lib.sdrgpu_host_register(ctypes.c_void_p(a.ctypes.data), ctypes.c_size_t(a.nbytes)) == 0
+    try:
+        g = dsp.FIR(taps, 8)
+        m = lib.sdrgpu_block_process(g._h, ctypes.c_void_p(xin.ctypes.data), len(xin), ctypes.c_void_p(yout.ctypes.data))
+        assert m == len(ref)
+        np.testing.assert_array_equal(yout[:m], ref)
+        f = dsp.FFTSpectrum(65536, 65536, 6)
+        db_ref = f.logmag(xin[:65536])
+        db = np.zeros(65536, dtype=np.float32)
+        assert lib.sdrgpu_host_register(ctypes.c_void_p(db.ctypes.data), ctypes.c_size_t(db.nbytes)) == 0
+        assert lib.sdrgpu_fft_logmag(f._h, ctypes.c_void_p(xin.ctypes.data), ctypes.c_void_p(db.ctypes.data)) == 65536
+        np.testing.assert_array_equal(db, db_ref)
+        assert lib.sdrgpu_host_unregister(ctypes.c_void_p(db.ctypes.data)) == 0
+    finally:
+        for a in (xin, yout):
+            assert lib.sdrgpu_host_unregister(ctypes.c_void_p(a.ctypes.data)) == 0
+
+
 def test_fm_tone_demod_amplitude():
     # 1 kHz tone FM-modulated at 75 kHz deviation, demodulated with dev 100 kHz -> amplitude 0.75
     fs = 240000.0
