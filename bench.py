@@ -278,7 +278,8 @@ def main():
     # One stream for the whole step. Forking the spectrum and the VFO chain onto two streams
     # (the reference runs them on separate block threads, iq_frontend.cpp:49,115) was
     # measured twice: the step time does not change (2.95 vs 2.97 ms; with the MFMA VFO stage
-    # 2.265 vs 2.261 ms) but the spectrum's event/rocprof durations stretch by the overlap
+    # 2.265 vs 2.261 ms; with the register-streaming VFO stage 1, 2.03-2.13 vs 2.01-2.04 ms)
+    # but the spectrum's event/rocprof durations stretch by the overlap
     # (1.58 -> 1.89 ms), so the roofline numbers would stop describing the kernel.
     def step(timed):
         evs = []
