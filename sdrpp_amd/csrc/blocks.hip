@@ -501,7 +501,7 @@ __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
     }
     float2* __restrict__ out2 = reinterpret_cast<float2*>(a.out);
     float* __restrict__ outf = reinterpret_cast<float*>(a.out);
-    // interior segments load unconditionally (32 row loads in flight); the few segments touching
+    // interior segments load unconditionally (BT row loads in flight); the few segments touching
     // the history or the end of the call fetch element-wise
     auto body = [&](auto fast) {
         constexpr bool F = decltype(fast)::value;
