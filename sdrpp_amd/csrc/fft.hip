@@ -551,9 +551,13 @@ static int launch_merged(const FftPlan& p, const float2* scratchB, int framesB, 
 // occupancy to pass A's 147 KB of LDS, so the 1M transform keeps separate launches.
 static int dispatch_merged(const FftPlan& p, const float2* scratchB, int framesB, float* outB, const float2* in,
                            long long stride, int framesA, float2* scratchA, hipStream_t s) {
+    if (p.sa == 64) return launch_merged<256, 64, 256, 64, false>(p, scratchB, framesB, outB, in, stride, framesA, scratchA, s);
+    if (p.sa == 32) return launch_merged<256, 32, 256, 32, false>(p, scratchB, framesB, outB, in, stride, framesA, scratchA, s);
     return launch_merged<256, 16, 256, 16, false>(p, scratchB, framesB, outB, in, stride, framesA, scratchA, s);
 }
-static bool merged_supported(const FftPlan& p, bool paired) { return !paired && p.N1 == 256 && p.N2 == 256 && p.sa == 16; }
+static bool merged_supported(const FftPlan& p, bool paired) {
+    return !paired && p.N1 == 256 && p.N2 == 256 && (p.sa == 16 || ((p.sa == 32 || p.sa == 64) && p.sb == p.sa));
+}
 
 static int dispatch_single(const FftPlan& p, const float2* in, long long stride, int frames, float* out, hipStream_t s) {
     switch (p.N) {
@@ -667,6 +671,10 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         // measured 2-5% slower for 64k with merged launches; 1M: 2.32 vs 2.39 ms at 64 MB)
         long long chunkMB = 128;
         if (const char* e = getenv("SDRGPU_FFT_CHUNK_MB")) chunkMB = std::max(1, atoi(e));
+        // 64k (256 x 256): 32 columns / 32 rows per workgroup (256-B pass-A row segments, 128-B
+        // pass-B dB segments, 512 threads, 2 workgroups per CU): the merged spectrum launches
+        // take 1.44 vs 1.58 ms per 2^28 samples with 16 / 16 (A/B on one box)
+        if (p.N1 == 256 && p.N2 == 256) p.sa = p.sb = 32;
         if (const char* e = getenv("SDRGPU_FFT_SA")) p.sa = atoi(e);
         if (const char* e = getenv("SDRGPU_FFT_SB")) p.sb = atoi(e);
         if (const char* e = getenv("SDRGPU_FFT_DEBUG")) p.dbg = atoi(e);
