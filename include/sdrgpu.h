@@ -115,6 +115,9 @@ int sdrgpu_rational_resampler_create(sdrgpu_block** h, int device, int dtype, do
 /* RxVFO: xlator(-offset) -> rational resampler -> LPF(bw/2) if bw != outSr */
 int sdrgpu_rxvfo_create(sdrgpu_block** h, int device, double inSamplerate, double outSamplerate, double bandwidth, double offset);
 int sdrgpu_rxvfo_set_offset(sdrgpu_block* h, double offset);
+/* Fused DDC: xlator(offsetRad) -> DecimatingFIR<complex_t,float>(taps, decim); complex_t out
+ * (frequency_xlator.h:43-50 + decimating_fir.h:45-68 in one kernel) */
+int sdrgpu_ddc_create(sdrgpu_block** h, int device, double offsetRad, const float* taps, int ntaps, int decim);
 /* Fused DDC: xlator(offsetRad) -> DecimatingFIR<complex_t,float>(taps, decim) -> Quadrature(deviationRad); float out */
 int sdrgpu_ddc_fm_create(sdrgpu_block** h, int device, double offsetRad, const float* taps, int ntaps, int decim, double deviationRad);
 /* FM<float> (demod/fm.h) and BroadcastFM mono (stereo_t out, broadcast_fm.h) */

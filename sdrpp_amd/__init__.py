@@ -80,6 +80,7 @@ def _load():
         "sdrgpu_rational_resampler_create": (i, [pp, i, i, d, d]),
         "sdrgpu_rxvfo_create": (i, [pp, i, d, d, d, d]),
         "sdrgpu_rxvfo_set_offset": (i, [vp, d]),
+        "sdrgpu_ddc_create": (i, [pp, i, d, fp, i, i]),
         "sdrgpu_ddc_fm_create": (i, [pp, i, d, fp, i, i, d]),
         "sdrgpu_fm_create": (i, [pp, i, d, d, i, i]),
         "sdrgpu_wfm_create": (i, [pp, i, d, d, i]),

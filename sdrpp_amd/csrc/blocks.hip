@@ -766,6 +766,19 @@ PinnedBuf::~PinnedBuf() {
     if (p) (void)hipHostFree(p);
 }
 
+int StreamOrder::follow(hipStream_t s) {
+    if (last != nullptr && last != s) {
+        if (!ev) SDRGPU_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        SDRGPU_HIP(hipEventRecord(ev, last));
+        SDRGPU_HIP(hipStreamWaitEvent(s, ev, 0));
+    }
+    last = s;
+    return SDRGPU_OK;
+}
+StreamOrder::~StreamOrder() {
+    if (ev) (void)hipEventDestroy(ev);
+}
+
 Block::~Block() {
     if (own) (void)hipStreamDestroy(own);
 }
@@ -791,13 +804,13 @@ struct FirBlock : Block {
         ttype = ttype_;
         if (decim < 1) { set_error("fir: decimation %d < 1", decim); return SDRGPU_EARG; }
         D = decim;
-        if (const char* e = getenv("SDRGPU_FIR_NT")) forceNT = atoi(e);
-        if (const char* e = getenv("SDRGPU_FIR_K")) forceK = atoi(e);
-        if (const char* e = getenv("SDRGPU_FIR_LDS_KB")) ldsCap = std::max(8, atoi(e));
-        if (const char* e = getenv("SDRGPU_FIR_MFMA")) useMfma = atoi(e);
-        if (const char* e = getenv("SDRGPU_FIR_MFMA_NW")) mfNW = atoi(e);
-        if (const char* e = getenv("SDRGPU_FIR_MFMA_PS")) usePS = atoi(e);
-        if (const char* e = getenv("SDRGPU_FIR_ROWS")) useRows = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FIR_NT")) forceNT = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FIR_K")) forceK = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FIR_LDS_KB")) ldsCap = std::max(8, atoi(e));
+        if (const char* e = tuning_env("SDRGPU_FIR_MFMA")) useMfma = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FIR_MFMA_NW")) mfNW = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FIR_MFMA_PS")) usePS = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FIR_ROWS")) useRows = atoi(e);
         SDRGPU_CHECK(init_stream());
         SDRGPU_CHECK(set_taps(t, n));
         return SDRGPU_OK;
@@ -1568,6 +1581,16 @@ extern "C" int sdrgpu_ddc_fm_create(sdrgpu_block** h, int device, double offsetR
     return wrap(h, f.release(), rc);
 }
 
+// Fused DDC without the demodulator: FrequencyXlator(offsetRad) -> DecimatingFIR<complex_t,float>
+// (frequency_xlator.h:43-50, decimating_fir.h:45-68), complex_t out. The same kernels as the fused
+// DDC+FM block with the quadrature epilogue off (RxVFO's first stage has this shape too).
+extern "C" int sdrgpu_ddc_create(sdrgpu_block** h, int device, double offsetRad, const float* taps, int ntaps, int decim) {
+    if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
+    int rc;
+    auto f = make_fir(device, SDRGPU_C64, SDRGPU_F32, taps, ntaps, decim, &rc, true, xlator_effective_omega(offsetRad));
+    return wrap(h, f.release(), rc);
+}
+
 // FM<float> (demod/fm.h:25-133): quadrature(bw/2) -> optional LPF/HPF/BPF
 extern "C" int sdrgpu_fm_create(sdrgpu_block** h, int device, double samplerate, double bandwidth, int lowPass, int highPass) {
     if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
@@ -1629,7 +1652,10 @@ extern "C" int sdrgpu_block_process_dev(sdrgpu_block* h, const void* in, int cou
     NEED_HANDLE(h);
     if (count < 0 || (count > 0 && (!in || !out))) { set_error("process: bad buffers"); return SDRGPU_EARG; }
     Block* b = h->impl;
-    return b->run(in, count, out, stream ? (hipStream_t)stream : b->own);
+    const hipStream_t s = stream ? (hipStream_t)stream : b->own;
+    SDRGPU_SET_DEVICE(b->device);
+    SDRGPU_CHECK(b->order.follow(s));
+    return b->run(in, count, out, s);
 }
 
 extern "C" int sdrgpu_block_process(sdrgpu_block* h, const void* in, int count, void* out) {
@@ -1654,8 +1680,10 @@ extern "C" int sdrgpu_block_process(sdrgpu_block* h, const void* in, int count, 
             std::memcpy(b->pin_in.p, in, (size_t)count * esize(b->in_dtype));
             src = b->pin_in.p;
         }
+        SDRGPU_CHECK(b->order.follow(b->own));
         SDRGPU_HIP(hipMemcpyAsync(b->dev_in.p, src, (size_t)count * esize(b->in_dtype), hipMemcpyHostToDevice, b->own));
     }
+    SDRGPU_CHECK(b->order.follow(b->own));
     int m = b->run(b->dev_in.p, count, b->dev_out.p, b->own);
     if (m < 0) return m;
     void* dst = (outPinned && m <= mExp) ? out : b->pin_out.p;

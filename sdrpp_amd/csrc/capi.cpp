@@ -1,10 +1,19 @@
 // C ABI: runtime helpers and the host-side design entry points of libsdrgpu.
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include "sdrgpu_internal.h"
 
 namespace sdrgpu { const char* last_error(); }
 using namespace sdrgpu;
+
+namespace sdrgpu {
+const char* tuning_env(const char* name) {
+    const char* t = std::getenv("SDRGPU_TUNING");
+    if (!t || t[0] != '1' || t[1] != 0) return nullptr;
+    return std::getenv(name);
+}
+}  // namespace sdrgpu
 
 extern "C" int sdrgpu_version(void) { return SDRGPU_VERSION; }
 extern "C" const char* sdrgpu_last_error(void) { return last_error(); }

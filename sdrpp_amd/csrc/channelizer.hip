@@ -217,8 +217,8 @@ struct ChannelizerBlock : Block {
         M = channels;
         ntaps = n;
         Hp = CHAN_Q * M - 1;
-        if (const char* e = getenv("SDRGPU_CHAN_FPW")) fpw = std::max(16, atoi(e) / 16 * 16);
-        if (const char* e = getenv("SDRGPU_CHAN_TWO")) two = atoi(e) != 0;
+        if (const char* e = tuning_env("SDRGPU_CHAN_FPW")) fpw = std::max(16, atoi(e) / 16 * 16);
+        if (const char* e = tuning_env("SDRGPU_CHAN_TWO")) two = atoi(e) != 0;
         SDRGPU_CHECK(init_stream());
         std::vector<float> pq((size_t)CHAN_Q * M, 0.0f);       // [q][r] = h[q M + r]
         for (int j = 0; j < n; j++) pq[j] = t[j];

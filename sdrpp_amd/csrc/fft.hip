@@ -21,9 +21,20 @@
 
 namespace sdrgpu {
 
+// K3, volk_32fc_s32f_power_spectrum_32f(out, X, 1.0, N): 10*log10(re^2 + im^2).
+// VOLK evaluates 10 * log10f(p) in fp32, which adds about one ulp of the dB value on top of the
+// FFT's own error (median 1 ulp vs the correctly rounded dB of the exact DFT). Here the exponent
+// of p is split off exactly (p = m 2^e, m in [0.5, 1)), only log2(m) is taken in fp32 (absolute
+// error ~1e-7), and e + log2(m) is scaled by 10 log10(2) in fp64 and rounded once: the dB row
+// then carries the FFT's error only (median 0 ulp, same class as pocketfft + an exact log;
+// tests/test_gpu_parity.py::test_spectrum_ulp_distribution). Three fp64 ops per bin in a
+// memory-bound epilogue. p = 0 gives -inf like log10f.
 __device__ __forceinline__ float db_of(float2 X) {
-    // volk_32fc_s32f_power_spectrum_32f(out, X, 1.0, N): 10*log10(re^2 + im^2)
-    return 10.0f * log10f(X.x * X.x + X.y * X.y);
+    const float p = X.x * X.x + X.y * X.y;
+    int e;
+    const float m = frexpf(p, &e);
+    const double l = (double)e + (double)__builtin_amdgcn_logf(m);   // v_log_f32: log2, m normal or 0
+    return (float)(3.0102999566398119521 * l);
 }
 
 // Persistent tile loop shared by the three spectrum kernels. Each workgroup walks tiles
@@ -100,32 +111,12 @@ template <int L, int S>
 __device__ __forceinline__ void passA_tile(
     float2* lds, int tile, const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win,
     int nz, int N2, int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull,
-    float2* __restrict__ scratch, int dbg) {
+    float2* __restrict__ scratch) {
     const int tid = threadIdx.x;
     const int c = tid % S, t = tid / S;
     constexpr int T = L / 16;
     const int nb = N2 / S;                        // column blocks per frame
     const int ntiles = nb * frames;
-    if (dbg & 16) {   // timing ablation only: the same loads and stores, no transform
-        if (tile >= ntiles) return;
-        const int b = tile % nb;
-        const long long f = tile / nb;
-        const float2* x = in + f * frameStride;
-        float2 v[16];
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const long long n = (long long)(t + r * T) * N2 + b * S + c;
-            const float w = (dbg & 1) ? 1.0f : win[n];
-            v[r] = make_float2(x[n].x * w, x[n].y * w);
-        }
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const long long o = (long long)(t + r * T) * N2 + b * S + c;
-            const float2 t0 = (dbg & 2) ? make_float2(1.f, 0.f) : tfull[o];
-            scratch[(f << logN) + o] = cmul(v[r], t0);
-        }
-        return;
-    }
     if constexpr (L == 256) {
         // 256-point columns: both stages are radix 16, so the whole column is one LDS exchange.
         // Every global read is issued up front (input, window, the exact four-step twiddles of
@@ -153,7 +144,7 @@ __device__ __forceinline__ void passA_tile(
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 xv[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, o0 * 8, r * rowB, 0));
-                wv[r] = (dbg & 1) ? 1.0f : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, o0 * 4, r * rowB / 2, 0));
+                wv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, o0 * 4, r * rowB / 2, 0));
             }
         } else {              // zero-padded tail: clamped (in-bounds) loads, then select
 #pragma unroll
@@ -164,14 +155,13 @@ __device__ __forceinline__ void passA_tile(
                 const float2 xe = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, nc * 8, 0, 0));
                 const float we = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, nc * 4, 0, 0));
                 xv[r] = live ? xe : make_float2(0.0f, 0.0f);
-                wv[r] = live ? ((dbg & 1) ? 1.0f : we) : 0.0f;
+                wv[r] = live ? we : 0.0f;
             }
         }
         for (int i = tid; i < L; i += S * T) twl[i] = tw[i];
 #pragma unroll
         for (int r = 0; r < 16; r++)   // exact W_N^(n2 k1), k1 = t + 16 r: same offsets as the input rows
-            tt[r] = (dbg & 2) ? make_float2(1.f, 0.f)
-                              : __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rt, o0 * 8, r * rowB, 0));
+            tt[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rt, o0 * 8, r * rowB, 0));
         float2 v[16];
 #pragma unroll
         for (int r = 0; r < 16; r++) v[r] = make_float2(xv[r].x * wv[r], xv[r].y * wv[r]);
@@ -206,7 +196,7 @@ __device__ __forceinline__ void passA_tile(
                 const bool live = n < nz;
                 const long long nc = live ? n : 0;   // frame[0]: always in bounds
                 fr.x[r] = x[nc];
-                fr.w[r] = live ? ((dbg & 1) ? 1.0f : win[nc]) : 0.0f;
+                fr.w[r] = live ? win[nc] : 0.0f;
             }
         },
         [&](const FragW& fr, float2 (&v)[16]) {
@@ -216,7 +206,7 @@ __device__ __forceinline__ void passA_tile(
         [&](int tile, int k1, float2 y) {
             const int b = tile % nb;
             const long long f = tile / nb;
-            const float2 t0 = (dbg & 2) ? make_float2(1.f, 0.f) : tfull[(long long)k1 * N2 + b * S + c];   // exact W_N^(n2 k1)
+            const float2 t0 = tfull[(long long)k1 * N2 + b * S + c];   // exact W_N^(n2 k1)
             scratch[(f << logN) + (long long)k1 * N2 + b * S + c] = cmul(y, t0);
         });
 }
@@ -225,9 +215,9 @@ template <int L, int S>
 __global__ __launch_bounds__(S * L / 16) __attribute__((amdgpu_waves_per_eu(4))) void fft_passA_kernel(
     const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
     int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull,
-    float2* __restrict__ scratch, int dbg) {
+    float2* __restrict__ scratch) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    passA_tile<L, S>(lds, blockIdx.x, in, frameStride, frames, win, nz, N2, logN, tw, tfull, scratch, dbg);
+    passA_tile<L, S>(lds, blockIdx.x, in, frameStride, frames, win, nz, N2, logN, tw, tfull, scratch);
 }
 
 // ---- pass A, paired columns: S columns x N1 rows per tile, two adjacent columns per lane --
@@ -313,8 +303,7 @@ __device__ __forceinline__ void stages_rest_v(float2* seq0, const float2* twl, i
 template <int L, int S>
 __device__ __forceinline__ void passA2_tile(
     float2* lds, int tile, const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win,
-    int nz, int N2, int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull, float2* __restrict__ scratch,
-    int dbg) {
+    int nz, int N2, int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull, float2* __restrict__ scratch) {
     constexpr int P = S / 2, T = L / 16, NT = P * T, LS = Lds<L>::LS;
     float2* twl = lds + S * LS;
     const int tid = threadIdx.x;
@@ -331,8 +320,8 @@ __device__ __forceinline__ void passA2_tile(
     for (int r = 0; r < 16; r++) {
         const long long n = (long long)(t + r * T) * N2 + col;
         if (n + 1 < nz) {
-            q[r] = *reinterpret_cast<const float4*>(x + ((dbg & 4) ? (long long)b * S * L + (long long)(r * NT + tid) * 2 : n));
-            w[r] = (dbg & 1) ? make_float2(1.0f, 1.0f) : *reinterpret_cast<const float2*>(win + n);
+            q[r] = *reinterpret_cast<const float4*>(x + n);
+            w[r] = *reinterpret_cast<const float2*>(win + n);
         } else {   // zero-padded tail (n >= nz) or the one pair straddling nz
             const bool live = n < nz;
             const float2 e = x[live ? n : 0];
@@ -359,20 +348,18 @@ __device__ __forceinline__ void passA2_tile(
     float2* dst = scratch + (f << logN);
     stages_rest_v<L, 2>(seq0, twl, t, [&](int k1, float2 (&y)[2]) {
         const long long o = (long long)k1 * N2 + col;
-        const float4 tt = (dbg & 2) ? make_float4(1.f, 0.f, 1.f, 0.f) : *reinterpret_cast<const float4*>(tfull + o);
+        const float4 tt = *reinterpret_cast<const float4*>(tfull + o);
         const float2 a = cmul(y[0], make_float2(tt.x, tt.y)), c = cmul(y[1], make_float2(tt.z, tt.w));
-        // (dbg & 8: tile-contiguous store, timing ablation only)
-        const long long od = (dbg & 8) ? (long long)b * S * L + (long long)k1 * S + 2 * cp : o;
-        *reinterpret_cast<float4*>(dst + od) = make_float4(a.x, a.y, c.x, c.y);
+        *reinterpret_cast<float4*>(dst + o) = make_float4(a.x, a.y, c.x, c.y);
     });
 }
 
 template <int L, int S>
 __global__ __launch_bounds__(S / 2 * L / 16) void fft_passA2_kernel(
     const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
-    int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull, float2* __restrict__ scratch, int dbg) {
+    int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull, float2* __restrict__ scratch) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    passA2_tile<L, S>(lds, blockIdx.x, in, frameStride, frames, win, nz, N2, logN, tw, tfull, scratch, dbg);
+    passA2_tile<L, S>(lds, blockIdx.x, in, frameStride, frames, win, nz, N2, logN, tw, tfull, scratch);
 }
 
 // ---- pass B: S rows of length N2 per tile, dB out, transposed store -----------------
@@ -431,9 +418,9 @@ __global__ __launch_bounds__((PAIRED ? SA / 2 : SA) * LA / 16) __attribute__((am
     if ((int)blockIdx.x < nB) {
         passB_tile<LB, SB>(lds, blockIdx.x, scratchB, framesB, LA, logN, tw2, outB);
     } else if constexpr (PAIRED) {
-        passA2_tile<LA, SA>(lds, blockIdx.x - nB, in, frameStride, framesA, win, nz, LB, logN, tw1, tfull, scratchA, 0);
+        passA2_tile<LA, SA>(lds, blockIdx.x - nB, in, frameStride, framesA, win, nz, LB, logN, tw1, tfull, scratchA);
     } else {
-        passA_tile<LA, SA>(lds, blockIdx.x - nB, in, frameStride, framesA, win, nz, LB, logN, tw1, tfull, scratchA, 0);
+        passA_tile<LA, SA>(lds, blockIdx.x - nB, in, frameStride, framesA, win, nz, LB, logN, tw1, tfull, scratchA);
     }
 }
 
@@ -444,7 +431,6 @@ struct FftPlan {
     DevBuf win, tw1, tw2, tfull, scratch;
     int chunkFrames = 1;
     int sa = 16, sb = 32;             // pass-A columns / pass-B rows per workgroup (tuning)
-    int dbg = 0;                      // timing-only ablations (SDRGPU_FFT_DEBUG; wrong results)
     float2* cur = nullptr;            // scratch buffer of the chunk being launched
     int sa2 = 0;                      // paired pass-A columns per workgroup (0: paired kernel off)
     hipStream_t own = nullptr;
@@ -458,6 +444,7 @@ struct FftPlan {
     // merged pass-B(c) + pass-A(c+1) launches (64k split): one launch boundary per chunk
     // instead of two; 1.87 -> 1.73 ms per 2^28 samples (A/B on one box). SDRGPU_FFT_MERGE=0 off.
     int merge = 1;
+    StreamOrder order;                // scratch is per plan: calls on different streams are serialised
     hipStream_t s2 = nullptr;
     hipEvent_t evFork = nullptr, evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr};
     DevBuf scratch2;
@@ -501,7 +488,7 @@ static int launch_passA(const FftPlan& p, const float2* in, long long stride, in
     SDRGPU_CHECK(set_lds(k, lds));
     const int g = (p.N2 / S) * frames;
     hipLaunchKernelGGL(k, dim3(g), dim3(S * L / 16), lds, s, in, stride, frames, p.win.as<float>(), p.nz, p.N2,
-                       p.logN, p.tw1.as<float2>(), p.tfull.as<float2>(), p.cur, p.dbg);
+                       p.logN, p.tw1.as<float2>(), p.tfull.as<float2>(), p.cur);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
@@ -514,7 +501,7 @@ static int launch_passA2(const FftPlan& p, const float2* in, long long stride, i
     SDRGPU_CHECK(set_lds(k, lds));
     const int g = (p.N2 / S) * frames;
     hipLaunchKernelGGL(k, dim3(g), dim3(S / 2 * L / 16), lds, s, in, stride, frames, p.win.as<float>(), p.nz, p.N2,
-                       p.logN, p.tw1.as<float2>(), p.tfull.as<float2>(), p.cur, p.dbg);
+                       p.logN, p.tw1.as<float2>(), p.tfull.as<float2>(), p.cur);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
@@ -658,7 +645,7 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         rc = make_twiddles(p.tw1, fftSize);
     } else {
         p.N1 = 1 << ((logN + 1) / 2);   // N1 >= N2, both <= 1024
-        if (const char* e = getenv("SDRGPU_FFT_N1")) {   // (tuning) another split, N1, N2 in [64, 1024]
+        if (const char* e = tuning_env("SDRGPU_FFT_N1")) {   // (tuning) another split, N1, N2 in [64, 1024]
             const int n1 = atoi(e);
             if (n1 >= 64 && n1 <= 1024 && (n1 & (n1 - 1)) == 0 && fftSize / n1 >= 64 && fftSize / n1 <= 1024) p.N1 = n1;
         }
@@ -670,22 +657,21 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         // resident in the Infinity Cache: 128 MB of intermediate per chunk (64 and 192-256 MB
         // measured 2-5% slower for 64k with merged launches; 1M: 2.32 vs 2.39 ms at 64 MB)
         long long chunkMB = 128;
-        if (const char* e = getenv("SDRGPU_FFT_CHUNK_MB")) chunkMB = std::max(1, atoi(e));
+        if (const char* e = tuning_env("SDRGPU_FFT_CHUNK_MB")) chunkMB = std::max(1, atoi(e));
         // 64k (256 x 256): 32 columns / 32 rows per workgroup (256-B pass-A row segments, 128-B
         // pass-B dB segments, 512 threads, 2 workgroups per CU): the merged spectrum launches
         // take 1.44 vs 1.58 ms per 2^28 samples with 16 / 16 (A/B on one box)
         if (p.N1 == 256 && p.N2 == 256) p.sa = p.sb = 32;
-        if (const char* e = getenv("SDRGPU_FFT_SA")) p.sa = atoi(e);
-        if (const char* e = getenv("SDRGPU_FFT_SB")) p.sb = atoi(e);
-        if (const char* e = getenv("SDRGPU_FFT_DEBUG")) p.dbg = atoi(e);
-        if (const char* e = getenv("SDRGPU_FFT_PIPE")) p.pipe = atoi(e);
-        if (const char* e = getenv("SDRGPU_FFT_MERGE")) p.merge = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_SA")) p.sa = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_SB")) p.sb = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_PIPE")) p.pipe = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_MERGE")) p.merge = atoi(e);
         p.chunkFrames = std::max(1, (int)((chunkMB << 20) / ((long long)fftSize * 8)));
         // paired-column pass A: +13% on the 1M transform (N1 = 1024), but slower than the
         // one-column kernel at N1 = 256 (64k: 2.05-2.10 vs 1.86 ms per 2^28 samples, A/B on
         // one box), so it is the default only for N1 >= 512
         p.sa2 = p.N1 >= 512 ? 16 : 0;
-        if (const char* e = getenv("SDRGPU_FFT_SA2")) p.sa2 = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_SA2")) p.sa2 = atoi(e);
         if (rc >= 0) {   // Tfull[k1][n2] = W_N^(n2 k1), exact argument mod N (both pass-A kernels)
             std::vector<float2> t((size_t)fftSize);
             for (int k1 = 0; k1 < p.N1; k1++)
@@ -733,6 +719,7 @@ extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long f
     FftPlan& p = h->p;
     SDRGPU_SET_DEVICE(p.device);
     hipStream_t s = stream ? (hipStream_t)stream : p.own;
+    SDRGPU_CHECK(p.order.follow(s));
     const float2* x = (const float2*)in;
     if (p.N1 == 0) {
         SDRGPU_CHECK(dispatch_single(p, x, frameStride, frames, out, s));

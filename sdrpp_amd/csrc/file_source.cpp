@@ -88,6 +88,15 @@ int wav_parse(sdrgpu_wav* w) {
     }
     w->dataOffset = data ? std::ftell(f) : w->fileSize;
     if (!fmt || !data || w->blockAlign <= 0) { set_error("wav: no fmt or data chunk"); return SDRGPU_EARG; }
+    // The reference's workers read the sample region as a packed stream of channels x bits/8-byte
+    // frames (readSamples into inBuf, main.cpp:320-537) and use wBlockAlign only to count frames
+    // (wavreader.h:85-88). A block align other than that frame size (padded or malformed) would
+    // frame the samples differently from the converters, so such files are rejected; every read
+    // below is sized by blockAlign == the packed frame size the callers allocate.
+    if (w->bits <= 0 || (w->bits % 8) != 0 || w->channels <= 0 || w->blockAlign != w->channels * (w->bits / 8)) {
+        set_error("wav: block align %d != channels (%d) x bytes per sample (%d bit)", w->blockAlign, w->channels, w->bits);
+        return SDRGPU_EARG;
+    }
     return SDRGPU_OK;
 }
 }  // namespace
@@ -134,7 +143,8 @@ extern "C" int sdrgpu_wav_block_size(sdrgpu_wav* w) {
     return std::max(1, (int)std::min<long long>(w->sampleRate / 200, 1000000));   // STREAM_BUFFER_SIZE
 }
 
-// next block of at most maxFrames sample frames, raw bytes into out (maxFrames * blockAlign bytes);
+// next block of at most maxFrames sample frames, raw bytes into out (maxFrames * blockAlign bytes, where
+// blockAlign = channels * bits / 8 is checked at open);
 // returns the frames read, 0 at the end of the file
 extern "C" int sdrgpu_wav_read(sdrgpu_wav* w, void* out, int maxFrames) {
     if (!w || (!out && maxFrames > 0) || maxFrames < 0) { set_error("wav_read: bad argument"); return SDRGPU_EARG; }

@@ -45,6 +45,7 @@ struct sdrgpu_frontend {
     int decim = 1, fftSize = 0, window = 0, nz = 0, skip = 0;
     bool dcBlocking = false, invertIQ = false;
     hipStream_t s = nullptr;
+    StreamOrder order;        // tails, stitch and VFO state are per front end: serialise across streams
     sdrgpu_block* decimB = nullptr;
     sdrgpu_block* dcb = nullptr;
     sdrgpu_fft* fft = nullptr;
@@ -293,6 +294,7 @@ extern "C" int sdrgpu_frontend_push_dev(sdrgpu_frontend* f, const void* in, int 
     if (count < 0 || (count > 0 && !in) || kind < -1 || kind > SDRGPU_CONV_F32) { set_error("frontend_push: bad argument"); return SDRGPU_EARG; }
     SDRGPU_SET_DEVICE(f->device);
     hipStream_t s = stream ? (hipStream_t)stream : f->s;
+    SDRGPU_CHECK(f->order.follow(s));
     const float2* x = (const float2*)in;
     if (kind >= 0 && count > 0) {
         SDRGPU_CHECK(f->conv.ensure(sizeof(float2) * count));

@@ -12,6 +12,12 @@ bool host_pinned(const void* p, size_t bytes);   // inside a sdrgpu_host_registe
 
 void set_error(const char* fmt, ...);
 
+// Kernel-selection / tile-shape overrides for A/B measurements (SDRGPU_FIR_*, SDRGPU_FFT_*,
+// SDRGPU_CHAN_*). They are read only when SDRGPU_TUNING=1 is set as well, so a stray variable
+// in a deployment cannot change the kernels that run. Every override selects another exact
+// kernel or tile shape of the same transform (none of them trades correctness for speed).
+const char* tuning_env(const char* name);
+
 #define SDRGPU_HIP(call)                                                              \
     do {                                                                              \
         hipError_t e_ = (call);                                                       \
@@ -60,6 +66,17 @@ struct PinnedBuf {
 
 inline size_t esize(int dtype) { return dtype == SDRGPU_C64 ? 8 : 4; }
 
+// A handle's device state is rewritten by every call (NCO coarse table, history / quadrature
+// ping-pong buffers, FFT scratch), so calls must not overlap. Calls on one stream are ordered by
+// the stream; a call on another stream than the previous one first makes its stream wait for
+// the previous call's work (one event, recorded only on a stream change).
+struct StreamOrder {
+    hipStream_t last = nullptr;
+    hipEvent_t ev = nullptr;
+    int follow(hipStream_t s);
+    ~StreamOrder();
+};
+
 // ---- host-side design (host_design.cpp) -----------------------------------
 double window_value(int type, double n, double N);
 int create_window(int type, float* buffer, int size, int centered);
@@ -88,6 +105,7 @@ struct Block {
     hipStream_t own = nullptr;
     PinnedBuf pin_in, pin_out;
     DevBuf dev_in, dev_out;
+    StreamOrder order;   // entry points (process / process_dev) only; sub-blocks share the caller's stream
     virtual ~Block();
     int init_stream();
     // exact number of outputs the next process() of `count` inputs yields

@@ -153,6 +153,16 @@ class RxVFO(Block):
         check(lib.sdrgpu_rxvfo_set_offset(self._h, float(offset)))
 
 
+class DDC(Block):
+    """Fused FrequencyXlator -> DecimatingFIR<complex_t,float> (complex out): the FIR stage of DDCFM."""
+
+    def __init__(self, offset_rad, taps, decim, device=0):
+        t = np.ascontiguousarray(taps, dtype=np.float32)
+        self._taps = t
+        h = _make(lib.sdrgpu_ddc_create, device, float(offset_rad), _fptr(t), int(t.shape[0]), int(decim))
+        super().__init__(h, np.complex64, np.complex64)
+
+
 class DDCFM(Block):
     """Fused FrequencyXlator -> DecimatingFIR<complex_t,float> -> Quadrature (BASELINE config C3)."""
 

@@ -55,6 +55,34 @@ def db_check(db_gpu, power_true, N, ref32_db=None, floor_db=60.0):
     return err.max(), nerr
 
 
+def db_ulp_errors(db, power_true, floor_db=60.0):
+    """|db - db_true| in units of the fp32 ulp of the true dB value (db_true = 10 log10 of the fp64
+    power, rounded once to fp32), on bins within `floor_db` of the frame peak. This is the
+    north_star's "<= 1 ulp on FFT magnitude" measured literally: a value of 1 means the dB row is
+    one fp32 step from the correctly rounded dB of the exact DFT."""
+    t64 = 10.0 * np.log10(np.maximum(np.asarray(power_true, np.float64), 1e-300))
+    sel = t64 >= t64.max() - floor_db
+    t32 = t64[sel].astype(np.float32)
+    ulp = np.spacing(np.abs(t32)).astype(np.float64)
+    return np.abs(np.asarray(db, np.float32)[sel].astype(np.float64) - t32.astype(np.float64)) / ulp
+
+
+def ulp_summary(e):
+    return {"bins": int(e.size), "p50": float(np.percentile(e, 50)), "p90": float(np.percentile(e, 90)),
+            "p99": float(np.percentile(e, 99)), "max": float(e.max()), "frac_le_1ulp": float(np.mean(e <= 1.0))}
+
+
+def write_report(name, obj):
+    """Append a JSON line to $SDRGPU_REPORT_DIR/<name>.jsonl when that directory is set (GPU
+    sessions copy these into profiles/)."""
+    import json
+    d = os.environ.get("SDRGPU_REPORT_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name + ".jsonl"), "a") as f:
+            f.write(json.dumps(obj) + "\n")
+
+
 def ref32_fft_db(x, nz, N, window):
     """A reference-class fp32 FFT (pocketfft single precision via scipy) on the windowed frame."""
     import scipy.fft

@@ -13,8 +13,8 @@ from sdrpp_amd import dsp
 PCM, IEEE_FLOAT, EXTENSIBLE = 1, 3, 0xFFFE
 
 
-def fmt_chunk(tag, ch, sr, bits, size=16, subformat=None):
-    align = ch * bits // 8
+def fmt_chunk(tag, ch, sr, bits, size=16, subformat=None, align=None):
+    align = ch * bits // 8 if align is None else align
     body = struct.pack("<HHIIHH", tag, ch, sr, sr * align, align, bits)
     if size == 18:
         body += struct.pack("<H", 0)
@@ -25,12 +25,13 @@ def fmt_chunk(tag, ch, sr, bits, size=16, subformat=None):
     return b"fmt " + struct.pack("<I", len(body)) + body
 
 
-def write_wav(path, data, tag, ch, sr, bits, fmt_size=16, subformat=None, rf64=False, before=b"", after=b""):
+def write_wav(path, data, tag, ch, sr, bits, fmt_size=16, subformat=None, rf64=False, before=b"", after=b"",
+              align=None):
     """A WAVE file: [ds64] fmt [extra chunk] data [trailing chunk]."""
     chunks = b""
     if rf64:
         chunks += b"ds64" + struct.pack("<I", 28) + struct.pack("<QQQI", 0, len(data), 0, 0)
-    chunks += fmt_chunk(tag, ch, sr, bits, fmt_size, subformat) + before
+    chunks += fmt_chunk(tag, ch, sr, bits, fmt_size, subformat, align) + before
     chunks += b"data" + struct.pack("<I", len(data)) + data + after
     head = (b"RF64" if rf64 else b"RIFF") + struct.pack("<I", 4 + len(chunks)) + b"WAVE"
     path.write_bytes(head + chunks)
@@ -88,6 +89,18 @@ def test_wav_rejects(tmp_path):
         dsp.WavFile(write_wav(tmp_path / "e.wav", x[:12], PCM, 3, 8000, 16))
     with pytest.raises(sdrpp_amd.SdrGpuError):        # 12-bit PCM: not a supported sample format
         dsp.WavFile(write_wav(tmp_path / "f.wav", x, PCM, 2, 8000, 12))
+
+
+@pytest.mark.parametrize("align", [8, 5, 2, 0])
+def test_wav_rejects_block_align_mismatch(align, tmp_path):
+    """wBlockAlign must equal channels x bits / 8: the reference workers read the sample region as
+    a packed stream of such frames (main.cpp:320-537), so a padded or malformed block align is
+    rejected at open instead of framing (or over-reading) the samples by it."""
+    x = np.zeros(64, np.int16).tobytes()
+    with pytest.raises(sdrpp_amd.SdrGpuError):
+        dsp.WavFile(write_wav(tmp_path / "g.wav", x, PCM, 2, 8000, 16, align=align))
+    ok = dsp.WavFile(write_wav(tmp_path / "h.wav", x, PCM, 2, 8000, 16, align=4))
+    assert ok.sample_count == 32 and ok.read().size == 128
 
 
 @pytest.mark.gpu

@@ -6,7 +6,8 @@ import pytest
 import oracle
 import sdrpp_amd
 from sdrpp_amd import dsp
-from _util import GOLDEN, assert_close_c, db_check, fir_atol, iq, ref32_fft_db
+from _util import (EPS32, GOLDEN, assert_close_c, db_check, db_ulp_errors, fir_atol, iq, ref32_fft_db,
+                   ulp_summary, write_report)
 
 pytestmark = pytest.mark.gpu
 
@@ -237,27 +238,94 @@ def test_rxvfo_c5(rng):
         assert_close_c(yg, yo, 5e-5, "rxvfo")
 
 
+def _quad_bound(y_ref, y_prev0, e_fir, inv_dev):
+    """Per-sample bound on the quadrature output (quadrature.h:41-56) of an FIR output stream
+    known to within e_fir (absolute) of y_ref: an error e in y_i turns arg(y_i) by at most
+    ~e/|y_i|, so |d out_i| <= [2 (e/|y_i| + e/|y_i-1|) + 8 eps pi] / dev (factor 2 = slack on the
+    first-order term; 8 eps pi covers atan2f and the fp32 conjugate product)."""
+    y = np.asarray(y_ref, np.complex128)
+    yp = np.concatenate([[y_prev0], y[:-1]])
+    with np.errstate(divide="ignore"):
+        b = 2.0 * (e_fir / np.abs(y) + e_fir / np.abs(yp)) + 8 * EPS32 * np.pi
+    return b * inv_dev
+
+
+def _wrapped_diff(a, b, inv_dev):
+    """|a - b| for quadrature outputs, modulo the 2 pi / dev wrap of atan2."""
+    d = (np.asarray(a, np.float64) - np.asarray(b, np.float64)) / inv_dev
+    return np.abs(np.angle(np.exp(1j * d))) * inv_dev
+
+
+def test_ddc_c3_fir_stage(rng):
+    """The C3 kernel's FIR stage (xlator fused into the load, 256 taps, D = 8, f32 MFMA) on its own,
+    complex out: every output within fir_atol of the oracle's xlator -> fp64-accumulated FIR."""
+    fs = 61.44e6
+    taps = dsp.low_pass(3.0e6, 912000.0, fs)
+    w = 2 * np.pi * (-1.5e6 / fs)
+    g = dsp.DDC(w, taps, 8)
+    ox, of = oracle.Xlator(w), oracle.FIR(taps, 8)
+    for n in [307200, 12345, 8, 500000, 7, 1 << 20]:
+        x = iq(rng, n)
+        yo = of.process(ox.process(x))
+        yg = g.process(x)
+        assert len(yg) == len(yo)
+        assert_close_c(yg, yo, fir_atol(taps, x) if n else 0, "C3 FIR stage")
+
+
+def _quad64(y, yprev0, inv_dev):
+    """fp64 quadrature (quadrature.h:41-56) of an FIR output stream."""
+    y = np.asarray(y, np.complex128)
+    yp = np.concatenate([[yprev0], y[:-1]])
+    return np.angle(y * np.conj(yp)) * inv_dev
+
+
 def test_ddc_fm_c3(rng):
+    """C3 fused xlator -> 256-tap FIR /8 -> quadrature, every output checked three ways:
+    1. the kernel's FIR stage (sdrgpu_ddc_create: the same fused kernel, complex out) is within
+       fir_atol of the oracle's xlator -> fp64-accumulated FIR;
+    2. the fused quadrature epilogue agrees with the fp64 quadrature of that FIR stage's output
+       within _quad_bound(e = the FIR stage's measured error): the quadrature kernel tiles by 1023
+       outputs, the plain one by 1024, so an output's MFMA tap grouping (hence its last bits)
+       differs between the two, which matters only where |y| is small;
+    3. against the oracle's own quadrature, each output lies within _quad_bound with e = 2x the
+       FIR stage's measured error.
+    A wrong output anywhere (e.g. one per 1024-output tile) fails 2 (and 1 if it is in the FIR)."""
     fs = 61.44e6
     taps = dsp.low_pass(3.0e6, 912000.0, fs)
     w = 2 * np.pi * (-1.5e6 / fs)
     dev = 2 * np.pi * 100e3 / (fs / 8)
-    g = dsp.DDCFM(w, taps, 8, dev)
+    inv = 1.0 / dev
+    g, gf = dsp.DDCFM(w, taps, 8, dev), dsp.DDC(w, taps, 8)
     ox, of, oq = oracle.Xlator(w), oracle.FIR(taps, 8), oracle.Quadrature(dev)
-    for n in [307200, 12345, 8, 500000]:
+    yprev = gprev = 0j
+    worst = {"fir_err": 0.0, "epilogue_over_bound": 0.0, "err_over_bound": 0.0}
+    for n in [307200, 12345, 8, 500000, 7, 1 << 20]:
         x = iq(rng, n)
-        yo = oq.process(of.process(ox.process(x)))
-        yg = g.process(x)
-        assert len(yg) == len(yo)
-        # atan2 of an fp32 FIR output: the phase error scales with 1/|y|; bound it on samples
-        # whose |y| is not tiny and check the global fraction
-        assert np.mean(np.abs(yg - yo) < 1e-3) > 0.999
+        yf = of.process(ox.process(x))
+        yo = oq.process(yf)
+        yg, ygf = g.process(x), gf.process(x)
+        assert len(yg) == len(yo) == len(yf) == len(ygf)
+        if len(yf) == 0:
+            continue
+        e_fir = max(float(np.abs(ygf.astype(np.complex128) - yf).max()), 1e-9)
+        ep = _wrapped_diff(yg, _quad64(ygf, gprev, inv), inv) / _quad_bound(ygf, gprev, 2 * e_fir, inv)
+        r = _wrapped_diff(yg, yo, inv) / _quad_bound(yf, yprev, 2 * e_fir, inv)
+        worst["fir_err"] = max(worst["fir_err"], e_fir)
+        worst["epilogue_over_bound"] = max(worst["epilogue_over_bound"], float(ep.max()))
+        worst["err_over_bound"] = max(worst["err_over_bound"], float(r.max()))
+        assert e_fir <= fir_atol(taps, x), (n, e_fir)
+        assert ep.max() <= 1.0, (n, int(np.sum(ep > 1)), np.nonzero(ep > 1)[0][:5])
+        assert r.max() <= 1.0, (n, int(np.sum(r > 1)), np.nonzero(r > 1)[0][:5])
+        yprev, gprev = complex(yf[-1]), complex(ygf[-1])
+    write_report("c3_quadrature_bound", {"test": "test_ddc_fm_c3", **worst})
 
 
 @pytest.mark.parametrize("ntaps,quad", [(256, True), (256, False), (150, False), (190, True)])
 def test_rows_kernel_d8_on_request(ntaps, quad, rng, monkeypatch):
     # fir_rows_kernel at D = 8 (taps per phase padded to 16/24/32, optional fused quadrature) is
-    # selected only with SDRGPU_FIR_ROWS=2 (read at block creation); check it against the oracle
+    # selected only with SDRGPU_TUNING=1 SDRGPU_FIR_ROWS=2 (read at block creation); check it
+    # against the oracle with the same per-sample bounds as the default C3 kernel
+    monkeypatch.setenv("SDRGPU_TUNING", "1")
     monkeypatch.setenv("SDRGPU_FIR_ROWS", "2")
     fs = 61.44e6
     taps = dsp.low_pass(3.0e6, 912000.0, fs) if ntaps == 256 else (rng.standard_normal(ntaps) / ntaps).astype(np.float32)
@@ -265,12 +333,17 @@ def test_rows_kernel_d8_on_request(ntaps, quad, rng, monkeypatch):
     dev = 2 * np.pi * 100e3 / (fs / 8)
     g = dsp.DDCFM(w, taps, 8, dev) if quad else dsp.FIR(taps, 8)
     ox, of, oq = oracle.Xlator(w), oracle.FIR(taps, 8), oracle.Quadrature(dev)
+    yprev = 0j
     for n in [307200, 12345, 8, 500000]:
         x = iq(rng, n)
         if quad:
-            yo, yg = oq.process(of.process(ox.process(x))), g.process(x)
+            yf = of.process(ox.process(x))
+            yo, yg = oq.process(yf), g.process(x)
             assert len(yg) == len(yo)
-            assert np.mean(np.abs(yg - yo) < 1e-3) > 0.999
+            bound = _quad_bound(yf, yprev, fir_atol(taps, x), 1.0 / dev)
+            err = _wrapped_diff(yg, yo, 1.0 / dev)
+            assert np.all(err <= bound), (n, int(np.sum(err > bound)))
+            yprev = complex(yf[-1])
         else:
             yo, yg = of.process(x), g.process(x)
             assert len(yg) == len(yo)
@@ -384,9 +457,10 @@ def test_converters_bit_exact():
         np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32), err_msg=f"kind {kind}")
 
 
-def test_fft_merged_chunks_bit_identical(rng, monkeypatch):
+def test_fft_merged_chunks_match_separate_launches(rng, monkeypatch):
     """The 64k plan's merged pass-B(c) + pass-A(c+1) launches (several small chunks, a ragged
-    last chunk) give the rows of one chunk per call, each within the spectrum parity bar."""
+    last chunk) agree with separate pass-A / pass-B launches to 1e-3 dB (not bit for bit: the two
+    kernels contract different products into FMAs), and every row meets the spectrum parity bar."""
     N, frames = 65536, 7
     x = iq(rng, N * frames)
     import torch
@@ -400,6 +474,7 @@ def test_fft_merged_chunks_bit_identical(rng, monkeypatch):
         f.close()
         return out.cpu().numpy()
 
+    monkeypatch.setenv("SDRGPU_TUNING", "1")
     monkeypatch.setenv("SDRGPU_FFT_CHUNK_MB", "1")          # 2 frames per chunk -> 4 chunks, merged
     a = rows()
     monkeypatch.setenv("SDRGPU_FFT_CHUNK_MB", "64")
@@ -432,3 +507,82 @@ def test_fft_64k_zero_pad_strided(nz, rng):
     for j in range(frames):
         xs = x[j * stride:j * stride + nz]
         db_check(rows[j * N:(j + 1) * N], oracle.fft_truth_power(xs, nz, N, w), N, ref32_fft_db(xs, nz, N, w))
+
+
+@pytest.mark.parametrize("nz,stride", [(1000000, 1000000), (666667, 666667), (1000000, 1000000 + 4321)])
+def test_fft_1m_batch_multi_chunk(nz, stride, rng):
+    """C2's bench path: a 1M-point batch of 17 frames read in place at the reshaper stride (16-frame
+    chunks -> 2 chunks, the last one ragged). Even strides take the paired (16-B) pass A, the odd
+    one (fftRate 15 at 10 MS/s: nz = 666,667, iq_frontend.h:56-60) the one-column pass A. Every
+    row meets the spectrum parity bar against the fp64 truth."""
+    import torch
+    N, frames = 1 << 20, 17
+    x = iq(rng, stride * (frames - 1) + nz)
+    d_x = torch.from_numpy(x.view(np.float32)).cuda()
+    f = dsp.FFTSpectrum(N, nz, 6)
+    out = torch.empty(frames * N, dtype=torch.float32, device="cuda")
+    assert f.execute_dev(d_x.data_ptr(), stride, frames, out.data_ptr()) == frames
+    torch.cuda.synchronize()
+    rows = out.cpu().numpy().reshape(frames, N)
+    w = oracle.create_window(6, nz)
+    for j in range(frames):
+        xs = x[j * stride:j * stride + nz]
+        db_check(rows[j], oracle.fft_truth_power(xs, nz, N, w), N, ref32_fft_db(xs, nz, N, w))
+
+
+def test_process_dev_across_streams(rng):
+    """A handle driven from two streams in turn (the NCO table, history and quadrature state are
+    per handle) gives the same output stream as one stream: each call waits for the previous one."""
+    import torch
+    x = iq(rng, 400000)
+    d_x = torch.from_numpy(x.view(np.float32)).cuda()
+    ref = dsp.RxVFO(61.44e6, 240000, 200000, 2.5e6).process(x)
+    g = dsp.RxVFO(61.44e6, 240000, 200000, 2.5e6)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    out = torch.zeros(2 * (len(ref) + 16), dtype=torch.float32, device="cuda")
+    m, a = 0, 0
+    for k, b in enumerate([50000, 50001, 123456, 300000, 400000]):
+        s = (s1 if k % 2 == 0 else s2).cuda_stream
+        m += g.process_dev(d_x.data_ptr() + 8 * a, b - a, out.data_ptr() + 8 * m, s)
+        a = b
+    torch.cuda.synchronize()
+    assert m == len(ref)
+    got = out[:2 * m].cpu().numpy().view(np.complex64)
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+SPECTRUM_ULP_CASES = [("random", 4096, 4096), ("random", 65536, 65536), ("random", 1 << 20, 1000000),
+                      ("tones", 65536, 65536), ("tones", 1 << 20, 1000000), ("aes17", 0, 0)]
+
+
+@pytest.mark.parametrize("kind,N,nz", SPECTRUM_ULP_CASES)
+def test_spectrum_ulp_distribution(kind, N, nz, rng):
+    """The north_star's "<= 1 ulp on FFT magnitude", measured literally: the dB error in fp32 ulps of
+    the correctly rounded truth (fp64 DFT of the same float-windowed frame), next to pocketfft's
+    (scipy single precision, the FFTW-class CPU reference) on the same frame. No fp32 FFT reaches
+    1 ulp on every bin; the assertion is that the GPU's distribution is in the same
+    class as pocketfft's: median no worse, the fraction within 1 ulp within 3 points of its own,
+    p99 within 2x (+1 ulp). The numbers go to the report (profiles/)."""
+    if kind == "aes17":
+        g = np.load(GOLDEN + "/fft_aes17.npz")
+        N = nz = int(g["N"])
+        x, truth = g["x"], g["power_f64"]
+        w = oracle.create_window(6, N)
+    else:
+        if kind == "random":
+            x = iq(rng, nz)
+        else:
+            n = np.arange(nz)
+            x = (0.5 * np.exp(2j * np.pi * 0.1234567 * n) + 0.01 * np.exp(-2j * np.pi * 0.3 * n)).astype(np.complex64)
+            x = (x + iq(rng, nz, 1e-4)).astype(np.complex64)
+        w = oracle.create_window(6, nz)
+        truth = oracle.fft_truth_power(x, nz, N, w)
+    db = dsp.FFTSpectrum(N, nz, 6).logmag(x)
+    e_gpu = db_ulp_errors(db, truth)
+    e_ref = db_ulp_errors(ref32_fft_db(x, nz, N, w), truth)
+    sg, sr = ulp_summary(e_gpu), ulp_summary(e_ref)
+    write_report("spectrum_ulp", {"case": kind, "N": N, "nz": nz, "gpu": sg, "pocketfft_f32": sr})
+    assert sg["p50"] <= sr["p50"], (sg, sr)
+    if sg["bins"] >= 1000:   # (a tonal frame has only a handful of bins within 60 dB of its peak)
+        assert sg["frac_le_1ulp"] >= sr["frac_le_1ulp"] - 0.03, (sg, sr)
+    assert sg["p99"] <= 2 * sr["p99"] + 1, (sg, sr)
