@@ -42,8 +42,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c5", choices=["c5", "c2", "c3", "c4"])
     ap.add_argument("--log2-batch", type=int, default=28, help="IQ samples per GPU per step = 2^k (c5/c3)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline leg (1-core, all-core)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-sub", action="store_true", help="time only --config (no C2/C3/C4 sub-objects)")
     return ap.parse_args()
 
 
@@ -63,7 +64,8 @@ class C5:
         self.audio = torch.empty(2 * (self.B // 256 + 64), dtype=torch.float32, device="cuda")
         self.bytes_per_sample = 8 + 4 + 8 / 256 + 8 / 256   # ~12.06 B
         self.kernel_bytes = 12.0 * self.B                   # spectrum pair: 8 B in + 4 B dB out per sample
-        self.kernel_name = "spectrum (fft_passA + fft_passB, N=65536)"
+        self.kernel_name = ("spectrum N=65536: fft_passA_kernel<256,32> (chunk 0) + fft_merged_kernel<256,32,256,32,false> "
+                            "(pass B chunk c + pass A chunk c+1) x15 + fft_passB_kernel<256,32> (last chunk)")
         self.pieces = max(1, int(os.environ.get("BENCH_C5_PIECES", "1")))
 
     def run(self, x, s, timed_call):
@@ -99,7 +101,7 @@ class C2:
         self.spectra = torch.empty(self.frames * self.N, dtype=torch.float32, device="cuda")
         self.bytes_per_sample = 8 + 4 * self.N / self.NZ
         self.kernel_bytes = self.bytes_per_sample * self.B
-        self.kernel_name = "spectrum (fft_passA + fft_passB, N=2^20, nz=1e6)"
+        self.kernel_name = "spectrum N=2^20, nz=1e6: fft_passA2_kernel<1024,16> + fft_passB_kernel<1024,16> per 16-frame chunk"
 
     def dominant(self, x, s):
         self.fft.execute_dev(x.data_ptr(), self.NZ, self.frames, self.spectra.data_ptr(), s)
@@ -147,7 +149,20 @@ class C4:
         self.out = torch.empty(2 * (self.B + self.M), dtype=torch.float32, device="cuda")
         self.bytes_per_sample = 16.0
         self.kernel_bytes = 16.0 * self.B
-        self.kernel_name = "chan_kernel<1024> (16-tap branch FIRs + 1024-pt FFT per frame)"
+        self.kernel_name = "chan2_kernel<1024> (16-tap branch FIRs + 1024-pt FFT per frame)"
+
+    def flop_roofline(self, kern_ms):
+        # report the flop side too. Executed algorithm: 16-tap complex x real branch
+        # FIR (64 flop/sample) + a 1024-point radix-16/4 FFT per frame (5 log2 M = 50 flop/sample,
+        # the standard count); the dense DFT-GEMM formulation the survey names would do 64 + 512.
+        fl = (64 + 5 * 10) * self.B
+        tf = fl / (kern_ms * 1e-3) / 1e12
+        gemm = (64 + 512) * self.B / (kern_ms * 1e-3) / 1e12
+        return {"bound": "valu-fp32", "achieved": round(tf, 2), "peak": 157.3, "unit": "TFLOP/s",
+                "frac": round(tf / 157.3, 4), "flop_per_sample": 114,
+                "dft_gemm_equivalent_TFLOPs": round(gemm, 1),
+                "note": "fp32 vector peak (MI355X_MICROARCH.md); gfx950's fp32 MFMA peak is the same 157 TF, "
+                        "so the 576-flop DFT-GEMM form would be compute-bound where the FFT form is HBM-bound"}
 
     def dominant(self, x, s):
         self.ch.process_dev(x.data_ptr(), self.B, self.out.data_ptr(), s)
@@ -164,110 +179,57 @@ def _run_generic(wl, x, s, timed_call):
     wl.rest(x, s)
 
 
-def _timed(fn, blk, seconds):
-    n, t0 = 0, time.perf_counter()
-    while True:
-        fn()
-        n += blk
-        dt = time.perf_counter() - t0
-        if dt >= seconds:
-            return n / dt / 1e6, n, dt
-
-
 def cpu_baseline(config, seconds):
-    """The reference CPU path for the config, time-bounded sample on the host (1 thread):
-    the oracle's C port (VOLK-generic-equivalent fp32 loops) and, for the FFT configs, an
-    optimized library FFT (torch.fft on CPU = pocketfft, 1 thread) -- the faster of the two
-    is the baseline value (every speed-up claim uses the faster CPU number)."""
+    """The reference CPU path for the config on the host cores, measured by
+    oracle/cpu_baseline.py (test infrastructure, run only here): the oracle's C restatement built
+    on this host with -O3 -march=native (vectorised VOLK-class dots) and, for the spectrum legs,
+    pocketfft (scipy.fft, fp32, 1 worker); SpeedTester-style 1e6-sample blocks. `value` is the
+    all-core aggregate (one independent stream per core, up to 16 cores = the box's CPU share),
+    i.e. the faster CPU number every speed-up claim is made against; `value_1core` the reference's
+    own model (one worker thread per block, single-threaded FFT)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
-    rng = np.random.default_rng(0xACE1)
-    torch.set_num_threads(1)
-    if config == "c5":
-        blk = 1 << 20
-        x = (rng.uniform(-1, 1, blk) + 1j * rng.uniform(-1, 1, blk)).astype(np.complex64)
-        chain = oracle.Chain(61.44e6, 65536, 2.5e6, precise=False)
-        v, n, dt = _timed(lambda: chain.process(x), blk, seconds)
-        return {"value": round(v, 3), "cores": 1, "kind": "port",
-                "sample": f"oracle C port of the same C5 chain (64k BH7 spectra + RxVFO + WFM mono; fp32, VOLK-style "
-                          f"rotator/dots), {n} samples in 1M blocks, {dt:.1f} s on 1 host core"}
-    if config == "c2":
-        N, nz = 1 << 20, 1000000
-        x = (rng.uniform(-1, 1, nz) + 1j * rng.uniform(-1, 1, nz)).astype(np.complex64)
-        w = oracle.create_window(6, nz)
-        v1, n1, dt1 = _timed(lambda: oracle.fft_logmag(x, nz, N, w), nz, seconds / 2)
-        xt, wt = torch.from_numpy(x), torch.from_numpy(w)
-
-        def lib_fft():
-            buf = torch.zeros(N, dtype=torch.complex64)
-            buf[:nz] = xt * wt
-            X = torch.fft.fft(buf)
-            return 10.0 * torch.log10(X.real * X.real + X.imag * X.imag)
-        v2, n2, dt2 = _timed(lib_fft, nz, seconds / 2)
-        best = max(v1, v2)
-        return {"value": round(best, 3), "cores": 1, "kind": "port",
-                "sample": f"1M BH7 window*FFT*log-power of nz=1e6 frames, 1 thread: oracle C port {v1:.2f} MS/s "
-                          f"({n1 // nz} frames, {dt1:.1f} s); torch.fft CPU (pocketfft) {v2:.2f} MS/s ({n2 // nz} frames, "
-                          f"{dt2:.1f} s); value = the faster"}
-    if config == "c3":
-        blk = 1 << 20
-        x = (rng.uniform(-1, 1, blk) + 1j * rng.uniform(-1, 1, blk)).astype(np.complex64)
-        taps = oracle.low_pass(3.0e6, 912000.0, 61.44e6)
-        d = oracle.DDCFM(2 * np.pi * (-1.5e6 / 61.44e6), taps, 8, 2 * np.pi * 100e3 / (61.44e6 / 8), precise=False)
-        v, n, dt = _timed(lambda: d.process(x), blk, seconds)
-        return {"value": round(v, 3), "cores": 1, "kind": "port",
-                "sample": f"oracle C port: FrequencyXlator -> 256-tap DecimatingFIR /8 -> Quadrature (fp32, VOLK-style), "
-                          f"{n} samples in 1M blocks, {dt:.1f} s on 1 host core"}
-    if config == "c4":
-        M, Q = 1024, 16
-        h = oracle.windowed_sinc(Q * M, np.pi / M).reshape(Q, M)
-        frames = 256
-        x = (rng.uniform(-1, 1, (frames + Q) * M) + 1j * rng.uniform(-1, 1, (frames + Q) * M)).astype(np.complex64)
-        xt = torch.from_numpy(x).reshape(frames + Q, M)
-        ht = torch.from_numpy(h)
-
-        def chan():   # same algorithm as the GPU (16-tap branch FIRs + M-point FFT per frame), vectorised
-            u = torch.zeros((frames, M), dtype=torch.complex64)
-            for q in range(Q):
-                u += ht[q] * xt[q:q + frames]
-            return torch.fft.fft(u, dim=1)
-        v, n, dt = _timed(chan, frames * M, seconds)
-        return {"value": round(v, 3), "cores": 1, "kind": "port",
-                "sample": f"polyphase channelizer restated with torch CPU ops (branch FIR + pocketfft), 1 thread, "
-                          f"{n} samples, {dt:.1f} s"}
-    return None
+    import cpu_baseline as cb
+    r = cb.measure(config, seconds)
+    h = r["host"]
+    return {"value": round(r["value_all_cores"], 3), "unit": "MS/s", "cores": r["cores_all"], "kind": "port",
+            "value_1core": round(r["value_1core"], 3),
+            "sample": f"{r['variant']}: {r['cores_all']} independent streams x {seconds:.0f} s (all-core aggregate), "
+                      f"1 stream {r['value_1core']:.2f} MS/s; 1-core variants "
+                      + ", ".join(f"{k} {v:.2f}" for k, v in r["variants_1core"].items())
+                      + f"; {r['build']}; SpeedTester-style 1e6-sample blocks of uniform [-1,1) IQ",
+            "host": {"nproc": h["nproc"], "affinity_cpus": h["affinity"], "model": h["model"]}}
 
 
 def traffic_per_sample(config):
-    """HBM bytes per input sample of the dominant launch group, from the committed rocprofv3
-    PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/pmc_traffic.py)."""
-    path = os.path.join(ROOT, "profiles", "r1", f"{config}_pmc_traffic.json")
-    try:
-        d = json.load(open(path))
-        return float(d["bytes_per_sample"])
-    except (OSError, KeyError, ValueError):
-        return None
+    """HBM bytes per input sample of the dominant launch group, from the newest committed
+    rocprofv3 PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/pmc_bytes_per_sample.py)."""
+    for rnd in ("r2", "r1"):
+        path = os.path.join(ROOT, "profiles", rnd, f"{config}_pmc_traffic.json")
+        try:
+            d = json.load(open(path))
+            return float(d["bytes_per_sample"]), f"profiles/{rnd}/{config}_pmc_traffic.json"
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
-def main():
-    a = parse()
-    shard = StreamShard(backend="nccl")
+WORKLOADS = {"c5": "C5 per-GPU slice: 64k BH7 FFT+log-mag (back-to-back) + RxVFO 61.44M->240k + BroadcastFM mono",
+             "c2": "C2: 1M-point BH7 FFT + log-mag, nz=1e6 zero-padded, 256 frames/step",
+             "c3": "C3: xlator + 256-tap FIR /8 + FM quadrature (fused), 2^28 samples/step",
+             "c4": "C4: 1024-channel polyphase channelizer (16384-tap prototype), 2^28 samples/step"}
+
+
+def run_config(config, a, shard, dev, stream):
+    """Time `a.steps` steps of one config on this rank; returns (B, elapsed_s, kernel_ms, wl)."""
     world, rank = shard.world, shard.rank
-    if world == 1:
-        torch.cuda.set_device(0)
-    dev = torch.cuda.current_device()
-    # one explicit non-default stream for every kernel of the step (libsdrgpu treats a NULL
-    # stream as "the handle's own stream", which would split the chain over several queues)
-    torch.cuda.set_stream(torch.cuda.Stream())
     B = 1 << a.log2_batch
-    if a.config == "c2":
+    if config == "c2":
         B = 256 * 1000000
-    wl = {"c5": C5, "c2": C2, "c3": C3, "c4": C4}[a.config](B, shard, dev)
+    wl = {"c5": C5, "c2": C2, "c3": C3, "c4": C4}[config](B, shard, dev)
     B = wl.B
     g = torch.Generator(device="cuda")
     g.manual_seed(shard.seed())
     x = (torch.rand(2 * B, device="cuda", generator=g) * 2 - 1).contiguous()   # complex_t interleaved
-    stream = torch.cuda.current_stream()
     gather_bufs = None
     if world > 1 and rank == 0:
         gather_bufs = [torch.empty_like(wl.gather_src()) for _ in range(world)]
@@ -326,34 +288,74 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = sum(sum(e0.elapsed_time(e1) for e0, e1 in evs) for evs in ev) / max(len(ev), 1)
     elapsed, kern_ms = shard.max_over_ranks([elapsed, kern_ms], device="cuda")
+    del x
+    return B, elapsed, kern_ms, wl
 
+
+def config_result(config, a, world, B, elapsed, kern_ms, wl):
+    value = world * B * a.steps / elapsed / 1e6
+    achieved = wl.kernel_bytes / (kern_ms * 1e-3) / 1e9
+    tps, tsrc = traffic_per_sample(config)
+    r = {"value": round(value, 3), "unit": "MS/s", "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+         "workload": WORKLOADS[config], "samples_per_gpu_per_step": B,
+         "bytes_per_sample": round(wl.bytes_per_sample, 4),
+         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(achieved / HBM_PEAK_GBS, 4),
+                      "traffic": round(tps * B) if tps else None, "traffic_source": tsrc,
+                      "kernel": wl.kernel_name, "kernel_ms": round(kern_ms, 4),
+                      "algorithmic_bytes": round(wl.kernel_bytes)},
+         "chain_hbm_GBs": round(wl.bytes_per_sample * value * 1e6 / world / 1e9, 1)}
+    if hasattr(wl, "flop_roofline"):
+        r["roofline_flops"] = wl.flop_roofline(kern_ms)
+    return r
+
+
+def main():
+    a = parse()
+    shard = StreamShard(backend="nccl")
+    world, rank = shard.world, shard.rank
+    if world == 1:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+    # one explicit non-default stream for every kernel of the step (libsdrgpu treats a NULL
+    # stream as "the handle's own stream", which would split the chain over several queues)
+    torch.cuda.set_stream(torch.cuda.Stream())
+    stream = torch.cuda.current_stream()
+    B, elapsed, kern_ms, wl = run_config(a.config, a, shard, dev, stream)
+    head = config_result(a.config, a, world, B, elapsed, kern_ms, wl)
+    del wl
+    # the other single-GPU configs of BASELINE.json, timed the same way in the same run (N = 1 only:
+    # C2 and C3 carry the north_star's >= 10x / >= 40% targets, C4 the channelizer)
+    subs = {}
+    if world == 1 and not a.no_sub:
+        for c in ("c2", "c3", "c4", "c5"):
+            if c == a.config:
+                continue
+            torch.cuda.empty_cache()
+            b2, el2, km2, wl2 = run_config(c, a, shard, dev, stream)
+            subs[c] = config_result(c, a, world, b2, el2, km2, wl2)
+            del wl2
     if rank == 0:
-        total = world * B * a.steps
-        value = total / elapsed / 1e6
-        achieved = wl.kernel_bytes / (kern_ms * 1e-3) / 1e9
-        tps = traffic_per_sample(a.config)
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "MS/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
+            "metric": METRIC, "value": head["value"], "unit": "MS/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic uniform[-1,1) complex IQ in HBM",
-            "config": {"workload": {"c5": "C5 per-GPU slice: 64k BH7 FFT+log-mag (back-to-back) + RxVFO 61.44M->240k "
-                                          "+ BroadcastFM mono; RCCL gather of 16 spectra/rank/step",
-                                    "c2": "C2: 1M-point BH7 FFT + log-mag, nz=1e6 zero-padded",
-                                    "c3": "C3: xlator + 256-tap FIR /8 + FM quadrature (fused)",
-                                    "c4": "C4: 1024-channel polyphase channelizer (16384-tap prototype), 1 stream"}[a.config],
+            "config": {"workload": head["workload"] + ("; RCCL gather of spectra to rank 0 each step" if world > 1 else ""),
                        "samples_per_gpu_per_step": B, "parallelism": f"replica-streams x{world}",
-                       "bytes_per_sample": round(wl.bytes_per_sample, 4)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": round(tps * B) if tps else None,
-                         "kernel": wl.kernel_name, "kernel_ms": round(kern_ms, 4)},
-            "chain_hbm_GBs": round(wl.bytes_per_sample * value * 1e6 / world / 1e9, 1),
+                       "bytes_per_sample": head["bytes_per_sample"]},
+            "roofline": head["roofline"],
+            "chain_hbm_GBs": head["chain_hbm_GBs"],
         }
+        if "roofline_flops" in head:
+            out["roofline_flops"] = head["roofline_flops"]
         if world == 1 and not a.no_cpu:
-            cb = cpu_baseline(a.config, a.cpu_seconds)
-            if cb:
-                out["cpu_baseline"] = {"value": cb["value"], "unit": "MS/s", "cores": cb["cores"], "kind": cb["kind"],
-                                       "sample": cb["sample"]}
+            out["cpu_baseline"] = cpu_baseline(a.config, a.cpu_seconds)
+            out["speedup_vs_cpu_all_cores"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+            for c, r in subs.items():
+                r["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds)
+                r["speedup_vs_cpu_all_cores"] = round(r["value"] / r["cpu_baseline"]["value"], 1)
+        if subs:
+            out["configs"] = subs
         print(json.dumps(out), flush=True)
     shard.close()
 

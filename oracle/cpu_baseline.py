@@ -1,0 +1,207 @@
+"""CPU baseline for bench.py (TEST INFRASTRUCTURE: only bench.py's cpu_baseline leg runs this).
+
+The reference's CPU dsp:: path cannot run on the GPU box (no VOLK/FFTW there, and the reference
+tree does not travel), so the baseline is the oracle's C restatement of the same chain, built on
+the host that runs it with -O3 -march=native (no fast-math; vectorised VOLK-class dot products),
+plus the FFTW-class library FFT the
+host has (pocketfft through scipy.fft, single precision, one worker) for the spectrum legs.
+For every config the faster CPU variant is the reported value.
+
+Harness: SpeedTester-style (core/src/dsp/bench/speed_tester.h:31-56): 1,000,000-sample blocks of
+uniform [-1, 1) IQ pushed through the chain for a bounded time; MS/s = samples / duration.
+  * 1 core: one stream on one thread (the reference's model: one worker thread per block, one
+    single-threaded FFT);
+  * all cores: one independent stream per core (separate processes, each pinned to a core),
+    aggregate = sum of the per-stream rates (they run concurrently).
+
+Usage (worker): python oracle/cpu_baseline.py --config c5 --seconds 8 --seed 3 [--cpu K]
+prints one JSON line {"samples": n, "seconds": t, "variant": "..."}.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BLK = 1000000        # SpeedTester block (speed_tester.h:37: 1e6 samples)
+
+
+def native_oracle():
+    """Build the oracle with -march=native for the host this runs on (outside the repo tree)."""
+    out_dir = os.path.join(os.environ.get("TMPDIR", "/tmp"), "sdrgpu_cpu_baseline")
+    os.makedirs(out_dir, exist_ok=True)
+    so = os.path.join(out_dir, "libsdr_oracle_native.so")
+    src = os.path.join(HERE, "sdr_oracle.c")
+    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        # -ffp-contract=fast: the dot products use FMA like VOLK's *_avx2_fma kernels (this copy
+        # is only timed; the in-tree checker build keeps -ffp-contract=off)
+        cmd = ["gcc", "-O3", "-march=native", "-ffp-contract=fast", "-fno-fast-math", "-fPIC", "-shared",
+               "-o", so, src, "-lm"]
+        try:
+            subprocess.check_call(cmd, cwd=HERE, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        except (OSError, subprocess.CalledProcessError):
+            return None
+    return so
+
+
+def host_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity": aff, "model": model}
+
+
+def _iq(rng, n):
+    import numpy as np
+    return (rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)).astype(np.complex64)
+
+
+def _timed(fn, blk, seconds):
+    n, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        n += blk
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            return n, dt
+
+
+def workloads(config, seed):
+    """{variant: (step_fn, samples_per_step)} for the config's CPU restatements."""
+    import numpy as np
+    sys.path.insert(0, HERE)
+    import oracle
+    import scipy.fft
+    rng = np.random.default_rng(0xACE1 + seed)
+    out = {}
+    if config == "c5":
+        # 64k BH7 spectra back to back (fftRate = fs / N) + RxVFO(61.44 M -> 240 k) + WFM mono
+        N = 65536
+        blk = 16 * N                                      # ~1e6 samples, whole frames
+        x = _iq(rng, blk)
+        w = oracle.create_window(6, N)
+        chain = oracle.Chain(61.44e6, N, 2.5e6, precise=False)
+        out["oracle C chain (radix-2 FFT)"] = (lambda: chain.process(x), blk)
+        vfo = oracle.RxVFO(61.44e6, 240000, 200000, 2.5e6, precise=False)
+        wfm = oracle.BroadcastFM(100000, 240000, True, precise=False)
+        frames = x.reshape(-1, N)
+
+        def pocket():
+            X = scipy.fft.fft(frames * w, axis=1, workers=1)
+            p = X.real * X.real + X.imag * X.imag
+            db = 10.0 * np.log10(p)
+            wfm.process(vfo.process(x))
+            return db
+        out["pocketfft spectra + oracle C VFO/WFM"] = (pocket, blk)
+    elif config == "c2":
+        N, nz = 1 << 20, 1000000
+        x = _iq(rng, nz)
+        w = oracle.create_window(6, nz)
+        out["oracle C radix-2 FFT"] = (lambda: oracle.fft_logmag(x, nz, N, w), nz)
+        buf = np.zeros(N, dtype=np.complex64)
+
+        def pocket():
+            buf[:nz] = x * w
+            X = scipy.fft.fft(buf, workers=1)
+            return 10.0 * np.log10(X.real * X.real + X.imag * X.imag)
+        out["pocketfft"] = (pocket, nz)
+    elif config == "c3":
+        x = _iq(rng, BLK)
+        taps = oracle.low_pass(3.0e6, 912000.0, 61.44e6)
+        d = oracle.DDCFM(2 * np.pi * (-1.5e6 / 61.44e6), taps, 8, 2 * np.pi * 100e3 / (61.44e6 / 8), precise=False)
+        out["oracle C xlator + 256-tap FIR/8 + quadrature"] = (lambda: d.process(x), BLK)
+    elif config == "c4":
+        M, Q = 1024, 16
+        h = oracle.windowed_sinc(Q * M, np.pi / M).reshape(Q, M).astype(np.float32)
+        frames = 1024
+        x = _iq(rng, (frames + Q) * M).reshape(frames + Q, M)
+
+        def chan():    # 16-tap branch FIRs + M-point FFT per output frame (the GPU's algorithm)
+            u = np.zeros((frames, M), dtype=np.complex64)
+            for q in range(Q):
+                u += h[q] * x[q:q + frames]
+            return scipy.fft.fft(u, axis=1, workers=1)
+        out["numpy branch FIR + pocketfft"] = (chan, frames * M)
+    return out
+
+
+def worker(config, seconds, seed, variant=None):
+    res = {}
+    for name, (fn, blk) in workloads(config, seed).items():
+        if variant is not None and name != variant:
+            continue
+        fn()   # warm
+        n, dt = _timed(fn, blk, seconds)
+        res[name] = {"samples": n, "seconds": dt}
+    return res
+
+
+def _spawn(config, seconds, seed, variant, cpu, lib):
+    env = dict(os.environ)
+    for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+        env[k] = "1"
+    if lib:
+        env["ORACLE_LIB_PATH"] = lib
+    cmd = [sys.executable, os.path.abspath(__file__), "--config", config, "--seconds", str(seconds), "--seed", str(seed),
+           "--variant", variant]
+    if cpu is not None:
+        cmd += ["--cpu", str(cpu)]
+    return subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+
+
+def measure(config, seconds=8.0, max_cores=16):
+    """1-core figure of every variant (in turn), then the fastest variant on all cores."""
+    lib = native_oracle()
+    info = host_info()
+    cores_avail = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count()))
+    ncores = max(1, min(max_cores, len(cores_avail)))
+    one = {}
+    for name in workloads_names(config):
+        p = _spawn(config, seconds, 0, name, cores_avail[0], lib)
+        r = json.loads(p.communicate()[0].strip().splitlines()[-1])[name]
+        one[name] = r["samples"] / r["seconds"] / 1e6
+    best = max(one, key=one.get)
+    procs = [_spawn(config, seconds, k + 1, best, cores_avail[k], lib) for k in range(ncores)]
+    rates = []
+    for p in procs:
+        r = json.loads(p.communicate()[0].strip().splitlines()[-1])[best]
+        rates.append(r["samples"] / r["seconds"] / 1e6)
+    return {"value_1core": one[best], "variant": best, "variants_1core": one, "value_all_cores": sum(rates),
+            "cores_all": ncores, "per_stream_min": min(rates), "host": info,
+            "build": "oracle C -O3 -march=native (host-built)" if lib else "oracle C (in-tree build)"}
+
+
+def workloads_names(config):
+    return {"c5": ["oracle C chain (radix-2 FFT)", "pocketfft spectra + oracle C VFO/WFM"],
+            "c2": ["oracle C radix-2 FFT", "pocketfft"],
+            "c3": ["oracle C xlator + 256-tap FIR/8 + quadrature"],
+            "c4": ["numpy branch FIR + pocketfft"]}[config]
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", required=True)
+    ap.add_argument("--seconds", type=float, default=8.0)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--variant", default=None)
+    ap.add_argument("--cpu", type=int, default=None)
+    ap.add_argument("--measure", action="store_true", help="run the 1-core + all-core measurement")
+    a = ap.parse_args()
+    if a.measure:
+        print(json.dumps(measure(a.config, a.seconds)))
+        sys.exit(0)
+    if a.cpu is not None and hasattr(os, "sched_setaffinity"):
+        os.sched_setaffinity(0, {a.cpu})
+    print(json.dumps(worker(a.config, a.seconds, a.seed, a.variant)))

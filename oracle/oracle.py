@@ -11,7 +11,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsdr_oracle.so")
+# ORACLE_LIB_PATH: a host-built -march=native copy of the same source (bench.py's CPU baseline)
+LIB_PATH = os.environ.get("ORACLE_LIB_PATH") or os.path.join(HERE, "libsdr_oracle.so")
 
 
 def _load():

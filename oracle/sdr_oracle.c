@@ -293,6 +293,35 @@ static void dot_ff(const float* x, const float* h, int n, float* o, int precise)
         o[0] = (((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]))) + b;
     }
 }
+/* CPU-baseline dot products (precise = 0), VOLK-class: 16-float vector multiply-adds (GCC vector
+ * extensions, lowered to AVX2 / AVX-512 by -march=native) with two accumulators, like
+ * volk_32fc_32f_dot_prod_32fc's SIMD kernels. Complex data x real taps runs as a float dot of
+ * length 2n against taps duplicated per (re, im) pair, hh[2j] = hh[2j + 1] = h[j]. */
+typedef float v16f __attribute__((vector_size(64)));
+static inline v16f ld16(const float* p) { v16f v; memcpy(&v, p, sizeof(v)); return v; }
+static float dot_vec(const float* x, const float* h, int m, float* odd) {
+    v16f a0 = {0}, a1 = {0};
+    int k = 0;
+    for (; k + 32 <= m; k += 32) {
+        a0 += ld16(x + k) * ld16(h + k);
+        a1 += ld16(x + k + 16) * ld16(h + k + 16);
+    }
+    for (; k + 16 <= m; k += 16) a0 += ld16(x + k) * ld16(h + k);
+    v16f a = a0 + a1;
+    float e = 0, o = 0;
+    for (int i = 0; i < 16; i += 2) { e += a[i]; o += a[i + 1]; }
+    for (; k < m; k++) { if (k & 1) o += x[k] * h[k]; else e += x[k] * h[k]; }
+    if (odd) { *odd = o; return e; }
+    return e + o;
+}
+static void dot_cf_vec(const float* x, const float* hh, int n, float* o) { o[0] = dot_vec(x, hh, 2 * n, o + 1); }
+static void dot_ff_vec(const float* x, const float* h, int n, float* o) { o[0] = dot_vec(x, h, n, NULL); }
+static float* dup_taps(const float* h, int n) {
+    float* hh = (float*)malloc(sizeof(float) * 2 * (size_t)(n > 0 ? n : 1));
+    for (int j = 0; j < n; j++) hh[2 * j] = hh[2 * j + 1] = h[j];
+    return hh;
+}
+
 static void dot_cc(const float* x, const float* h, int n, float* o, int precise) {
     if (precise) {
         double re = 0, im = 0;
@@ -316,6 +345,7 @@ static void dot_cc(const float* x, const float* h, int n, float* o, int precise)
 struct orc_fir {
     int dtype, ttype, ntaps, decim, offset, precise, cap;
     float* taps;
+    float* hh;    /* taps duplicated per (re, im) pair (CPU-baseline complex x real dot) */
     float* buf;   /* [ntaps-1 history | input], elements of dtype */
 };
 
@@ -341,6 +371,8 @@ void orc_fir_set_taps(orc_fir* f, const float* taps, int ntaps) {
     free(f->taps);
     f->taps = (float*)malloc(sizeof(float) * ntaps * esz(f->ttype));
     memcpy(f->taps, taps, sizeof(float) * ntaps * esz(f->ttype));
+    free(f->hh);
+    f->hh = (f->ttype == ORC_F32) ? dup_taps(taps, ntaps) : NULL;
     f->ntaps = ntaps;
     f->offset = 0;   /* DecimatingFIR::setTaps (decimating_fir.h:19-26) */
 }
@@ -362,9 +394,13 @@ int orc_fir_process(orc_fir* f, const float* in, int count, float* out) {
     for (; f->offset < count; f->offset += f->decim) {
         const float* x = f->buf + (size_t)f->offset * e;
         float* o = out + (size_t)outCount * e;
-        if (f->dtype == ORC_F32) dot_ff(x, f->taps, f->ntaps, o, f->precise);
-        else if (f->ttype == ORC_F32) dot_cf(x, f->taps, f->ntaps, o, f->precise);
-        else dot_cc(x, f->taps, f->ntaps, o, f->precise);
+        if (f->dtype == ORC_F32) {
+            if (f->precise) dot_ff(x, f->taps, f->ntaps, o, 1); else dot_ff_vec(x, f->taps, f->ntaps, o);
+        } else if (f->ttype == ORC_F32) {
+            if (f->precise) dot_cf(x, f->taps, f->ntaps, o, 1); else dot_cf_vec(x, f->hh, f->ntaps, o);
+        } else {
+            dot_cc(x, f->taps, f->ntaps, o, f->precise);
+        }
         outCount++;
     }
     f->offset -= count;
@@ -372,7 +408,7 @@ int orc_fir_process(orc_fir* f, const float* in, int count, float* out) {
     return outCount;
 }
 
-void orc_fir_destroy(orc_fir* f) { if (!f) return; free(f->buf); free(f->taps); free(f); }
+void orc_fir_destroy(orc_fir* f) { if (!f) return; free(f->buf); free(f->taps); free(f->hh); free(f); }
 
 /* ------------------------------------------------------------------ xlator */
 /* channel/frequency_xlator.h:15-50. phaseDelta = lv_cmake(cos(w), sin(w)) is
@@ -486,6 +522,7 @@ void orc_pdec_destroy(orc_pdec* p) { if (!p) return; for (int s = 0; s < p->nst;
 struct orc_poly {
     int dtype, interp, decim, tpp, phase, offset, precise, cap;
     float* bank;  /* [interp][tpp] */
+    float* hh;    /* bank duplicated per (re, im) pair (CPU-baseline complex dot) */
     float* buf;
 };
 orc_poly* orc_poly_create(int dtype, int interp, int decim, const float* taps, int ntaps, int precise) {
@@ -496,6 +533,7 @@ orc_poly* orc_poly_create(int dtype, int interp, int decim, const float* taps, i
     int tot = interp * p->tpp;
     for (int i = 0; i < tot; i++)
         p->bank[(size_t)((interp - 1) - (i % interp)) * p->tpp + i / interp] = (i < ntaps) ? taps[i] : 0.0f;
+    p->hh = dup_taps(p->bank, tot);
     p->buf = (float*)calloc((size_t)(p->tpp > 1 ? p->tpp - 1 : 1) * esz(dtype), sizeof(float));
     return p;
 }
@@ -515,8 +553,14 @@ int orc_poly_process(orc_poly* p, const float* in, int count, float* out) {
     while (p->offset < count) {
         const float* x = p->buf + (size_t)p->offset * e;
         const float* ph = p->bank + (size_t)p->phase * p->tpp;
-        if (p->dtype == ORC_F32) dot_ff(x, ph, p->tpp, out + outCount, p->precise);
-        else dot_cf(x, ph, p->tpp, out + 2 * outCount, p->precise);
+        if (p->precise) {
+            if (p->dtype == ORC_F32) dot_ff(x, ph, p->tpp, out + outCount, 1);
+            else dot_cf(x, ph, p->tpp, out + 2 * outCount, 1);
+        } else if (p->dtype == ORC_F32) {
+            dot_ff_vec(x, ph, p->tpp, out + outCount);
+        } else {
+            dot_cf_vec(x, p->hh + 2 * (size_t)p->phase * p->tpp, p->tpp, out + 2 * outCount);
+        }
         outCount++;
         p->phase += p->decim;
         p->offset += p->phase / p->interp;
@@ -526,7 +570,7 @@ int orc_poly_process(orc_poly* p, const float* in, int count, float* out) {
     memmove(p->buf, p->buf + (size_t)count * e, sizeof(float) * h * e);
     return outCount;
 }
-void orc_poly_destroy(orc_poly* p) { if (!p) return; free(p->bank); free(p->buf); free(p); }
+void orc_poly_destroy(orc_poly* p) { if (!p) return; free(p->bank); free(p->hh); free(p->buf); free(p); }
 
 /* ------------------------------------------------------ RationalResampler */
 /* multirate/rational_resampler.h:83-167 */

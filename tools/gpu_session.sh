@@ -13,12 +13,12 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   rc=$?; echo "tests rc=$rc" >> "$OUT/${TAG}_status.txt"; fatal $rc tests
 fi
 for cfg in ${BENCH_CFGS:-c5 c3 c2}; do
-  timeout -k 10 400 python bench.py --config $cfg --steps ${STEPS:-20} --warmup 3 --cpu-seconds ${CPUSEC:-10} > "$OUT/${TAG}_bench_$cfg.json" 2> "$OUT/${TAG}_bench_$cfg.err"
+  timeout -k 10 400 python bench.py --config $cfg --no-sub --steps ${STEPS:-20} --warmup 3 --cpu-seconds ${CPUSEC:-6} > "$OUT/${TAG}_bench_$cfg.json" 2> "$OUT/${TAG}_bench_$cfg.err"
   rc=$?; echo "bench $cfg rc=$rc" >> "$OUT/${TAG}_status.txt"; fatal $rc bench_$cfg
 done
 if [ "${PROFILE:-1}" == "1" ]; then
   for cfg in ${PROF_CFGS:-c5}; do
-    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof_$cfg" -o run -- python3 "$R/bench.py" --config $cfg --steps 10 --warmup 2 --no-cpu > "$OUT/${TAG}_prof_$cfg.log" 2>&1)
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof_$cfg" -o run -- python3 "$R/bench.py" --config $cfg --no-sub --steps 10 --warmup 2 --no-cpu > "$OUT/${TAG}_prof_$cfg.log" 2>&1)
     rc=$?; echo "prof $cfg rc=$rc" >> "$OUT/${TAG}_status.txt"; fatal $rc prof_$cfg
   done
 fi
@@ -27,7 +27,7 @@ echo "done $(date)" >> "$OUT/${TAG}_status.txt"
 if [ "${PMC:-0}" == "1" ]; then
   for cfg in ${PROF_CFGS:-c5}; do
     for ctr in FETCH_SIZE WRITE_SIZE; do
-      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$OUT/${TAG}_pmc_${cfg}_$ctr" -o run -- python3 "$R/bench.py" --config $cfg --steps 3 --warmup 1 --no-cpu > "$OUT/${TAG}_pmc_${cfg}_$ctr.log" 2>&1)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$OUT/${TAG}_pmc_${cfg}_$ctr" -o run -- python3 "$R/bench.py" --config $cfg --no-sub --steps 3 --warmup 1 --no-cpu > "$OUT/${TAG}_pmc_${cfg}_$ctr.log" 2>&1)
       rc=$?; echo "pmc $cfg $ctr rc=$rc" >> "$OUT/${TAG}_status.txt"; fatal $rc pmc_$cfg
     done
   done
