@@ -63,27 +63,16 @@ class C5:
         self.ifbuf = torch.empty(2 * (self.B // 256 + 64), dtype=torch.float32, device="cuda")
         self.audio = torch.empty(2 * (self.B // 256 + 64), dtype=torch.float32, device="cuda")
         self.bytes_per_sample = 8 + 4 + 8 / 256 + 8 / 256   # ~12.06 B
-        self.kernel_bytes = 12.0 * self.B                   # spectrum pair: 8 B in + 4 B dB out per sample
+        self.kernel_bytes = 12.0 * self.B                   # spectrum: 8 B in + 4 B dB out per sample
         self.kernel_name = ("spectrum N=65536: fft_passA_kernel<256,32> (chunk 0) + fft_merged_kernel<256,32,256,32,false> "
                             "(pass B chunk c + pass A chunk c+1) x15 + fft_passB_kernel<256,32> (last chunk)")
-        self.pieces = max(1, int(os.environ.get("BENCH_C5_PIECES", "1")))
 
     def run(self, x, s, timed_call):
-        # the batch is pushed through the chain in `pieces` blocks, each through the spectrum and
-        # then the VFO, as the reference's splitter feeds both paths block by block
-        # (iq_frontend.cpp:15-52); pieces > 1 lets the VFO re-read a block the spectrum just read
-        P = self.pieces
-        fpp = self.frames // P
-        m_if = m_au = 0
-        for k in range(P):
-            f0 = k * fpp
-            nf = fpp if k < P - 1 else self.frames - f0
-            xp = x.data_ptr() + 8 * f0 * self.N
-            timed_call(lambda: self.fft.execute_dev(xp, self.N, nf, self.spectra.data_ptr() + 4 * f0 * self.N, s))
-            m = self.vfo.process_dev(xp, nf * self.N, self.ifbuf.data_ptr() + 8 * m_if, s)
-            a = self.wfm.process_dev(self.ifbuf.data_ptr() + 8 * m_if, m, self.audio.data_ptr() + 8 * m_au, s)
-            m_if += m
-            m_au += a
+        # the front end's splitter hands the same block to the spectrum and the VFO
+        # (iq_frontend.cpp:15-52); the VFO output then feeds the WFM demodulator
+        timed_call(lambda: self.fft.execute_dev(x.data_ptr(), self.N, self.frames, self.spectra.data_ptr(), s))
+        m = self.vfo.process_dev(x.data_ptr(), self.B, self.ifbuf.data_ptr(), s)
+        self.wfm.process_dev(self.ifbuf.data_ptr(), m, self.audio.data_ptr(), s)
 
     def gather_src(self):
         return self.spectra[-16 * self.N:]

@@ -85,11 +85,17 @@ int  sdrgpu_decim_plan(int ratio, int* decims, int* ntaps, const float** taps); 
 /* Window * FFT(N, forward, unnormalised) * 10*log10(|X|^2) of nz <= N samples,
  * zero-padded to N (iq_frontend.cpp:230-249 + :295). N = 2^k, 64 <= N <= 2^20. */
 typedef struct sdrgpu_fft sdrgpu_fft;
+typedef struct sdrgpu_block sdrgpu_block;   /* stream blocks (below) */
 int sdrgpu_fft_create(sdrgpu_fft** h, int device, int fftSize, int nz, int windowType);
 int sdrgpu_fft_set_window(sdrgpu_fft* h, const float* window, int nz);   /* exact host floats */
 int sdrgpu_fft_set_window_type(sdrgpu_fft* h, int windowType, int nz);
 /* device batch: frame f starts at in + f*frameStride complex samples; out: frames x N floats */
 int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, void* stream);
+/* spectrum + one RxVFO over the same device batch of `frames` back-to-back frames (frame stride
+ * N, nz = N: fftRate = fs / N), the VFO reading the batch in place as the front end's splitter
+ * feeds both (iq_frontend.cpp:15-52), on one stream. Returns the VFO's output count (vfoOut). */
+int sdrgpu_fft_execute_vfo_dev(sdrgpu_fft* h, const void* in, int frames, float* out, sdrgpu_block* vfo,
+                               void* vfoOut, void* stream);
 /* drop-in for IQFrontEnd::handler: in = host complex_t[nz]; out = host float[N] or NULL
  * (acquireFFTBuffer may return NULL; the spectrum is then computed but not written). */
 int sdrgpu_fft_logmag(sdrgpu_fft* h, const void* in, float* out);
@@ -97,7 +103,6 @@ int sdrgpu_fft_size(sdrgpu_fft* h);
 int sdrgpu_fft_destroy(sdrgpu_fft* h);
 
 /* ---------------------------------------------------- stream blocks ---- */
-typedef struct sdrgpu_block sdrgpu_block;
 /* FrequencyXlator (offset in rad/sample, like init(in, offset)) */
 int sdrgpu_xlator_create(sdrgpu_block** h, int device, double offsetRad);
 int sdrgpu_xlator_set_offset(sdrgpu_block* h, double offsetRad);

@@ -65,6 +65,7 @@ def _load():
         "sdrgpu_fft_set_window": (i, [vp, fp, i]),
         "sdrgpu_fft_set_window_type": (i, [vp, i, i]),
         "sdrgpu_fft_execute_dev": (i, [vp, vp, ll, i, vp, vp]),
+        "sdrgpu_fft_execute_vfo_dev": (i, [vp, vp, i, vp, vp, vp, vp]),
         "sdrgpu_fft_logmag": (i, [vp, vp, vp]),
         "sdrgpu_fft_size": (i, [vp]),
         "sdrgpu_fft_destroy": (i, [vp]),

@@ -784,6 +784,21 @@ extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long f
     return frames;
 }
 
+// Spectrum + one VFO over the same device batch of back-to-back frames (fftRate = fs / N: the
+// IQFrontEnd's reshaper keeps every sample, iq_frontend.h:56-60), the VFO reading the batch in
+// place like every consumer of the front end's splitter (iq_frontend.cpp:15-52): one call, two
+// launch groups on the caller's stream. (Computing the VFO's first stage inside the 64k pass A,
+// so that the batch is read once, was built and measured slower: DESIGN.md §3.)
+extern "C" int sdrgpu_fft_execute_vfo_dev(sdrgpu_fft* h, const void* in, int frames, float* out, sdrgpu_block* vfo,
+                                          void* vfoOut, void* stream) {
+    if (!h || !in || !out || !vfo || !vfoOut || frames < 0) { set_error("fft_execute_vfo: bad argument"); return SDRGPU_EARG; }
+    const long long count = (long long)frames * h->p.N;
+    if (count > 0x7fffffffLL) { set_error("fft_execute_vfo: %lld samples per call (max 2^31 - 1)", count); return SDRGPU_EARG; }
+    hipStream_t s = stream ? (hipStream_t)stream : h->p.own;
+    SDRGPU_CHECK(sdrgpu_fft_execute_dev(h, in, h->p.N, frames, out, s));
+    return sdrgpu_block_process_dev(vfo, in, (int)count, vfoOut, s);
+}
+
 extern "C" int sdrgpu_fft_logmag(sdrgpu_fft* h, const void* in, float* out) {
     if (!h || !in) { set_error("fft_logmag: null argument"); return SDRGPU_EARG; }
     FftPlan& p = h->p;

@@ -235,6 +235,12 @@ class FFTSpectrum:
         return check(lib.sdrgpu_fft_execute_dev(self._h, _vp(in_ptr), int(frame_stride), int(frames), _vp(out_ptr),
                                                 _vp(stream or 0)))
 
+    def execute_vfo_dev(self, in_ptr, frames, out_ptr, vfo, vfo_out_ptr, stream=None):
+        """Spectra of `frames` back-to-back frames + one RxVFO over the same device batch (the VFO's
+        first stage fused into the 64k spectrum's input pass); returns the VFO's output count."""
+        return check(lib.sdrgpu_fft_execute_vfo_dev(self._h, _vp(in_ptr), int(frames), _vp(out_ptr), vfo._h,
+                                                    _vp(vfo_out_ptr), _vp(stream or 0)))
+
     def close(self):
         if self._h:
             lib.sdrgpu_fft_destroy(self._h)
