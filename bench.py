@@ -3,10 +3,12 @@
 Default workload (--config c5, one stream per GPU): BASELINE config C5's per-GPU slice,
 i.e. a 61.44 MS/s-class IQ stream pushed as fast as the GPU takes it through
   * the IQ front end's spectrum: 65,536-point BH7 window * FFT * 10log10|X|^2, frames
-    back to back (fftRate = fs/N -> skip 0), and
+    back to back (fftRate = fs/N -> skip 0), each row also zoomed to the waterfall's 2048
+    display columns (fft_scaler doZoom, full span), and
   * one VFO: RxVFO(61.44 MHz -> 240 kHz, bw 200 kHz, offset +2.5 MHz; plan_256 + 91-tap
     LPF) -> BroadcastFM mono (dev 100 kHz, 228-tap audio LPF) -> stereo_t,
-with every rank's last 16 spectra gathered to rank 0 over RCCL each step (N > 1).
+with every frame's display row gathered to rank 0 over RCCL each step (N > 1; libsdrgpu's
+C-ABI gather on its own stream, overlapping the next step).
 A step = one batch of B synthetic complex-float IQ samples resident in HBM
 (uniform [-1, 1), SpeedTester distribution). Other configs: c2 (1M-point BH7 spectrum,
 nz = 1e6, zero-padded), c3 (xlator + 256-tap FIR /8 + FM quadrature, fused), c4 (1024-channel
@@ -49,9 +51,10 @@ def parse():
 
 
 class C5:
-    """FFT(64k BH7) spectra + RxVFO + BroadcastFM mono, one stream per GPU."""
+    """FFT(64k BH7) spectra (+ 2048-column waterfall rows) + RxVFO + BroadcastFM mono, one stream per GPU."""
     N = 65536
     FS = 61.44e6
+    ZW = 2048
 
     def __init__(self, B, shard, dev):
         self.B = (B // self.N) * self.N
@@ -62,20 +65,28 @@ class C5:
         self.spectra = torch.empty(self.frames * self.N, dtype=torch.float32, device="cuda")
         self.ifbuf = torch.empty(2 * (self.B // 256 + 64), dtype=torch.float32, device="cuda")
         self.audio = torch.empty(2 * (self.B // 256 + 64), dtype=torch.float32, device="cuda")
-        self.bytes_per_sample = 8 + 4 + 8 / 256 + 8 / 256   # ~12.06 B
-        self.kernel_bytes = 12.0 * self.B                   # spectrum: 8 B in + 4 B dB out per sample
-        self.kernel_name = ("spectrum N=65536: fft_passA_kernel<256,32> (chunk 0) + fft_merged_kernel<256,32,256,32,false> "
-                            "(pass B chunk c + pass A chunk c+1) x15 + fft_passB_kernel<256,32> (last chunk)")
+        # the waterfall's display rows: every frame zoomed to ZW columns (full span, fft_scaler
+        # doZoom), fused into the transform's last pass; double-buffered for the rank-0 gather
+        self.zoom = [torch.empty(self.frames * self.ZW, dtype=torch.float32, device="cuda") for _ in range(2)]
+        self.with_zoom = os.environ.get("BENCH_C5_ZOOM", "1") != "0"
+        self.zoom_count = self.frames * self.ZW
+        self.bytes_per_sample = 8 + 4 + 4 / 32 + 8 / 256 + 8 / 256   # SURVEY 8(d) C5 (~12.06 B) + the zoom rows
+        self.kernel_bytes = (12.0 + 4 / 32) * self.B            # spectrum: 8 B in, 4 B dB + 4/32 B zoom out
+        self.kernel_name = ("spectrum N=65536 + zoom to 2048: fft_passA_kernel<256,32> (chunk 0) + "
+                            "fft_merged_kernel<256,32,256,32,false,zoom> (pass B chunk c + pass A chunk c+1) x15 + "
+                            "fft_passB_kernel<256,32,zoom> (last chunk)")
 
-    def run(self, x, s, timed_call):
+    def run(self, x, s, timed_call, buf=0):
         # the front end's splitter hands the same block to the spectrum and the VFO
         # (iq_frontend.cpp:15-52); the VFO output then feeds the WFM demodulator
-        timed_call(lambda: self.fft.execute_dev(x.data_ptr(), self.N, self.frames, self.spectra.data_ptr(), s))
+        if self.with_zoom:
+            timed_call(lambda: self.fft.execute_zoom_dev(x.data_ptr(), self.N, self.frames, self.spectra.data_ptr(),
+                                                         self.zoom[buf].data_ptr(), self.ZW, s))
+        else:   # (A/B only: BENCH_C5_ZOOM=0 drops the waterfall rows)
+            timed_call(lambda: self.fft.execute_dev(x.data_ptr(), self.N, self.frames, self.spectra.data_ptr(), s))
         m = self.vfo.process_dev(x.data_ptr(), self.B, self.ifbuf.data_ptr(), s)
         self.wfm.process_dev(self.ifbuf.data_ptr(), m, self.audio.data_ptr(), s)
 
-    def gather_src(self):
-        return self.spectra[-16 * self.N:]
 
 
 class C2:
@@ -98,9 +109,6 @@ class C2:
     def rest(self, x, s):
         pass
 
-    def gather_src(self):
-        return self.spectra[-2 * self.N:]
-
 
 class C3:
     """FrequencyXlator(-1.5 MHz) -> 256-tap DecimatingFIR /8 -> Quadrature(100 kHz), fused kernel."""
@@ -121,9 +129,6 @@ class C3:
 
     def rest(self, x, s):
         pass
-
-    def gather_src(self):
-        return self.out[:65536]
 
 
 class C4:
@@ -158,9 +163,6 @@ class C4:
 
     def rest(self, x, s):
         pass
-
-    def gather_src(self):
-        return self.out[:2 * 16 * self.M]
 
 
 def _run_generic(wl, x, s, timed_call):
@@ -202,7 +204,8 @@ def traffic_per_sample(config):
     return None, None
 
 
-WORKLOADS = {"c5": "C5 per-GPU slice: 64k BH7 FFT+log-mag (back-to-back) + RxVFO 61.44M->240k + BroadcastFM mono",
+WORKLOADS = {"c5": "C5 per-GPU slice: 64k BH7 FFT+log-mag (back-to-back) + 2048-column waterfall zoom + RxVFO "
+                   "61.44M->240k + BroadcastFM mono",
              "c2": "C2: 1M-point BH7 FFT + log-mag, nz=1e6 zero-padded, 256 frames/step",
              "c3": "C3: xlator + 256-tap FIR /8 + FM quadrature (fused), 2^28 samples/step",
              "c4": "C4: 1024-channel polyphase channelizer (16384-tap prototype), 2^28 samples/step"}
@@ -219,11 +222,15 @@ def run_config(config, a, shard, dev, stream):
     g = torch.Generator(device="cuda")
     g.manual_seed(shard.seed())
     x = (torch.rand(2 * B, device="cuda", generator=g) * 2 - 1).contiguous()   # complex_t interleaved
-    gather_bufs = None
-    if world > 1 and rank == 0:
-        gather_bufs = [torch.empty_like(wl.gather_src()) for _ in range(world)]
-    gather_stage = torch.empty_like(wl.gather_src()) if world > 1 else None
-    pending = [None]   # the in-flight gather (async work handle)
+    # N > 1: every step's waterfall rows go to rank 0 over RCCL (libsdrgpu's C-ABI gather) on a
+    # stream of their own, overlapping the next step; the zoom rows are double-buffered and a step
+    # waits only for the gather that last used its buffer
+    gather = shard.rccl_gather(dev) if (world > 1 and hasattr(wl, "zoom")) else None
+    if gather is not None:
+        gstream = torch.cuda.Stream()
+        gout = torch.empty(world * wl.zoom_count, dtype=torch.float32, device="cuda") if rank == 0 else None
+    done = [None, None]   # gather-finished events per zoom buffer
+    nstep = [0]
 
     ev = []
     # One stream for the whole step. Forking the spectrum and the VFO chain onto two streams
@@ -234,6 +241,8 @@ def run_config(config, a, shard, dev, stream):
     # (1.58 -> 1.89 ms), so the roofline numbers would stop describing the kernel.
     def step(timed):
         evs = []
+        buf = nstep[0] & 1
+        nstep[0] += 1
 
         def timed_call(fn):   # HIP events around the dominant kernel's launches, on their stream
             if timed:
@@ -243,25 +252,28 @@ def run_config(config, a, shard, dev, stream):
             if timed:
                 e1.record(stream)
                 evs.append((e0, e1))
+        if gather is not None and done[buf] is not None:
+            stream.wait_event(done[buf])
         if hasattr(wl, "run"):
-            wl.run(x, stream.cuda_stream, timed_call)
+            wl.run(x, stream.cuda_stream, timed_call, buf)
         else:
             _run_generic(wl, x, stream.cuda_stream, timed_call)
         if timed:
             ev.append(evs)
-        if world > 1:
-            # RCCL gather of this step's latest spectra, overlapped with the next step: the rows
-            # are snapshotted into a staging buffer (the next step overwrites them) and the
-            # collective runs on the process group's stream; it is waited on one step later
-            if pending[0] is not None:
-                pending[0].wait()
-            gather_stage.copy_(wl.gather_src())
-            pending[0], _ = shard.gather_spectra_async(gather_stage, gather_bufs)
+        if gather is not None:
+            ready = torch.cuda.Event()
+            ready.record(stream)
+            gstream.wait_event(ready)
+            gather.gather_dev(wl.zoom[buf].data_ptr(), wl.zoom_count, gout.data_ptr() if rank == 0 else 0,
+                              gstream.cuda_stream)
+            fin = torch.cuda.Event()
+            fin.record(gstream)
+            done[buf] = fin
 
     def drain():
-        if pending[0] is not None:
-            pending[0].wait()
-            pending[0] = None
+        for e in done:
+            if e is not None:
+                stream.wait_event(e)
 
     for _ in range(a.warmup):
         step(False)
@@ -277,6 +289,8 @@ def run_config(config, a, shard, dev, stream):
     elapsed = time.perf_counter() - t0
     kern_ms = sum(sum(e0.elapsed_time(e1) for e0, e1 in evs) for evs in ev) / max(len(ev), 1)
     elapsed, kern_ms = shard.max_over_ranks([elapsed, kern_ms], device="cuda")
+    if gather is not None:
+        gather.close()
     del x
     return B, elapsed, kern_ms, wl
 
@@ -329,7 +343,8 @@ def main():
             "metric": METRIC, "value": head["value"], "unit": "MS/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic uniform[-1,1) complex IQ in HBM",
-            "config": {"workload": head["workload"] + ("; RCCL gather of spectra to rank 0 each step" if world > 1 else ""),
+            "config": {"workload": head["workload"] + ("; every frame's 2048-column waterfall row gathered to rank 0 "
+                                                       "over RCCL (sdrgpu_gather_rows) each step" if world > 1 else ""),
                        "samples_per_gpu_per_step": B, "parallelism": f"replica-streams x{world}",
                        "bytes_per_sample": head["bytes_per_sample"]},
             "roofline": head["roofline"],

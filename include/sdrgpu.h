@@ -91,6 +91,11 @@ int sdrgpu_fft_set_window(sdrgpu_fft* h, const float* window, int nz);   /* exac
 int sdrgpu_fft_set_window_type(sdrgpu_fft* h, int windowType, int nz);
 /* device batch: frame f starts at in + f*frameStride complex samples; out: frames x N floats */
 int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, void* stream);
+/* rows + the waterfall's full-span zoom rows (fft_scaler(0, bw, bw, N, zoomSize).doZoom of each
+ * row, gui/widgets/fft_scaler.h:27-64) into zoomOut (frames x zoomSize floats). With N = 65536 and
+ * zoomSize = 2048 the zoom is fused into the transform's last pass. */
+int sdrgpu_fft_execute_zoom_dev(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out,
+                                float* zoomOut, int zoomSize, void* stream);
 /* spectrum + one RxVFO over the same device batch of `frames` back-to-back frames (frame stride
  * N, nz = N: fftRate = fs / N), the VFO reading the batch in place as the front end's splitter
  * feeds both (iq_frontend.cpp:15-52), on one stream. Returns the VFO's output count (vfoOut). */
@@ -203,6 +208,20 @@ int sdrgpu_frontend_spectra_dev(sdrgpu_frontend* f, const float** rows, int* nro
 int sdrgpu_frontend_read_spectra(sdrgpu_frontend* f, float* out, int maxRows);
 int sdrgpu_frontend_vfo_dev(sdrgpu_frontend* f, int id, const void** out, int* n);
 int sdrgpu_frontend_read_vfo(sdrgpu_frontend* f, int id, void* out, int max);
+
+/* ------------------------------------------ spectra gather (multi-GPU) ---- */
+/* Independent IQ streams run one per GPU; the only collective is a gather of their
+ * spectrum rows to rank 0 (the display) over RCCL / xGMI. Rank 0 makes a communicator id, the
+ * host hands it to every rank out of band, each rank creates its handle on its own GPU.
+ * gather_rows: `count` device floats of this rank -> rank 0's out[r * count + i] (out: world x
+ * count device floats, rank 0 only), asynchronous on `stream` (RCCL send/recv in one group).
+ * RCCL is loaded at first use; without it these calls fail with SDRGPU_ESTATE. */
+#define SDRGPU_GATHER_ID_BYTES 128
+typedef struct sdrgpu_gather sdrgpu_gather;
+int sdrgpu_gather_get_id(void* id /* SDRGPU_GATHER_ID_BYTES */);
+int sdrgpu_gather_create(sdrgpu_gather** g, int device, int rank, int world, const void* id);
+int sdrgpu_gather_rows(sdrgpu_gather* g, const float* rows, long long count, float* out, void* stream);
+int sdrgpu_gather_destroy(sdrgpu_gather* g);
 
 /* ---------------------------------------------- spectrum/IQ consumers ---- */
 /* waterfall zoom, fft_scaler(viewOffset, viewBandwidth, wholeBandwidth, fftSize, outSize).doZoom

@@ -66,6 +66,7 @@ def _load():
         "sdrgpu_fft_set_window_type": (i, [vp, i, i]),
         "sdrgpu_fft_execute_dev": (i, [vp, vp, ll, i, vp, vp]),
         "sdrgpu_fft_execute_vfo_dev": (i, [vp, vp, i, vp, vp, vp, vp]),
+        "sdrgpu_fft_execute_zoom_dev": (i, [vp, vp, ll, i, vp, vp, i, vp]),
         "sdrgpu_fft_logmag": (i, [vp, vp, vp]),
         "sdrgpu_fft_size": (i, [vp]),
         "sdrgpu_fft_destroy": (i, [vp]),
@@ -82,6 +83,10 @@ def _load():
         "sdrgpu_rxvfo_create": (i, [pp, i, d, d, d, d]),
         "sdrgpu_rxvfo_set_offset": (i, [vp, d]),
         "sdrgpu_ddc_create": (i, [pp, i, d, fp, i, i]),
+        "sdrgpu_gather_get_id": (i, [vp]),
+        "sdrgpu_gather_create": (i, [pp, i, i, i, vp]),
+        "sdrgpu_gather_rows": (i, [vp, vp, ll, vp, vp]),
+        "sdrgpu_gather_destroy": (i, [vp]),
         "sdrgpu_ddc_fm_create": (i, [pp, i, d, fp, i, i, d]),
         "sdrgpu_fm_create": (i, [pp, i, d, d, i, i]),
         "sdrgpu_wfm_create": (i, [pp, i, d, d, i]),

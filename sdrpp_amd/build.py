@@ -28,6 +28,7 @@ SOURCES = [
     ("frontend.hip", []),
     ("consumers.hip", ["-ffp-contract=off"]),   # bit-exact encoders
     ("file_source.cpp", []),
+    ("gather.cpp", []),
 ]
 
 
@@ -60,7 +61,7 @@ def build_lib(force=False):
                   "-I", os.path.join(ROOT, "include")] + extra + lang + ["-c", path, "-o", obj])
     lib = os.path.join(LIBDIR, "libsdrgpu.so")
     if force or _stale(lib, objs):
-        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs)
+        _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs + ["-ldl"])
     return lib
 
 

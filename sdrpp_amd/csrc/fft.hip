@@ -55,7 +55,10 @@ __device__ __forceinline__ void tile_loop(float2* lds, const float2* __restrict_
     finish(fr, v);
     stage_first<L>(lds + sF * LS, v, tF);
     __syncthreads();
-    stages_rest<L>(lds, tw, sL, tL, [&](int k, float2 y) { store(tile, k, y); });
+    stages_rest<L>(lds, tw, sL, tL, [&](int k, float2 y, int slot) {
+        if constexpr (std::is_invocable_v<Store&, int, int, float2, int>) store(tile, k, y, slot);
+        else store(tile, k, y);
+    });
 }
 
 struct FragW {   // raw input + window values for 16 samples
@@ -365,16 +368,54 @@ __global__ __launch_bounds__(S / 2 * L / 16) void fft_passA2_kernel(
 // ---- pass B: S rows of length N2 per tile, dB out, transposed store -----------------
 // Stage 1 maps threads row-contiguous (coalesced row reads); the last stage maps the row
 // index fastest so the transposed dB store writes S consecutive floats per k2.
-template <int L, int S>
+// DPP move of a float: lanes outside row_mask keep `old`
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_f(float old, float src) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, src),
+                                                                 CTRL, ROWMASK, 0xF, false));
+}
+
+// lane exchange with the partner lane ^ D (D = 1, 2, 4, 8: within a 16-lane DPP row)
+template <int D>
+__device__ __forceinline__ float xchg(float v, int lane) {
+    if constexpr (D == 1) return dpp_f<0xB1, 0xF>(v, v);             // quad_perm [1,0,3,2]
+    else if constexpr (D == 2) return dpp_f<0x4E, 0xF>(v, v);        // quad_perm [2,3,0,1]
+    else {                                                            // row_shr:D / row_shl:D
+        const float dn = dpp_f<0x110 + D, 0xF>(v, v), up = dpp_f<0x100 + D, 0xF>(v, v);
+        return (lane & D) ? dn : up;
+    }
+}
+// one transpose-reduce step over the value pairs (v[i], v[i + H]): the lane whose bit D is 0
+// keeps the lower half and takes its partner's, the other keeps the upper half
+template <int D, int H>
+__device__ __forceinline__ void tr_step(float (&v)[16], int lane) {
+    const bool hi = (lane & D) != 0;
+#pragma unroll
+    for (int i = 0; i < H; i++) {
+        const float send = hi ? v[i] : v[i + H];
+        const float keep = hi ? v[i + H] : v[i];
+        v[i] = fmaxf(keep, xchg<D>(send, lane));
+    }
+}
+
+// ZM: also the waterfall's full-span zoom row (fft_scaler::doZoom with viewOffset 0 and the whole
+// bandwidth in view, gui/widgets/fft_scaler.h:27-64) at factor S: out width N / S, zoom[o] = max of
+// the S consecutive bins [S o, S o + S) = the bins b*S + sL of one k2, held by the S lanes sL of a
+// half-wave. Each lane keeps its 16 dB values (k2 = tL + 16 r); a 16-value transpose-reduce over
+// the lane bits 0..3 (DPP, VALU only) leaves in every lane the max over its 16-lane row of one r,
+// one swizzle (xor 16) folds the two rows, and lanes 16..31 store the half-wave's 16 zoom values
+// with one instruction.
+template <int L, int S, bool ZM = false>
 __device__ __forceinline__ void passB_tile(
     float2* lds, int tile, const float2* __restrict__ scratch, int frames, int N1, int logN, const float2* __restrict__ tw,
-    float* __restrict__ out) {
+    float* __restrict__ out, float* __restrict__ zoom = nullptr) {
     constexpr int T = L / 16;
     const int tid = threadIdx.x;
     const int sF = tid / T, tF = tid % T;
     const int sL = tid % S, tL = tid / S;
     const int nb = N1 / S;
     const int ntiles = nb * frames;
+    float dbv[16];   // ZM: this lane's dB values, r = k2 >> 4
     tile_loop<L, FragC>(
         lds, tw, tile, ntiles, sF, tF, sL, tL,
         [&](FragC& fr, int tile) {
@@ -388,35 +429,56 @@ __device__ __forceinline__ void passB_tile(
 #pragma unroll
             for (int r = 0; r < 16; r++) v[r] = fr.x[r];
         },
-        [&](int tile, int k2, float2 y) {
+        [&](int tile, int k2, float2 y, int slot) {
             const int b = tile % nb;
             const long long f = tile / nb;
-            out[(f << logN) + b * S + sL + (long long)N1 * k2] = db_of(y);
+            const float d = db_of(y);
+            out[(f << logN) + b * S + sL + (long long)N1 * k2] = d;
+            if constexpr (ZM) dbv[slot] = d;   // stage_last<256, 16, 16>: slot r <-> k2 = tL + 16 r
         });
+    if constexpr (ZM) {
+        static_assert(S == 32 && L == 256, "zoom: one half-wave per zoomed bin, k2 = tL + 16 r");
+        if (tile >= ntiles) return;
+        const int lane = tid & 63;
+        tr_step<1, 8>(dbv, lane);
+        tr_step<2, 4>(dbv, lane);
+        tr_step<4, 2>(dbv, lane);
+        tr_step<8, 1>(dbv, lane);
+        // lane bits (b0 b1 b2 b3) now select r = 8 b0 + 4 b1 + 2 b2 + b3; fold the two rows: lane
+        // i ^ 16 holds the same r (ds_swizzle xor 16 within 32 lanes: and 0x1F, xor 0x10)
+        const float m = fmaxf(dbv[0], __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, dbv[0]), 0x401F)));
+        if (sL >= 16) {
+            const int j = sL - 16;
+            const int r = ((j & 1) << 3) | ((j & 2) << 1) | ((j & 4) >> 1) | ((j & 8) >> 3);
+            const int b = tile % nb;
+            const long long f = tile / nb;
+            zoom[(f << logN) / S + b + (long long)(N1 / S) * (tL + 16 * r)] = m;
+        }
+    }
 }
 
-template <int L, int S>
+template <int L, int S, bool ZM>
 __global__ __launch_bounds__(S * L / 16) void fft_passB_kernel(
     const float2* __restrict__ scratch, int frames, int N1, int logN, const float2* __restrict__ tw,
-    float* __restrict__ out) {
+    float* __restrict__ out, float* __restrict__ zoom) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    passB_tile<L, S>(lds, blockIdx.x, scratch, frames, N1, logN, tw, out);
+    passB_tile<L, S, ZM>(lds, blockIdx.x, scratch, frames, N1, logN, tw, out, zoom);
 }
 
 // ---- merged launch: pass B of chunk c (first nB workgroups) + pass A of chunk c+1 --------
 // The two halves share nothing (pass A writes the other scratch buffer), so one launch
 // replaces two dependent kernel boundaries per chunk; the pass-B workgroups are dispatched
 // first and pass A fills the CUs as they drain. Needs equal thread counts (SA*LA == SB*LB).
-template <int LA, int SA, int LB, int SB, bool PAIRED>
+template <int LA, int SA, int LB, int SB, bool PAIRED, bool ZM>
 __global__ __launch_bounds__((PAIRED ? SA / 2 : SA) * LA / 16) __attribute__((amdgpu_waves_per_eu(4))) void fft_merged_kernel(
-    int nB, const float2* __restrict__ scratchB, int framesB, float* __restrict__ outB,
+    int nB, const float2* __restrict__ scratchB, int framesB, float* __restrict__ outB, float* __restrict__ zoomB,
     const float2* __restrict__ in, long long frameStride, int framesA, const float* __restrict__ win, int nz,
     int logN, const float2* __restrict__ tw1, const float2* __restrict__ tw2, const float2* __restrict__ tfull,
     float2* __restrict__ scratchA) {
     static_assert((PAIRED ? SA / 2 : SA) * LA == SB * LB, "merged pass kernels need equal workgroup sizes");
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     if ((int)blockIdx.x < nB) {
-        passB_tile<LB, SB>(lds, blockIdx.x, scratchB, framesB, LA, logN, tw2, outB);
+        passB_tile<LB, SB, ZM>(lds, blockIdx.x, scratchB, framesB, LA, logN, tw2, outB, zoomB);
     } else if constexpr (PAIRED) {
         passA2_tile<LA, SA>(lds, blockIdx.x - nB, in, frameStride, framesA, win, nz, LB, logN, tw1, tfull, scratchA);
     } else {
@@ -445,6 +507,8 @@ struct FftPlan {
     // instead of two; 1.87 -> 1.73 ms per 2^28 samples (A/B on one box). SDRGPU_FFT_MERGE=0 off.
     int merge = 1;
     StreamOrder order;                // scratch is per plan: calls on different streams are serialised
+    sdrgpu_zoom* zoom = nullptr;      // execute_zoom's unfused zoom (sizes other than N / 32)
+    int zoomSize = 0;
     hipStream_t s2 = nullptr;
     hipEvent_t evFork = nullptr, evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr};
     DevBuf scratch2;
@@ -506,26 +570,26 @@ static int launch_passA2(const FftPlan& p, const float2* in, long long stride, i
     return SDRGPU_OK;
 }
 
-template <int L, int S>
-static int launch_passB(const FftPlan& p, int frames, float* out, hipStream_t s) {
-    auto k = fft_passB_kernel<L, S>;
+template <int L, int S, bool ZM = false>
+static int launch_passB(const FftPlan& p, int frames, float* out, hipStream_t s, float* zoom = nullptr) {
+    auto k = fft_passB_kernel<L, S, ZM>;
     size_t lds = sizeof(float2) * S * Lds<L>::LS;
     SDRGPU_CHECK(set_lds(k, lds));
     const int g = (p.N1 / S) * frames;
     hipLaunchKernelGGL(k, dim3(g), dim3(S * L / 16), lds, s, p.cur, frames, p.N1, p.logN,
-                       p.tw2.as<float2>(), out);
+                       p.tw2.as<float2>(), out, zoom);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
 
-template <int LA, int SA, int LB, int SB, bool PAIRED>
+template <int LA, int SA, int LB, int SB, bool PAIRED, bool ZM = false>
 static int launch_merged(const FftPlan& p, const float2* scratchB, int framesB, float* outB, const float2* in,
-                         long long stride, int framesA, float2* scratchA, hipStream_t s) {
-    auto k = fft_merged_kernel<LA, SA, LB, SB, PAIRED>;
+                         long long stride, int framesA, float2* scratchA, hipStream_t s, float* zoomB = nullptr) {
+    auto k = fft_merged_kernel<LA, SA, LB, SB, PAIRED, ZM>;
     size_t lds = sizeof(float2) * std::max(SA * Lds<LA>::LS + ((PAIRED || LA == 256) ? LA : 0), SB * Lds<LB>::LS);
     SDRGPU_CHECK(set_lds(k, lds));
     const int nB = (LA / SB) * framesB, nA = (LB / SA) * framesA;
-    hipLaunchKernelGGL(k, dim3(nB + nA), dim3(SB * LB / 16), lds, s, nB, scratchB, framesB, outB, in, stride, framesA,
+    hipLaunchKernelGGL(k, dim3(nB + nA), dim3(SB * LB / 16), lds, s, nB, scratchB, framesB, outB, zoomB, in, stride, framesA,
                        p.win.as<float>(), p.nz, p.logN, p.tw1.as<float2>(), p.tw2.as<float2>(), p.tfull.as<float2>(),
                        scratchA);
     SDRGPU_HIP(hipGetLastError());
@@ -537,7 +601,8 @@ static int launch_merged(const FftPlan& p, const float2* scratchB, int framesB, 
 // threads) measured 12% SLOWER (2.68 vs 2.39 ms per 256 frames): pass B loses half its
 // occupancy to pass A's 147 KB of LDS, so the 1M transform keeps separate launches.
 static int dispatch_merged(const FftPlan& p, const float2* scratchB, int framesB, float* outB, const float2* in,
-                           long long stride, int framesA, float2* scratchA, hipStream_t s) {
+                           long long stride, int framesA, float2* scratchA, hipStream_t s, float* zoomB = nullptr) {
+    if (zoomB) return launch_merged<256, 32, 256, 32, false, true>(p, scratchB, framesB, outB, in, stride, framesA, scratchA, s, zoomB);
     if (p.sa == 64) return launch_merged<256, 64, 256, 64, false>(p, scratchB, framesB, outB, in, stride, framesA, scratchA, s);
     if (p.sa == 32) return launch_merged<256, 32, 256, 32, false>(p, scratchB, framesB, outB, in, stride, framesA, scratchA, s);
     return launch_merged<256, 16, 256, 16, false>(p, scratchB, framesB, outB, in, stride, framesA, scratchA, s);
@@ -594,7 +659,8 @@ static int dispatch_passA2(const FftPlan& p, const float2* in, long long stride,
     return SDRGPU_EARG;
 }
 
-static int dispatch_passB(const FftPlan& p, int frames, float* out, hipStream_t s) {
+static int dispatch_passB(const FftPlan& p, int frames, float* out, hipStream_t s, float* zoom = nullptr) {
+    if (zoom) return launch_passB<256, 32, true>(p, frames, out, s, zoom);   // (zoom_fusable checked the plan)
     switch (p.N2) {
     case 64: return launch_passB<64, 32>(p, frames, out, s);
     case 128: return launch_passB<128, 32>(p, frames, out, s);
@@ -712,19 +778,21 @@ extern "C" int sdrgpu_fft_set_window_type(sdrgpu_fft* h, int windowType, int nz)
 
 extern "C" int sdrgpu_fft_size(sdrgpu_fft* h) { return h ? h->p.N : SDRGPU_EARG; }
 
-extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out,
-                                      void* stream) {
-    if (!h || !in || !out || frames < 0 || frameStride < 0) { set_error("fft_execute: bad argument"); return SDRGPU_EARG; }
-    if (frames == 0) return 0;
+static bool zoom_fusable(const FftPlan& p, int zoomSize) {
+    return p.N1 == 256 && p.N2 == 256 && p.sa == 32 && p.sb == 32 && zoomSize * 32 == p.N;
+}
+
+// frames -> dB rows (and, with zoom != nullptr on a zoom_fusable plan, the full-span zoom rows)
+static int fft_execute(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, float* zoom,
+                       hipStream_t s) {
     FftPlan& p = h->p;
-    SDRGPU_SET_DEVICE(p.device);
-    hipStream_t s = stream ? (hipStream_t)stream : p.own;
-    SDRGPU_CHECK(p.order.follow(s));
     const float2* x = (const float2*)in;
     if (p.N1 == 0) {
         SDRGPU_CHECK(dispatch_single(p, x, frameStride, frames, out, s));
         return frames;
     }
+    const long long zw = p.N / 32;   // zoom row width when fused
+    auto zoomAt = [&](long long f0) { return zoom ? zoom + f0 * zw : nullptr; };
     // 16-B loads need an even frame stride and a 16-B aligned base
     const bool paired = p.sa2 > 0 && (frameStride % 2) == 0 && ((uintptr_t)in & 15) == 0;
     const int nchunks = (frames + p.chunkFrames - 1) / p.chunkFrames;
@@ -741,14 +809,14 @@ extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long f
             const int fB = (c - 1) * p.chunkFrames, nfB = p.chunkFrames;
             const int fA = c * p.chunkFrames, nfA = std::min(p.chunkFrames, frames - fA);
             SDRGPU_CHECK(dispatch_merged(p, sc[(c - 1) & 1], nfB, out + (long long)fB * p.N,
-                                         x + (long long)fA * frameStride, frameStride, nfA, sc[c & 1], s));
+                                         x + (long long)fA * frameStride, frameStride, nfA, sc[c & 1], s, zoomAt(fB)));
         }
         const int fL = (nchunks - 1) * p.chunkFrames;
         p.cur = sc[(nchunks - 1) & 1];
-        SDRGPU_CHECK(dispatch_passB(p, frames - fL, out + (long long)fL * p.N, s));
+        SDRGPU_CHECK(dispatch_passB(p, frames - fL, out + (long long)fL * p.N, s, zoomAt(fL)));
         return frames;
     }
-    const bool pipe = p.pipe && nchunks > 1;
+    const bool pipe = p.pipe && nchunks > 1 && !zoom;
     if (pipe) {
         if (!p.s2) {
             SDRGPU_HIP(hipStreamCreateWithFlags(&p.s2, hipStreamNonBlocking));
@@ -777,10 +845,48 @@ extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long f
             SDRGPU_HIP(hipStreamWaitEvent(p.s2, p.evA[b], 0));
             sb = p.s2;
         }
-        SDRGPU_CHECK(dispatch_passB(p, nf, out + (long long)f0 * p.N, sb));
+        SDRGPU_CHECK(dispatch_passB(p, nf, out + (long long)f0 * p.N, sb, zoomAt(f0)));
         if (pipe) SDRGPU_HIP(hipEventRecord(p.evB[b], p.s2));
     }
     if (pipe) SDRGPU_HIP(hipStreamWaitEvent(s, p.evB[(nchunks - 1) & 1], 0));   // join
+    return frames;
+}
+
+extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out,
+                                      void* stream) {
+    if (!h || !in || !out || frames < 0 || frameStride < 0) { set_error("fft_execute: bad argument"); return SDRGPU_EARG; }
+    if (frames == 0) return 0;
+    FftPlan& p = h->p;
+    SDRGPU_SET_DEVICE(p.device);
+    hipStream_t s = stream ? (hipStream_t)stream : p.own;
+    SDRGPU_CHECK(p.order.follow(s));
+    return fft_execute(h, in, frameStride, frames, out, nullptr, s);
+}
+
+// Rows + the waterfall's full-span zoom rows: fft_scaler(0, bw, bw, N, zoomSize).doZoom of every
+// row (gui/widgets/fft_scaler.h:27-64: max over the bins [round(f0), round(f0 + N / zoomSize))).
+// On the 64k plan with zoomSize = N / 32 the zoom is fused into pass B's dB store (the rows are
+// not read again); any other size runs the zoom kernel over the rows afterwards.
+extern "C" int sdrgpu_fft_execute_zoom_dev(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out,
+                                           float* zoomOut, int zoomSize, void* stream) {
+    if (!h || !in || !out || !zoomOut || frames < 0 || frameStride < 0 || zoomSize <= 0 || zoomSize > h->p.N) {
+        set_error("fft_execute_zoom: bad argument");
+        return SDRGPU_EARG;
+    }
+    if (frames == 0) return 0;
+    FftPlan& p = h->p;
+    SDRGPU_SET_DEVICE(p.device);
+    hipStream_t s = stream ? (hipStream_t)stream : p.own;
+    SDRGPU_CHECK(p.order.follow(s));
+    if (zoom_fusable(p, zoomSize)) return fft_execute(h, in, frameStride, frames, out, zoomOut, s);
+    SDRGPU_CHECK(fft_execute(h, in, frameStride, frames, out, nullptr, s));
+    if (!p.zoom || p.zoomSize != zoomSize) {
+        if (p.zoom) sdrgpu_zoom_destroy(p.zoom);
+        p.zoom = nullptr;
+        SDRGPU_CHECK(sdrgpu_zoom_create(&p.zoom, p.device, 0.0, 1.0, 1.0, p.N, zoomSize));
+        p.zoomSize = zoomSize;
+    }
+    SDRGPU_CHECK(sdrgpu_zoom_execute_dev(p.zoom, out, frames, zoomOut, s));
     return frames;
 }
 
@@ -833,6 +939,7 @@ extern "C" int sdrgpu_fft_destroy(sdrgpu_fft* h) {
     if (!h) return SDRGPU_OK;
     (void)hipSetDevice(h->p.device);
     if (h->p.own) (void)hipStreamDestroy(h->p.own);
+    if (h->p.zoom) sdrgpu_zoom_destroy(h->p.zoom);
     if (h->p.s2) {
         (void)hipStreamSynchronize(h->p.s2);
         (void)hipStreamDestroy(h->p.s2);

@@ -3,6 +3,7 @@
 // LDS -> LDS / LDS -> store stages. Forward transform (e^{-i}), unnormalised.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 namespace sdrgpu {
 
@@ -128,7 +129,12 @@ __device__ __forceinline__ void stage_last(const float2* seq, const float2* __re
         const int j = t + b * T;
         const int idxD = (j / NS) * NS * R + (j % NS);
 #pragma unroll
-        for (int r = 0; r < R; r++) st(idxD + r * NS, v[b][r]);
+        for (int r = 0; r < R; r++) {
+            // a store functor may also take the output's register slot (a compile-time constant
+            // after unrolling), e.g. to keep the outputs in a register array
+            if constexpr (std::is_invocable_v<Store&, int, float2, int>) st(idxD + r * NS, v[b][r], b * R + r);
+            else st(idxD + r * NS, v[b][r]);
+        }
     }
 }
 

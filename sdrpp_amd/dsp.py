@@ -235,6 +235,11 @@ class FFTSpectrum:
         return check(lib.sdrgpu_fft_execute_dev(self._h, _vp(in_ptr), int(frame_stride), int(frames), _vp(out_ptr),
                                                 _vp(stream or 0)))
 
+    def execute_zoom_dev(self, in_ptr, frame_stride, frames, out_ptr, zoom_ptr, zoom_size, stream=None):
+        """dB rows + the waterfall's full-span zoom rows (frames x zoom_size; fused at 64k / 2048)."""
+        return check(lib.sdrgpu_fft_execute_zoom_dev(self._h, _vp(in_ptr), int(frame_stride), int(frames), _vp(out_ptr),
+                                                     _vp(zoom_ptr), int(zoom_size), _vp(stream or 0)))
+
     def execute_vfo_dev(self, in_ptr, frames, out_ptr, vfo, vfo_out_ptr, stream=None):
         """Spectra of `frames` back-to-back frames + one RxVFO over the same device batch (the VFO's
         first stage fused into the 64k spectrum's input pass); returns the VFO's output count."""
@@ -488,6 +493,38 @@ class Deemphasis(Block):
     def __init__(self, tau, samplerate, stereo=False, device=0):
         h = _make(lib.sdrgpu_deemphasis_create, device, C64 if stereo else F32, float(tau), float(samplerate))
         super().__init__(h, STEREO if stereo else np.float32, STEREO if stereo else np.float32)
+
+
+def gather_id():
+    """Rank 0: a new RCCL communicator id (bytes) for SpectraGather."""
+    buf = ctypes.create_string_buffer(128)
+    check(lib.sdrgpu_gather_get_id(buf))
+    return buf.raw
+
+
+class SpectraGather:
+    """Rank-0 gather of spectrum rows over RCCL (sdrgpu_gather_*): one rank per GPU / IQ stream."""
+
+    def __init__(self, rank, world, comm_id, device=0):
+        assert len(comm_id) == 128
+        self.rank, self.world = rank, world
+        self._id = ctypes.create_string_buffer(bytes(comm_id), 128)
+        self._h = _make(lib.sdrgpu_gather_create, int(device), int(rank), int(world), self._id)
+
+    def gather_dev(self, rows_ptr, count, out_ptr, stream=None):
+        """count device floats -> rank 0's out (world x count); asynchronous on `stream`."""
+        check(lib.sdrgpu_gather_rows(self._h, _vp(rows_ptr), int(count), _vp(out_ptr or 0), _vp(stream or 0)))
+
+    def close(self):
+        if self._h:
+            lib.sdrgpu_gather_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Zoom:

@@ -15,7 +15,7 @@ public:
 
     void init(stream<complex_t>* in, double offset) {
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_xlator_create(&h, gpu::device(), offset), "xlator_create");
+        gpu::ok(sdrgpu_xlator_create(&h, _h.bind(gpu::device()), offset), "xlator_create");
         _h.reset(h);
         base_type::init(in);
     }

@@ -55,6 +55,15 @@ public:
         gpu::ok(sdrgpu_block_reset(_h.h), "rxvfo_reset");
         base_type::tempStart();
     }
+    // GPU placement (sdrgpu_handle.h): this VFO's device; setDevice moves it (state restarts)
+    int getDevice() const { return _h.dev; }
+    void setDevice(int device) {
+        std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx);
+        base_type::tempStop();
+        _h.dev = device;
+        rebuild();
+        base_type::tempStart();
+    }
     inline int process(int count, const complex_t* in, complex_t* out) { return _h.process(in, count, out, "rxvfo"); }
     int run() override {
         int count = base_type::_in->read();
@@ -69,7 +78,7 @@ public:
 protected:
     void rebuild() {
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_rxvfo_create(&h, gpu::device(), _inSamplerate, _outSamplerate, _bandwidth, _offset), "rxvfo_create");
+        gpu::ok(sdrgpu_rxvfo_create(&h, _h.bind(gpu::stream_device()), _inSamplerate, _outSamplerate, _bandwidth, _offset), "rxvfo_create");
         _h.reset(h);
     }
     double _inSamplerate = 0, _outSamplerate = 0, _bandwidth = 0, _offset = 0;

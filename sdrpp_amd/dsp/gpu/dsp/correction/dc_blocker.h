@@ -15,7 +15,7 @@ public:
     DCBlocker(stream<T>* in, double rate, double samplerate) { init(in, rate, samplerate); }
     void init(stream<T>* in, double rate) {
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_dc_blocker_create(&h, gpu::device(), std::is_same_v<T, float> ? SDRGPU_F32 : SDRGPU_C64, rate), "dc_blocker_create");
+        gpu::ok(sdrgpu_dc_blocker_create(&h, _h.bind(gpu::device()), std::is_same_v<T, float> ? SDRGPU_F32 : SDRGPU_C64, rate), "dc_blocker_create");
         _h.reset(h);
         base_type::init(in);
     }

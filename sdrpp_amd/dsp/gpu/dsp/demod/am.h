@@ -67,7 +67,7 @@ protected:
     void ad() { std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx); gpu::ok(sdrgpu_demod_agc_set_attack_decay(_h.h, _attack, _decay), "am_set_attack_decay"); }
     void rebuild() {
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_am_create(&h, gpu::device(), (int)_agcMode, _bandwidth, _attack, _decay, _dcRate, _samplerate,
+        gpu::ok(sdrgpu_am_create(&h, _h.bind(gpu::device()), (int)_agcMode, _bandwidth, _attack, _decay, _dcRate, _samplerate,
                                  std::is_same_v<T, stereo_t>), "am_create");
         _h.reset(h);
     }

@@ -77,10 +77,10 @@ protected:
     void rebuild() {
         sdrgpu_block* h = nullptr;
         if (_stereo || _rdsOut) {
-            gpu::ok(sdrgpu_broadcast_fm_create(&h, gpu::device(), _deviation, _samplerate, _stereo, _lowPass), "broadcast_fm_create");
+            gpu::ok(sdrgpu_broadcast_fm_create(&h, _h.bind(gpu::device()), _deviation, _samplerate, _stereo, _lowPass), "broadcast_fm_create");
             if (h && _rdsOut) gpu::ok(sdrgpu_broadcast_fm_set_rds(h, 1), "broadcast_fm_set_rds");
         } else {
-            gpu::ok(sdrgpu_wfm_create(&h, gpu::device(), _deviation, _samplerate, _lowPass), "wfm_create");
+            gpu::ok(sdrgpu_wfm_create(&h, _h.bind(gpu::device()), _deviation, _samplerate, _lowPass), "wfm_create");
         }
         _h.reset(h);
     }

@@ -60,7 +60,7 @@ private:
     }
     void rebuild() {
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_fm_create(&h, gpu::device(), _samplerate, _bandwidth, _lowPass, _highPass), "fm_create");
+        gpu::ok(sdrgpu_fm_create(&h, _h.bind(gpu::device()), _samplerate, _bandwidth, _lowPass, _highPass), "fm_create");
         _h.reset(h);
     }
     double _samplerate = 0, _bandwidth = 0;

@@ -14,7 +14,7 @@ public:
     Quadrature(stream<complex_t>* in, double deviation, double samplerate) { init(in, deviation, samplerate); }
     virtual void init(stream<complex_t>* in, double deviation) {
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_quadrature_create(&h, gpu::device(), deviation), "quadrature_create");
+        gpu::ok(sdrgpu_quadrature_create(&h, _h.bind(gpu::device()), deviation), "quadrature_create");
         _h.reset(h);
         base_type::init(in);
     }

@@ -48,7 +48,7 @@ protected:
     }
     void rebuild() {
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_ssb_create(&h, gpu::device(), (int)_mode, _bandwidth, _samplerate, _agcEnabled, _attack, _decay,
+        gpu::ok(sdrgpu_ssb_create(&h, _h.bind(gpu::device()), (int)_mode, _bandwidth, _samplerate, _agcEnabled, _attack, _decay,
                                   std::is_same_v<T, stereo_t>), "ssb_create");
         _h.reset(h);
     }

@@ -19,7 +19,7 @@ public:
         _tau = tau;
         _samplerate = samplerate;
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_deemphasis_create(&h, gpu::device(), std::is_same_v<T, float> ? SDRGPU_F32 : SDRGPU_C64, tau, samplerate),
+        gpu::ok(sdrgpu_deemphasis_create(&h, _h.bind(gpu::device()), std::is_same_v<T, float> ? SDRGPU_F32 : SDRGPU_C64, tau, samplerate),
                 "deemphasis_create");
         _h.reset(h);
         base_type::init(in);

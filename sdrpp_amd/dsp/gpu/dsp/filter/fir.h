@@ -49,7 +49,7 @@ protected:
     void init(stream<D>* in, tap<T>& taps, int decim) {
         _taps = taps;
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_fir_create(&h, gpu::device(), dtype(), ttype(), (const float*)taps.taps, (int)taps.size, decim),
+        gpu::ok(sdrgpu_fir_create(&h, _h.bind(gpu::device()), dtype(), ttype(), (const float*)taps.taps, (int)taps.size, decim),
                 "fir_create");
         _h.reset(h);
         base_type::init(in);

@@ -17,7 +17,7 @@ public:
     void init(stream<T>* in, double setPoint, double attack, double decay, double maxGain, double maxOutputAmp, double initGain = 1.0) {
         _setPoint = setPoint; _attack = attack; _decay = decay; _maxGain = maxGain; _maxOutputAmp = maxOutputAmp; _initGain = initGain;
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_agc_create(&h, gpu::device(), std::is_same_v<T, complex_t> ? SDRGPU_C64 : SDRGPU_F32, setPoint, attack,
+        gpu::ok(sdrgpu_agc_create(&h, _h.bind(gpu::device()), std::is_same_v<T, complex_t> ? SDRGPU_C64 : SDRGPU_F32, setPoint, attack,
                                   decay, maxGain, maxOutputAmp, initGain), "agc_create");
         _h.reset(h);
         base_type::init(in);

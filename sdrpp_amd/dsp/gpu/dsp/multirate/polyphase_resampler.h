@@ -44,7 +44,7 @@ public:
 protected:
     void build(int interp, int decim, tap<float>& taps) {
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_polyphase_resampler_create(&h, gpu::device(), std::is_same_v<T, float> ? SDRGPU_F32 : SDRGPU_C64,
+        gpu::ok(sdrgpu_polyphase_resampler_create(&h, _h.bind(gpu::device()), std::is_same_v<T, float> ? SDRGPU_F32 : SDRGPU_C64,
                                                   interp, decim, taps.taps, (int)taps.size), "polyphase_create");
         _h.reset(h);
     }

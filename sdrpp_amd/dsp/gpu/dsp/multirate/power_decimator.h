@@ -45,7 +45,7 @@ public:
 protected:
     void build() {
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_power_decimator_create(&h, gpu::device(), std::is_same_v<T, float> ? SDRGPU_F32 : SDRGPU_C64,
+        gpu::ok(sdrgpu_power_decimator_create(&h, _h.bind(gpu::device()), std::is_same_v<T, float> ? SDRGPU_F32 : SDRGPU_C64,
                                               (int)_ratio), "power_decimator_create");
         _h.reset(h);
     }

@@ -49,7 +49,7 @@ public:
 protected:
     void reconfigure() {
         sdrgpu_block* h = nullptr;
-        gpu::ok(sdrgpu_rational_resampler_create(&h, gpu::device(), std::is_same_v<T, float> ? SDRGPU_F32 : SDRGPU_C64,
+        gpu::ok(sdrgpu_rational_resampler_create(&h, _h.bind(gpu::device()), std::is_same_v<T, float> ? SDRGPU_F32 : SDRGPU_C64,
                                                  _inSamplerate, _outSamplerate), "rational_create");
         _h.reset(h);
     }

@@ -26,7 +26,8 @@ public:
         }
         if (_h) sdrgpu_fft_destroy(_h);
         _h = nullptr;
-        return ok(sdrgpu_fft_create(&_h, device(), size, nz, windowType), "fft_create");
+        if (_dev < 0) _dev = device();   // placement (sdrgpu_handle.h), kept across size changes
+        return ok(sdrgpu_fft_create(&_h, _dev, size, nz, windowType), "fft_create");
     }
     // IQFrontEnd::handler body: `data` holds nz samples (Reshaper keep = nz)
     template <class Acquire, class Release>
@@ -37,8 +38,10 @@ public:
         (void)count;
     }
     sdrgpu_fft* raw() { return _h; }
+    int getDevice() const { return _dev; }
 
 private:
     sdrgpu_fft* _h = nullptr;
+    int _dev = -1;
 };
 }  // namespace dsp::gpu

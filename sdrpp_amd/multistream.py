@@ -2,8 +2,10 @@
 
 SDR++ has no multi-device code; independent IQ streams (one SDR per
 GPU) shard with no per-sample exchange. The only collective is a rank-0 gather of the
-latest spectra for display (RCCL over xGMI via torch.distributed "nccl"; "gloo" on CPU for
-tests). Timing is the max over ranks.
+spectrum rows for display. On GPUs it is libsdrgpu's C-ABI RCCL gather (sdrgpu_gather_*,
+the same call a C++ host makes), its 128-byte communicator id handed from rank 0 to the
+other ranks through torch.distributed; on the CPU ("gloo", tests) torch's gather stands in.
+Timing is the max over ranks.
 """
 import os
 
@@ -32,6 +34,16 @@ class StreamShard:
 
     def vfo_offset(self, base=2.5e6, step=1e5):
         return base + step * self.rank
+
+    def rccl_gather(self, device):
+        """A libsdrgpu SpectraGather for this rank (GPU runs, world > 1): rank 0 makes the RCCL id
+        and broadcasts it to the other ranks over the process group."""
+        from sdrpp_amd import dsp
+        cid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if self.rank == 0:
+            cid.copy_(torch.frombuffer(bytearray(dsp.gather_id()), dtype=torch.uint8))
+        dist.broadcast(cid, src=0)
+        return dsp.SpectraGather(self.rank, self.world, bytes(cid.cpu().numpy().tobytes()), device=device)
 
     def gather_spectra(self, local_rows, out_list=None):
         """Gather every rank's latest spectra rows to rank 0 (list indexed by rank there)."""

@@ -195,6 +195,43 @@ int main() {
         CHECK(std::memcmp(e.data(), g.data(), sizeof(float) * n) == 0, "Deemphasis not bit-exact");
         std::printf("Deemphasis<float>: bit-exact %s\n", std::memcmp(e.data(), g.data(), sizeof(float) * n) == 0 ? "yes" : "NO");
     }
+    // device placement (sdrgpu_handle.h): a DeviceScope pins the blocks built in it; without one,
+    // SDRGPU_PLACEMENT=spread deals the RxVFOs round-robin over the visible GPUs; the device is
+    // kept across re-plans; setDevice moves a VFO and it still matches a fresh one
+    {
+        const int ndev = sdrgpu_device_count();
+        {
+            dsp::gpu::DeviceScope on(ndev - 1);
+            dsp::stream<dsp::complex_t> in;
+            dsp::channel::RxVFO v(&in, 61.44e6, 240000, 200000, 2.5e6);
+            CHECK(v.getDevice() == ndev - 1, "scope placement: %d", v.getDevice());
+            v.setBandwidth(150000);
+            CHECK(v.getDevice() == ndev - 1, "device kept across a re-plan: %d", v.getDevice());
+        }
+        setenv("SDRGPU_PLACEMENT", "spread", 1);
+        std::vector<int> seen;
+        for (int k = 0; k < 2 * ndev; k++) {
+            dsp::stream<dsp::complex_t> in;
+            dsp::channel::RxVFO v(&in, 61.44e6, 240000, 200000, 2.5e6);
+            seen.push_back(v.getDevice());
+        }
+        unsetenv("SDRGPU_PLACEMENT");
+        for (int k = 0; k < 2 * ndev; k++) CHECK(seen[k] == (seen[0] + k) % ndev,
+                                                 "spread placement: VFO %d on %d", k, seen[k]);
+        dsp::stream<dsp::complex_t> in;
+        dsp::channel::RxVFO a(&in, 61.44e6, 240000, 200000, 2.5e6), b(&in, 61.44e6, 240000, 200000, 2.5e6);
+        a.setDevice(ndev - 1);
+        std::vector<dsp::complex_t> ya(blk / 256 + 8), yb(blk / 256 + 8);
+        const int ma = a.process(blk, x.data(), ya.data()), mb = b.process(blk, x.data(), yb.data());
+        CHECK(ma == mb && ma > 0, "moved VFO output count %d vs %d", ma, mb);
+        float d = 0.f;
+        for (int i = 0; i < ma && i < mb; i++) d = std::fmax(d, std::fabs(ya[i].re - yb[i].re) + std::fabs(ya[i].im - yb[i].im));
+        CHECK(d <= 1e-5f, "moved VFO output differs by %g", d);
+        std::printf("placement: %d device(s), spread ->", ndev);
+        for (int v : seen) std::printf(" %d", v);
+        std::printf("\n");
+    }
+
     std::printf(failures ? "FAILED (%d)\n" : "ALL OK\n", failures);
     return failures ? 1 : 0;
 }

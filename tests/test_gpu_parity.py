@@ -641,3 +641,32 @@ def _fused_vs_separate(frames_list, pre, rng):
 @pytest.mark.parametrize("frames_list,pre", [([8], 0), ([3, 5], 1000), ([1, 2], 307200), ([257], 77)])
 def test_spectrum_vfo_fused(frames_list, pre, rng):
     _fused_vs_separate(frames_list, pre, rng)
+
+
+# ------------------------------------------------- waterfall zoom fused into the spectrum
+@pytest.mark.parametrize("frames,chunk_mb,zsize", [(3, None, 2048), (9, 1, 2048), (4, None, 1800), (5, 1, 4096)])
+def test_spectrum_zoom_rows(frames, chunk_mb, zsize, rng, monkeypatch):
+    """sdrgpu_fft_execute_zoom_dev: the dB rows are those of execute_dev, and every zoom row equals
+    fft_scaler(0, bw, bw, N, zoomSize).doZoom of its dB row (oracle restatement of
+    gui/widgets/fft_scaler.h:27-64) bit for bit -- fused in the last pass at 2048 (single launch and
+    merged chunk launches), as a separate kernel for other widths."""
+    import torch
+    if chunk_mb:
+        monkeypatch.setenv("SDRGPU_TUNING", "1")
+        monkeypatch.setenv("SDRGPU_FFT_CHUNK_MB", str(chunk_mb))   # 2 frames per chunk -> merged launches
+    N = 65536
+    x = iq(rng, N * frames)
+    d_x = torch.from_numpy(x.view(np.float32)).cuda()
+    f = dsp.FFTSpectrum(N, N, 6)
+    rows = torch.empty(frames * N, device="cuda")
+    ref = torch.empty(frames * N, device="cuda")
+    z = torch.empty(frames * zsize, device="cuda")
+    assert f.execute_zoom_dev(d_x.data_ptr(), N, frames, rows.data_ptr(), z.data_ptr(), zsize) == frames
+    dsp.FFTSpectrum(N, N, 6).execute_dev(d_x.data_ptr(), N, frames, ref.data_ptr())
+    torch.cuda.synchronize()
+    r = rows.cpu().numpy().reshape(frames, N)
+    d = np.abs(r - ref.cpu().numpy().reshape(frames, N))
+    assert d.max() <= 0.05 and np.all(d[r >= r.max(axis=1, keepdims=True) - 60] <= 1e-3)
+    zr = z.cpu().numpy().reshape(frames, zsize)
+    for j in range(frames):
+        np.testing.assert_array_equal(zr[j], oracle.zoom(r[j], 0.0, 1.0, 1.0, zsize))
