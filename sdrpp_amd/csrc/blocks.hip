@@ -77,6 +77,8 @@ struct FirArgs {
     const float2* nstep;  // XL: e^{i w u NT}, u < NCO_PF, for this launch's NT
     float invDev;
     int gzs;            // MFMA phase-split: gz entries per phase
+    void* histNext;     // non-null: the launch has one extra, last workgroup that writes the next
+                        // call's history (the last H samples of hist | in, translated) there
 };
 
 // FIR tile kernel: one tile of NT*K outputs per workgroup.
@@ -105,8 +107,32 @@ __device__ __forceinline__ DT fir_fetch(const FirArgs& a, long long b) {
     return x;
 }
 
+// The history carry of FIR::process (fir.h:80: memmove of the last ntaps - 1 inputs) as the
+// launch's extra workgroup, so a call needs no separate history kernel: next[k] = [hist | in]
+// [count + k], k < H (the xlator applied to `in` samples, as fir_fetch does).
+template <typename DT, bool XL>
+__device__ __forceinline__ bool fir_hist_block(const FirArgs& a) {
+    if (a.histNext == nullptr || blockIdx.x != gridDim.x - 1) return false;
+    const DT* hist = reinterpret_cast<const DT*>(a.hist);
+    const DT* in = reinterpret_cast<const DT*>(a.in);
+    DT* next = reinterpret_cast<DT*>(a.histNext);
+    for (int k = threadIdx.x; k < a.H; k += blockDim.x) {
+        const long long b = (long long)a.count + k;
+        DT v;
+        if (b < a.H) {
+            v = hist[b];
+        } else {
+            v = in[b - a.H];
+            if constexpr (XL) v = cmulf(v, nco_tab(a.phi, a.plo, b - a.H));
+        }
+        next[k] = v;
+    }
+    return true;
+}
+
 template <typename DT, typename TT, int K, bool XL, bool QUAD, bool STEREO, bool TL>
 __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
+    if (fir_hist_block<DT, XL>(a)) return;
     constexpr int PF = sizeof(DT) == 8 ? 36 : 40;   // load slots per thread issued together
     const int NT = blockDim.x;       // 64, 128 or 256 (host picks the largest tile that fits LDS)
     const int TM = NT * K;
@@ -265,6 +291,7 @@ constexpr int mf_rows(int nw) { return 256 * nw + 4 * MF_KS; }   // span rows pe
 
 template <int NW, bool XL, bool QUAD>   // NW waves per workgroup, 256 outputs each
 __global__ __launch_bounds__(64 * NW) void fir_mfma_kernel(FirArgs a) {
+    if (fir_hist_block<float2, XL>(a)) return;
     constexpr int NT = 64 * NW, MF_TM = 256 * NW, MF_ROWS = mf_rows(NW);
     constexpr int PF = (MF_ROWS * 8 + NT - 1) / NT;    // load slots per thread for D <= 8
     constexpr int QOFF = QUAD ? 1 : 0;
@@ -371,6 +398,7 @@ __global__ __launch_bounds__(64 * NW) void fir_mfma_kernel(FirArgs a) {
 // LDS for D up to 32 (75 KB at D = 32, 2 workgroups per CU) and for D = 8 let 7 share a CU.
 template <bool XL, bool QUAD>
 __global__ __launch_bounds__(256) void fir_mfma_ps_kernel(FirArgs a) {
+    if (fir_hist_block<float2, XL>(a)) return;
     constexpr int NT = 256, TM = 256, PF = 36, QOFF = QUAD ? 1 : 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float2* X = reinterpret_cast<float2*>(smem);
@@ -474,13 +502,18 @@ __global__ __launch_bounds__(256) void fir_mfma_ps_kernel(FirArgs a) {
 // SIMD) was no faster. D = 8 (C3) measured equal to fir_mfma_kernel (0.84 vs 0.85 ms), so it
 // runs only on request (SDRGPU_FIR_ROWS=2).
 constexpr int ROWS_STEP = 512;  // e^{i w D u} table length (>= RS + QP - 1)
+constexpr int kRowsMinOutputs = 1 << 19;   // D = 32: 128-output segments from this many outputs per call
 template <int D> constexpr int rows_rs() { return D == 32 ? 128 : 256; }
-template <int D, int QP, bool XL, bool QUAD>
+template <int D, int QP, bool XL, bool QUAD, int RS = rows_rs<D>()>
 __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
-    constexpr int RS = rows_rs<D>(), NG = 64 / D, QOFF = QUAD ? 1 : 0;
+    if (fir_hist_block<float2, XL>(a)) return;
+    constexpr int NG = 64 / D, QOFF = QUAD ? 1 : 0;
     // rows per load batch: D = 32 keeps 64 rows (32 KB per wave) in flight at 2 waves per SIMD,
-    // 0.6% faster than 32 rows at 3 (the kernel waits on its row loads); QP = 32 fits 16
-    constexpr int BT = QP > 16 ? 16 : (D == 32 ? 64 : 32);
+    // 0.6% faster than 32 rows at 3 (the kernel waits on its row loads); QP = 32 fits 16; short
+    // segments (small calls) take one batch of RS rows
+    constexpr int BT0 = QP > 16 ? 16 : (D == 32 ? 64 : 32);
+    constexpr int BT = BT0 < RS ? BT0 : RS;
+    static_assert(RS % BT == 0 && BT % D == 0, "rows kernel: segment = whole batches of D rows");
     const int lane = threadIdx.x & 63, p = lane & (D - 1), g = lane / D;
     const long long seg = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * NG + g;
     const long long mseg = seg * (RS - QOFF) - QOFF;   // output of local index 0
@@ -607,6 +640,7 @@ __global__ void fir_hist_kernel(const DT* __restrict__ hist, const DT* __restric
     }
     next[k] = v;
 }
+
 
 // --------------------------------------------------------------- xlator
 __global__ void xlator_kernel(const float2* __restrict__ in, float2* __restrict__ out, long long n,
@@ -885,20 +919,31 @@ struct FirBlock : Block {
         }
         return SDRGPU_OK;
     }
+    void* histNextArg = nullptr;   // the running call's history destination (FirArgs::histNext)
     bool mf = false;        // fir_mfma_kernel selected for the current taps / decimation
     bool mfps = false;      // fir_mfma_ps_kernel selected
     bool rowsk = false;     // fir_rows_kernel selected
     int useRows = 1;        // SDRGPU_FIR_ROWS (tuning): 0 off, 1 auto (D = 32), 2 also D = 8
-    template <int D, int QP, bool QD>
-    int launch_rows(FirArgs& a, hipStream_t s) {
-        constexpr int RS = rows_rs<D>();
+    template <int D, int QP, bool QD, int RS = rows_rs<D>()>
+    int launch_rows_rs(FirArgs& a, hipStream_t s) {
         const int q = QD ? 1 : 0;
         const long long segs = ((long long)a.M + q + (RS - q) - 1) / (RS - q);
         const int blocks = (int)((segs + 4 * (64 / D) - 1) / (4 * (64 / D)));   // 4 waves x 64/D groups
-        if (xl) hipLaunchKernelGGL((fir_rows_kernel<D, QP, true, QD>), dim3(blocks), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((fir_rows_kernel<D, QP, false, QD>), dim3(blocks), dim3(256), 0, s, a);
+        const int g = blocks + (a.histNext ? 1 : 0);
+        if (xl) hipLaunchKernelGGL((fir_rows_kernel<D, QP, true, QD, RS>), dim3(g), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((fir_rows_kernel<D, QP, false, QD, RS>), dim3(g), dim3(256), 0, s, a);
         SDRGPU_HIP(hipGetLastError());
         return SDRGPU_OK;
+    }
+    // D = 32: 128-output segments for big calls; a small call (a reference-size block: 9,600
+    // stage-1 outputs -> 75 segments, 10 workgroups, 62 us) takes 32-output segments instead
+    // (300 segments, one row batch each)
+    template <int D, int QP, bool QD>
+    int launch_rows(FirArgs& a, hipStream_t s) {
+        if constexpr (D == 32 && !QD) {
+            if (a.M < kRowsMinOutputs) return launch_rows_rs<D, QP, QD, 32>(a, s);
+        }
+        return launch_rows_rs<D, QP, QD>(a, s);
     }
     // taps per phase of the rows kernel: D = 32 exact (2..8), D = 8 padded to 16, 24 or 32
     static int rows_qp(int D, int Qr) {
@@ -908,6 +953,7 @@ struct FirBlock : Block {
     }
     int run_rows(const void* in, int count, void* out, int M, hipStream_t s) {
         FirArgs a{};
+        a.histNext = histNextArg;
         a.hist = hist[cur].p; a.in = in; a.taps = taps.p; a.out = out;
         a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
         a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>();
@@ -941,12 +987,13 @@ struct FirBlock : Block {
     int launch_mfma_ps(FirArgs& a, int tiles, size_t lds, hipStream_t s) {
         auto k = fir_mfma_ps_kernel<XL, QD>;
         SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(k, dim3(tiles), dim3(256), lds, s, a);
+        hipLaunchKernelGGL(k, dim3(tiles + (a.histNext ? 1 : 0)), dim3(256), lds, s, a);
         SDRGPU_HIP(hipGetLastError());
         return SDRGPU_OK;
     }
     int run_mfma_ps(const void* in, int count, void* out, int M, hipStream_t s) {
         FirArgs a{};
+        a.histNext = histNextArg;
         a.hist = hist[cur].p; a.in = in; a.taps = gzTaps.p; a.out = out;
         a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
         a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>();
@@ -975,7 +1022,7 @@ struct FirBlock : Block {
     int launch_mfma(FirArgs& a, int tiles, size_t lds, hipStream_t s) {
         auto k = fir_mfma_kernel<NW, XL, QD>;
         SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(k, dim3(tiles), dim3(64 * NW), lds, s, a);
+        hipLaunchKernelGGL(k, dim3(tiles + (a.histNext ? 1 : 0)), dim3(64 * NW), lds, s, a);
         SDRGPU_HIP(hipGetLastError());
         return SDRGPU_OK;
     }
@@ -984,6 +1031,7 @@ struct FirBlock : Block {
     int run_mfma_nw(const void* in, int count, void* out, int M, hipStream_t s) {
         constexpr int MF_TM = 256 * NW, MF_ROWS = mf_rows(NW);
         FirArgs a{};
+        a.histNext = histNextArg;
         a.hist = hist[cur].p; a.in = in; a.taps = gzTaps.p; a.out = out;
         a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
         a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>();
@@ -1040,7 +1088,7 @@ struct FirBlock : Block {
         // one tile per workgroup: a co-resident persistent grid with a register prefetch of the
         // next tile was measured 1.5x SLOWER on C3 (the hardware's own workgroup turnover
         // staggers the load/compute phases of the workgroups sharing a CU better)
-        hipLaunchKernelGGL(k, dim3(tiles), dim3(NT), lds, s, a);
+        hipLaunchKernelGGL(k, dim3(tiles + (a.histNext ? 1 : 0)), dim3(NT), lds, s, a);
         SDRGPU_HIP(hipGetLastError());
         return SDRGPU_OK;
     }
@@ -1057,6 +1105,8 @@ struct FirBlock : Block {
         const int M = out_count(count);
         const int H = ntaps - 1;
         if (xl && count > 0) SDRGPU_CHECK(nco.prepare(count, s));
+        // with outputs to compute, the FIR launch itself carries the history (fir_hist_block)
+        histNextArg = (M > 0 && H > 0) ? hist[cur ^ 1].p : nullptr;
         if (M > 0 && rowsk) {
             SDRGPU_CHECK(run_rows(in, count, out, M, s));
         } else if (M > 0 && mf) {
@@ -1096,6 +1146,7 @@ struct FirBlock : Block {
             const int TMS = quad ? TM - 1 : TM;
             const int tiles = (M + TMS - 1) / TMS;
             FirArgs a{};
+            a.histNext = histNextArg;
             a.hist = hist[cur].p; a.in = in; a.taps = taps.p; a.out = out;
             a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
             a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>();
@@ -1122,7 +1173,7 @@ struct FirBlock : Block {
         if (quad && M == 0) {
             SDRGPU_HIP(hipMemcpyAsync(din[cur ^ 1].p, din[cur].p, sizeof(float2), hipMemcpyDeviceToDevice, s));
         }
-        if (H > 0) {
+        if (H > 0 && M == 0) {
             const int nb = (H + 255) / 256;
             if (in_dtype == SDRGPU_F32) {
                 hipLaunchKernelGGL((fir_hist_kernel<float, false>), dim3(nb), dim3(256), 0, s, hist[cur].as<float>(),

@@ -200,6 +200,38 @@ extern "C" int sdrgpu_frontend_set_vfo_offset(sdrgpu_frontend* f, int id, double
     return sdrgpu_rxvfo_set_offset(it->second.vfo, offset);
 }
 
+// up to four device-to-device copies of complex samples in one launch (replaces as many
+// hipMemcpyAsync calls, each of which is a copy-kernel launch of its own)
+struct CopySegArgs {
+    float2* dst[4];
+    const float2* src[4];
+    int n[4];
+    int count;
+};
+__global__ void copy_segs_kernel(CopySegArgs a) {
+    const int seg = blockIdx.y;
+    if (seg >= a.count) return;
+    const int n = a.n[seg];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) a.dst[seg][i] = a.src[seg][i];
+}
+struct CopySegs {
+    CopySegArgs a{};
+    int maxN = 0;
+    void add(float2* d, const float2* s, int n) {
+        if (n <= 0) return;
+        a.dst[a.count] = d; a.src[a.count] = s; a.n[a.count] = n;
+        a.count++;
+        maxN = std::max(maxN, n);
+    }
+    int launch(hipStream_t s) {
+        if (!a.count) return SDRGPU_OK;
+        const int bx = std::min((maxN + 255) / 256, 256);
+        hipLaunchKernelGGL(copy_segs_kernel, dim3(bx, a.count), dim3(256), 0, s, a);
+        SDRGPU_HIP(hipGetLastError());
+        return SDRGPU_OK;
+    }
+};
+
 // Core of a push: the preprocessed block `x` (m samples, device) -> VFOs + spectrum frames.
 static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s) {
     for (auto& [id, v] : f->vfos) {
@@ -217,12 +249,36 @@ static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s)
     SDRGPU_CHECK(f->spectra.ensure(sizeof(float) * (size_t)std::max(nf, 1) * f->fftSize));
     float* spec = f->spectra.as<float>();
     int done = 0;
+    // the stitched straddling frame and the new tail are built by one copy launch (up to four
+    // device segments) before the spectrum: both read only the old tail and this block
+    CopySegs cs;
     if (nf > 0 && f->nextFrame < T) {
         // the one frame straddling the previous push: [tail (tailLen) || x[0 : nz - tailLen])
         const int head = (int)(T - f->nextFrame);   // == tailLen
         SDRGPU_CHECK(f->stitch.ensure(sizeof(float2) * f->nz));
-        SDRGPU_HIP(hipMemcpyAsync(f->stitch.p, f->tail[f->curTail].p, sizeof(float2) * head, hipMemcpyDeviceToDevice, s));
-        SDRGPU_HIP(hipMemcpyAsync(f->stitch.as<float2>() + head, x, sizeof(float2) * (f->nz - head), hipMemcpyDeviceToDevice, s));
+        cs.add(f->stitch.as<float2>(), f->tail[f->curTail].as<float2>(), head);
+        cs.add(f->stitch.as<float2>() + head, x, f->nz - head);
+    }
+    const long long nextAfter = f->nextFrame + (long long)nf * st;
+    // new tail: samples [nextAfter, T + m) (fewer than nz), from the old tail and/or this block
+    const long long end = T + m;
+    int newLen = 0, nb = f->curTail;
+    if (nextAfter < end) {
+        newLen = (int)(end - nextAfter);
+        nb = f->curTail ^ 1;
+        SDRGPU_CHECK(f->tail[0].ensure(sizeof(float2) * f->nz));
+        SDRGPU_CHECK(f->tail[1].ensure(sizeof(float2) * f->nz));
+        float2* dst = f->tail[nb].as<float2>();
+        int fromOld = 0;
+        if (nextAfter < T) {   // keep part of the old tail (no frame completed)
+            fromOld = (int)(T - nextAfter);
+            cs.add(dst, f->tail[f->curTail].as<float2>() + (f->tailLen - fromOld), fromOld);
+        }
+        const long long fromBlock = newLen - fromOld;
+        if (fromBlock > 0) cs.add(dst + fromOld, x + (m - fromBlock), (int)fromBlock);
+    }
+    SDRGPU_CHECK(cs.launch(s));
+    if (nf > 0 && f->nextFrame < T) {
         SDRGPU_CHECK(sdrgpu_fft_execute_dev(f->fft, f->stitch.p, f->nz, 1, spec, s));
         done = 1;
     }
@@ -231,28 +287,8 @@ static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s)
         SDRGPU_CHECK(sdrgpu_fft_execute_dev(f->fft, x + first, st, nf - done, spec + (size_t)done * f->fftSize, s));
     }
     f->nSpec = nf;
-    f->nextFrame += (long long)nf * st;
-    // new tail: samples [nextFrame, T + m) (fewer than nz), from the old tail and/or this block
-    const long long end = T + m;
-    int newLen = 0;
-    if (f->nextFrame < end) {
-        newLen = (int)(end - f->nextFrame);
-        const int nb = (int)(f->curTail ^ 1);
-        SDRGPU_CHECK(f->tail[0].ensure(sizeof(float2) * f->nz));
-        SDRGPU_CHECK(f->tail[1].ensure(sizeof(float2) * f->nz));
-        float2* dst = f->tail[nb].as<float2>();
-        int fromOld = 0;
-        if (f->nextFrame < T) {   // keep part of the old tail (no frame completed)
-            fromOld = (int)(T - f->nextFrame);
-            const int oldOff = f->tailLen - fromOld;
-            SDRGPU_HIP(hipMemcpyAsync(dst, f->tail[f->curTail].as<float2>() + oldOff, sizeof(float2) * fromOld,
-                                      hipMemcpyDeviceToDevice, s));
-        }
-        const long long fromBlock = newLen - fromOld;
-        if (fromBlock > 0)
-            SDRGPU_HIP(hipMemcpyAsync(dst + fromOld, x + (m - fromBlock), sizeof(float2) * fromBlock, hipMemcpyDeviceToDevice, s));
-        f->curTail = nb;
-    }
+    f->nextFrame = nextAfter;
+    f->curTail = nb;
     f->tailLen = newLen;
     f->total = end;
     return nf;

@@ -467,6 +467,12 @@ class IQFrontEnd:
     def push_dev(self, ptr, count, kind=-1, stream=None):
         return check(lib.sdrgpu_frontend_push_dev(self._h, _vp(ptr), int(count), int(kind), _vp(stream or 0)))
 
+    def vfo_dev(self, vid):
+        """(device pointer, count) of the VFO's output for the last push."""
+        ptr, n = ctypes.c_void_p(), ctypes.c_int()
+        check(lib.sdrgpu_frontend_vfo_dev(self._h, int(vid), ctypes.byref(ptr), ctypes.byref(n)))
+        return ptr.value, n.value
+
     def vfo_output(self, vid):
         n = ctypes.c_int()
         check(lib.sdrgpu_frontend_vfo_dev(self._h, int(vid), None, ctypes.byref(n)))
