@@ -208,6 +208,8 @@ int sdrgpu_frontend_spectra_dev(sdrgpu_frontend* f, const float** rows, int* nro
 int sdrgpu_frontend_read_spectra(sdrgpu_frontend* f, float* out, int maxRows);
 int sdrgpu_frontend_vfo_dev(sdrgpu_frontend* f, int id, const void** out, int* n);
 int sdrgpu_frontend_read_vfo(sdrgpu_frontend* f, int id, void* out, int max);
+/* host copy of the last push's preprocessed IQ (what bound IQ streams receive, iq_frontend.cpp:114-120) */
+int sdrgpu_frontend_read_iq(sdrgpu_frontend* f, void* out, int max);
 
 /* ------------------------------------------ spectra gather (multi-GPU) ---- */
 /* Independent IQ streams run one per GPU; the only collective is a gather of their

@@ -46,6 +46,8 @@ struct sdrgpu_frontend {
     bool dcBlocking = false, invertIQ = false;
     hipStream_t s = nullptr;
     StreamOrder order;        // tails, stitch and VFO state are per front end: serialise across streams
+    const float2* lastIQ = nullptr;   // the last push's preprocessed block (device) and its length
+    int lastIQn = 0;
     sdrgpu_block* decimB = nullptr;
     sdrgpu_block* dcb = nullptr;
     sdrgpu_fft* fft = nullptr;
@@ -340,6 +342,8 @@ extern "C" int sdrgpu_frontend_push_dev(sdrgpu_frontend* f, const void* in, int 
     const float2* p = nullptr;
     const int m = fe_preproc(f, x, count, s, &p);
     if (m < 0) return m;
+    f->lastIQ = p;
+    f->lastIQn = m;
     return fe_consume(f, p, m, s);
 }
 
@@ -387,6 +391,18 @@ extern "C" int sdrgpu_frontend_vfo_dev(sdrgpu_frontend* f, int id, const void** 
     if (n) *n = it->second.n;
     return it->second.n;
 }
+// the last push's preprocessed IQ (decimated / DC-blocked / conjugated as configured): what the
+// reference's Splitter hands to bound IQ streams (iq_frontend.cpp:114-120, routing/splitter.h:46-60)
+extern "C" int sdrgpu_frontend_read_iq(sdrgpu_frontend* f, void* out, int max) {
+    NEED_FE(f);
+    const int n = std::min(max, f->lastIQn);
+    if (n <= 0 || !f->lastIQ) return 0;
+    SDRGPU_SET_DEVICE(f->device);
+    SDRGPU_HIP(hipStreamSynchronize(f->s));
+    SDRGPU_HIP(hipMemcpy(out, f->lastIQ, sizeof(float2) * (size_t)n, hipMemcpyDeviceToHost));
+    return n;
+}
+
 extern "C" int sdrgpu_frontend_read_vfo(sdrgpu_frontend* f, int id, void* out, int max) {
     NEED_FE(f);
     auto it = f->vfos.find(id);

@@ -2,6 +2,7 @@
 // xlator(-offset) fused into the first full-rate decimation stage, then the remaining
 // plan stages / polyphase resampler and the bw/2 low-pass (when bw != outSr).
 #pragma once
+#include <mutex>
 #include "../processor.h"
 #include "../sdrgpu_handle.h"
 
@@ -47,12 +48,34 @@ public:
     void setOffset(double offset) {
         std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx);
         _offset = offset;
+        if (_fe) {
+            std::lock_guard<std::mutex> fl(*_feMtx);
+            gpu::ok(sdrgpu_frontend_set_vfo_offset(_fe, _feId, offset), "frontend_set_vfo_offset");
+            return;
+        }
         gpu::ok(sdrgpu_rxvfo_set_offset(_h.h, offset), "rxvfo_set_offset");
     }
+    // ---- attached to a device front end (the IQFrontEnd drop-in, signal_path/iq_frontend.h):
+    // the front end runs this VFO on the block it already holds on the device and writes `out`
+    // (this block's own worker does nothing); the setters re-plan it there, under the front
+    // end's lock. `in` is an idle placeholder input (the block API needs one).
+    void attach(stream<complex_t>* in, sdrgpu_frontend* fe, int id, std::mutex* feMtx, double inSamplerate,
+                double outSamplerate, double bandwidth, double offset) {
+        _fe = fe;
+        _feId = id;
+        _feMtx = feMtx;
+        _inSamplerate = inSamplerate;
+        _outSamplerate = outSamplerate;
+        _bandwidth = bandwidth;
+        _offset = offset;
+        base_type::init(in);
+    }
+    int frontEndId() const { return _feId; }
     void reset() {
         std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx);
         base_type::tempStop();
-        gpu::ok(sdrgpu_block_reset(_h.h), "rxvfo_reset");
+        if (_fe) rebuild();
+        else gpu::ok(sdrgpu_block_reset(_h.h), "rxvfo_reset");
         base_type::tempStart();
     }
     // GPU placement (sdrgpu_handle.h): this VFO's device; setDevice moves it (state restarts)
@@ -66,6 +89,7 @@ public:
     }
     inline int process(int count, const complex_t* in, complex_t* out) { return _h.process(in, count, out, "rxvfo"); }
     int run() override {
+        if (_fe) return -1;   // attached: the front end's worker produces `out`
         int count = base_type::_in->read();
         if (count < 0) return -1;
         int n = process(count, base_type::_in->readBuf, base_type::out.writeBuf);
@@ -77,11 +101,22 @@ public:
 
 protected:
     void rebuild() {
+        if (_fe) {   // attached: the front end's VFO is re-planned (its filter state restarts)
+            std::lock_guard<std::mutex> fl(*_feMtx);
+            gpu::ok(sdrgpu_frontend_remove_vfo(_fe, _feId), "frontend_remove_vfo");
+            int id = -1;
+            gpu::ok(sdrgpu_frontend_add_vfo(_fe, &id, _outSamplerate, _bandwidth, _offset), "frontend_add_vfo");
+            _feId = id;
+            return;
+        }
         sdrgpu_block* h = nullptr;
         gpu::ok(sdrgpu_rxvfo_create(&h, _h.bind(gpu::stream_device()), _inSamplerate, _outSamplerate, _bandwidth, _offset), "rxvfo_create");
         _h.reset(h);
     }
     double _inSamplerate = 0, _outSamplerate = 0, _bandwidth = 0, _offset = 0;
     gpu::Handle _h;
+    sdrgpu_frontend* _fe = nullptr;   // attached mode
+    int _feId = -1;
+    std::mutex* _feMtx = nullptr;
 };
 }  // namespace dsp::channel
