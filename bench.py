@@ -295,7 +295,7 @@ def run_config(config, a, shard, dev, stream):
     return B, elapsed, kern_ms, wl
 
 
-def per_call_c5(dev, stream, calls=300, block=307200):
+def per_call_c5(dev, stream, calls=300, block=307200, single_only=False):
     """C5 at the reference's block size: file/hardware sources push fs / 200 samples per block
     (source_modules/file_source/src/main.cpp:296,440: 307,200 at 61.44 MS/s). Each call is one
     block through the device front end (sdrgpu_frontend_push_dev: spectrum frames back to back,
@@ -324,6 +324,9 @@ def per_call_c5(dev, stream, calls=300, block=307200):
         one(k)
     torch.cuda.synchronize()
     dev_us = (time.perf_counter() - t0) / calls * 1e6
+    if single_only:
+        fe.close()
+        return {"block": block, "us_per_call_device": round(dev_us, 1), "MSps_device": round(block / dev_us, 1)}
     # K independent block streams on K HIP streams (one SDR each): each call's kernels fill only a
     # few CUs, so concurrent streams overlap on the device
     K = 16

@@ -29,15 +29,18 @@ constexpr int NCO_LO = 1 << NCO_LO_BITS;
 __device__ __forceinline__ float2 nco_tab(const float2* __restrict__ phi, const float2* __restrict__ plo, long long i) {
     return cmulf(phi[i >> NCO_LO_BITS], plo[i & (NCO_LO - 1)]);
 }
-__global__ void nco_hi_kernel(float2* __restrict__ phi, int n, double theta0, double w) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
+__device__ __forceinline__ float2 nco_phi(double theta0, double w, long long j) {
     const double TWO_PI = 6.283185307179586476925286766559;
     double a = fma(w * (double)NCO_LO, (double)j, theta0);
     a = fma(-rint(a / TWO_PI), TWO_PI, a);
     double sn, cs;
     sincos(a, &sn, &cs);
-    phi[j] = make_float2((float)cs, (float)sn);
+    return make_float2((float)cs, (float)sn);
+}
+__global__ void nco_hi_kernel(float2* __restrict__ phi, int n, double theta0, double w) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    phi[j] = nco_phi(theta0, w, j);
 }
 
 template <typename T> __device__ __forceinline__ T zero_of();
@@ -67,8 +70,9 @@ struct FirArgs {
     void* out;
     const float2* din;  // QUAD: y[-1] (carried)
     float2* dinNext;    // QUAD: y[M-1]
-    const float2* phi;  // XL: per-call coarse phasors
+    const float2* phi;  // XL: per-call coarse phasors (only the separate history kernel reads them)
     const float2* plo;  // XL: fine phasors
+    double ncoTheta0, ncoW;   // XL: the coarse phasor of index j is nco_phi(ncoTheta0, ncoW, j)
     int ntaps, H, count, D, Q, offset0, M, TMS, RSK, RSP;
     int dshift;         // log2(D) when D is a power of two, else -1
     int ntiles;         // tiles of TMS outputs (persistent grid walks them)
@@ -80,6 +84,21 @@ struct FirArgs {
     void* histNext;     // non-null: the launch has one extra, last workgroup that writes the next
                         // call's history (the last H samples of hist | in, translated) there
 };
+// XL phasor of input index i inside a FIR kernel: the coarse factor computed in place (the same
+// fp64 expression as nco_hi_kernel's table, so the same bits) instead of read from a per-call
+// table, which would need a launch of its own before every call. The row kernel (VFO stage 1:
+// the C5 chain's only translating FIR) does this; the MFMA / LDS tile kernels keep the table:
+// there every wave forms its own phasors and the fp64 sincos serialises with the matrix work
+// (C3: +1.3% kernel time measured).
+__device__ __forceinline__ float2 nco_inline(const FirArgs& a, long long i) {
+    return cmulf(nco_phi(a.ncoTheta0, a.ncoW, i >> NCO_LO_BITS), a.plo[i & (NCO_LO - 1)]);
+}
+template <bool TAB = true>   // TAB: read the per-call table; else form the coarse phasor in place
+__device__ __forceinline__ float2 nco_at(const FirArgs& a, long long i) {
+    if constexpr (TAB) return nco_tab(a.phi, a.plo, i);
+    else return nco_inline(a, i);
+}
+
 
 // FIR tile kernel: one tile of NT*K outputs per workgroup.
 //  1. The tile's input span (rows * D elements) is loaded with all PF loads per thread in
@@ -92,25 +111,29 @@ struct FirArgs {
 //  2. Each thread computes K consecutive outputs with a register window sliding one row per
 //     tap; taps are staged once per workgroup in LDS (wave-uniform broadcast reads).
 // History / tail samples come from [hist (H) || in (count)]; hist is stored translated.
-template <typename DT, bool XL>
+template <typename DT, bool XL, bool TAB = true>
 __device__ __forceinline__ DT fir_fetch(const FirArgs& a, long long b) {
     const DT* hist = reinterpret_cast<const DT*>(a.hist);
     const DT* in = reinterpret_cast<const DT*>(a.in);
-    DT x = zero_of<DT>();
-    if (b >= 0) {
-        if (b < a.H) x = hist[b];
-        else if (b - a.H < a.count) {
-            x = in[b - a.H];
-            if constexpr (XL) x = cmulf(x, nco_tab(a.phi, a.plo, b - a.H));
-        }
+    // branch-free: one load from an address that exists (clamped), then a select, so the callers'
+    // unrolled row loops keep all their edge fetches in flight instead of issuing one
+    // branch-guarded load (and its NCO table loads) at a time. An edge segment of the VFO's
+    // stage-1 FIR at the reference block size took 19 us that way: the whole launch's time.
+    const long long i = b - a.H;
+    const bool inH = b >= 0 && b < a.H, inI = i >= 0 && i < a.count;
+    const DT* src = inH ? hist + b : (inI ? in + i : (a.count > 0 ? in : hist));
+    DT x = *src;
+    if constexpr (XL) {
+        const float2 r = nco_at<TAB>(a, inI ? i : 0);
+        if (inI) x = cmulf(x, r);
     }
-    return x;
+    return (inH || inI) ? x : zero_of<DT>();
 }
 
 // The history carry of FIR::process (fir.h:80: memmove of the last ntaps - 1 inputs) as the
 // launch's extra workgroup, so a call needs no separate history kernel: next[k] = [hist | in]
 // [count + k], k < H (the xlator applied to `in` samples, as fir_fetch does).
-template <typename DT, bool XL>
+template <typename DT, bool XL, bool TAB = true>
 __device__ __forceinline__ bool fir_hist_block(const FirArgs& a) {
     if (a.histNext == nullptr || blockIdx.x != gridDim.x - 1) return false;
     const DT* hist = reinterpret_cast<const DT*>(a.hist);
@@ -123,7 +146,7 @@ __device__ __forceinline__ bool fir_hist_block(const FirArgs& a) {
             v = hist[b];
         } else {
             v = in[b - a.H];
-            if constexpr (XL) v = cmulf(v, nco_tab(a.phi, a.plo, b - a.H));
+            if constexpr (XL) v = cmulf(v, nco_at<TAB>(a, b - a.H));
         }
         next[k] = v;
     }
@@ -178,7 +201,7 @@ __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
         }
         if constexpr (XL) {
             // phasor(i0 + tid + u NT) = nco(i0 + tid) * e^{i w u NT}
-            const float2 ph0 = nco_tab(a.phi, a.plo, b0 - a.H + tid);
+            const float2 ph0 = nco_at(a, b0 - a.H + tid);
             const float2* __restrict__ S = a.nstep;
 #pragma unroll
             for (int u = 0; u < PF; u++) pf[u] = cmulf(pf[u], cmulf(ph0, S[u]));
@@ -322,7 +345,7 @@ __global__ __launch_bounds__(64 * NW) void fir_mfma_kernel(FirArgs a) {
             if (sx < span) pf[u] = src[sx];
         }
         if constexpr (XL) {
-            const float2 ph0 = nco_tab(a.phi, a.plo, b0 - a.H + tid);
+            const float2 ph0 = nco_at(a, b0 - a.H + tid);
             const float2* __restrict__ S = a.nstep;
 #pragma unroll
             for (int u = 0; u < PF; u++) pf[u] = cmulf(pf[u], cmulf(ph0, S[u]));
@@ -428,7 +451,7 @@ __global__ __launch_bounds__(256) void fir_mfma_ps_kernel(FirArgs a) {
             if (sx < span) pf[u] = src[sx];
         }
         if constexpr (XL) {
-            const float2 ph0 = nco_tab(a.phi, a.plo, b0 - a.H + tid);
+            const float2 ph0 = nco_at(a, b0 - a.H + tid);
             const float2* __restrict__ S = a.nstep;
 #pragma unroll
             for (int u = 0; u < PF; u++) pf[u] = cmulf(pf[u], cmulf(ph0, S[u]));
@@ -506,7 +529,7 @@ constexpr int kRowsMinOutputs = 1 << 19;   // D = 32: 128-output segments from t
 template <int D> constexpr int rows_rs() { return D == 32 ? 128 : 256; }
 template <int D, int QP, bool XL, bool QUAD, int RS = rows_rs<D>()>
 __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
-    if (fir_hist_block<float2, XL>(a)) return;
+    if (fir_hist_block<float2, XL, false>(a)) return;
     constexpr int NG = 64 / D, QOFF = QUAD ? 1 : 0;
     // rows per load batch: D = 32 keeps 64 rows (32 KB per wave) in flight at 2 waves per SIMD,
     // 0.6% faster than 32 rows at 3 (the kernel waits on its row loads); QP = 32 fits 16; short
@@ -530,7 +553,7 @@ __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
     // the row-step table through the constant address space: scalar (SMEM) loads
     const __attribute__((address_space(4))) float* nstep = (const __attribute__((address_space(4))) float*)a.nstep;
     if constexpr (XL) {
-        if (interior) ph0 = nco_tab(a.phi, a.plo, b0 - a.H + p);
+        if (interior) ph0 = nco_inline(a, b0 - a.H + p);
     }
     float2* __restrict__ out2 = reinterpret_cast<float2*>(a.out);
     float* __restrict__ outf = reinterpret_cast<float*>(a.out);
@@ -540,7 +563,7 @@ __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
         constexpr bool F = decltype(fast)::value;
         auto row = [&](int r) -> float2 {   // raw row sample (the slow path applies the xlator itself)
             if constexpr (F) return src[D * r];
-            else return fir_fetch<float2, XL>(a, b0 + (long long)D * r + p);
+            else return fir_fetch<float2, XL, false>(a, b0 + (long long)D * r + p);
         };
         auto xlate = [&](float2 x, int r) -> float2 {   // fused xlator of the fast path: e^{i w D r}
             if constexpr (F && XL) x = cmulf(x, cmulf(ph0, make_float2(nstep[2 * r], nstep[2 * r + 1])));
@@ -920,6 +943,7 @@ struct FirBlock : Block {
         return SDRGPU_OK;
     }
     void* histNextArg = nullptr;   // the running call's history destination (FirArgs::histNext)
+    bool ncoTable = false;         // the running call's kernels read the per-call NCO table
     bool mf = false;        // fir_mfma_kernel selected for the current taps / decimation
     bool mfps = false;      // fir_mfma_ps_kernel selected
     bool rowsk = false;     // fir_rows_kernel selected
@@ -956,7 +980,7 @@ struct FirBlock : Block {
         a.histNext = histNextArg;
         a.hist = hist[cur].p; a.in = in; a.taps = taps.p; a.out = out;
         a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
-        a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>();
+        a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>(); a.ncoTheta0 = nco.phase.value(); a.ncoW = nco.w;
         a.ntaps = ntaps; a.H = ntaps - 1; a.count = count; a.D = D; a.Q = Q; a.offset0 = offset; a.M = M;
         a.invDev = invDev;
         a.nstep = xl ? nco.rstep_for(D) : nullptr;
@@ -996,7 +1020,7 @@ struct FirBlock : Block {
         a.histNext = histNextArg;
         a.hist = hist[cur].p; a.in = in; a.taps = gzTaps.p; a.out = out;
         a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
-        a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>();
+        a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>(); a.ncoTheta0 = nco.phase.value(); a.ncoW = nco.w;
         a.ntaps = ntaps; a.H = ntaps - 1; a.count = count; a.D = D; a.offset0 = offset; a.M = M;
         const int Qr = (ntaps + D - 1) / D;
         a.Q = (15 + Qr + 3) / 4;                        // k steps
@@ -1034,7 +1058,7 @@ struct FirBlock : Block {
         a.histNext = histNextArg;
         a.hist = hist[cur].p; a.in = in; a.taps = gzTaps.p; a.out = out;
         a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
-        a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>();
+        a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>(); a.ncoTheta0 = nco.phase.value(); a.ncoW = nco.w;
         a.ntaps = ntaps; a.H = ntaps - 1; a.count = count; a.D = D; a.offset0 = offset; a.M = M;
         a.TMS = quad ? MF_TM - 1 : MF_TM;
         a.RSP = MF_ROWS + MF_ROWS / 16 + 1;
@@ -1104,7 +1128,10 @@ struct FirBlock : Block {
         SDRGPU_SET_DEVICE(device);
         const int M = out_count(count);
         const int H = ntaps - 1;
-        if (xl && count > 0) SDRGPU_CHECK(nco.prepare(count, s));
+        // the row kernel forms its coarse phasors itself (nco_inline); the tile kernels and the
+        // separate history kernel of a call without outputs read the per-call table
+        ncoTable = xl && count > 0 && (M == 0 || !rowsk);
+        if (ncoTable) SDRGPU_CHECK(nco.prepare(count, s));
         // with outputs to compute, the FIR launch itself carries the history (fir_hist_block)
         histNextArg = (M > 0 && H > 0) ? hist[cur ^ 1].p : nullptr;
         if (M > 0 && rowsk) {
@@ -1149,7 +1176,7 @@ struct FirBlock : Block {
             a.histNext = histNextArg;
             a.hist = hist[cur].p; a.in = in; a.taps = taps.p; a.out = out;
             a.din = din[cur].as<float2>(); a.dinNext = din[cur ^ 1].as<float2>();
-            a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>();
+            a.phi = nco.phi.as<float2>(); a.plo = nco.plo.as<float2>(); a.ncoTheta0 = nco.phase.value(); a.ncoW = nco.w;
             a.ntaps = ntaps; a.H = H; a.count = count; a.D = D; a.Q = Q; a.offset0 = offset; a.M = M;
             a.TMS = TMS; a.RSK = RSK; a.RSP = RSP; a.invDev = invDev;
             a.dshift = (D & (D - 1)) ? -1 : __builtin_ctz((unsigned)D);

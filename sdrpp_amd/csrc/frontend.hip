@@ -12,7 +12,9 @@
 // genReshapeParams, iq_frontend.h:56-60): frame j covers samples [j*(nz+skip), j*(nz+skip)+nz)
 // of the preprocessed stream. Only the (at most one) frame straddling two pushes is
 // stitched, from a device tail buffer of < nz samples; every other frame is read in place,
-// so each sample crosses PCIe once and is read from HBM once per consumer.
+// so each sample crosses PCIe once and is read from HBM once per consumer (a push with a
+// straddling frame and at most 4 more copies those behind it, so one transform launch pair
+// covers the push).
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -205,9 +207,9 @@ extern "C" int sdrgpu_frontend_set_vfo_offset(sdrgpu_frontend* f, int id, double
 // up to four device-to-device copies of complex samples in one launch (replaces as many
 // hipMemcpyAsync calls, each of which is a copy-kernel launch of its own)
 struct CopySegArgs {
-    float2* dst[4];
-    const float2* src[4];
-    int n[4];
+    float2* dst[8];
+    const float2* src[8];
+    int n[8];
     int count;
 };
 __global__ void copy_segs_kernel(CopySegArgs a) {
@@ -254,12 +256,20 @@ static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s)
     // the stitched straddling frame and the new tail are built by one copy launch (up to four
     // device segments) before the spectrum: both read only the old tail and this block
     CopySegs cs;
-    if (nf > 0 && f->nextFrame < T) {
+    // with a straddling frame, up to kGatherFrames in-block frames are copied behind it in the
+    // same copy launch, so one transform launch pair covers the call (a reference-size block
+    // has 1-2 frames: one pass-A / pass-B pair instead of two, ~10 us per call)
+    constexpr int kGatherFrames = 4;
+    const bool straddle = nf > 0 && f->nextFrame < T;
+    const int gathered = (straddle && nf - 1 <= kGatherFrames) ? nf - 1 : 0;
+    if (straddle) {
         // the one frame straddling the previous push: [tail (tailLen) || x[0 : nz - tailLen])
         const int head = (int)(T - f->nextFrame);   // == tailLen
-        SDRGPU_CHECK(f->stitch.ensure(sizeof(float2) * f->nz));
+        SDRGPU_CHECK(f->stitch.ensure(sizeof(float2) * (size_t)f->nz * (1 + gathered)));
         cs.add(f->stitch.as<float2>(), f->tail[f->curTail].as<float2>(), head);
         cs.add(f->stitch.as<float2>() + head, x, f->nz - head);
+        for (int j = 1; j <= gathered; j++)
+            cs.add(f->stitch.as<float2>() + (size_t)j * f->nz, x + (f->nextFrame + j * st - T), f->nz);
     }
     const long long nextAfter = f->nextFrame + (long long)nf * st;
     // new tail: samples [nextAfter, T + m) (fewer than nz), from the old tail and/or this block
@@ -280,9 +290,9 @@ static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s)
         if (fromBlock > 0) cs.add(dst + fromOld, x + (m - fromBlock), (int)fromBlock);
     }
     SDRGPU_CHECK(cs.launch(s));
-    if (nf > 0 && f->nextFrame < T) {
-        SDRGPU_CHECK(sdrgpu_fft_execute_dev(f->fft, f->stitch.p, f->nz, 1, spec, s));
-        done = 1;
+    if (straddle) {
+        SDRGPU_CHECK(sdrgpu_fft_execute_dev(f->fft, f->stitch.p, f->nz, 1 + gathered, spec, s));
+        done = 1 + gathered;
     }
     if (nf > done) {   // frames entirely inside this block, read in place with the reshaper's stride
         const long long first = f->nextFrame + done * st - T;
