@@ -583,20 +583,35 @@ __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
             P[1] = make_float2(x.x * h[0], x.y * h[0]);
             return done;
         };
-        for (int r0 = 0; r0 < QP - 1; r0 += 8) {   // prologue: rows 0 .. QP - 2 close no output
-            float2 pro[8];
+        // one-batch segments (small calls) issue the prologue rows with the batch: one round
+        // of row loads per segment instead of two dependent ones
+        constexpr bool ONE = RS == BT;
+        if constexpr (!ONE) {
+            for (int r0 = 0; r0 < QP - 1; r0 += 8) {   // prologue: rows 0 .. QP - 2 close no output
+                float2 pro[8];
 #pragma unroll
-            for (int r = 0; r < 8; r++) pro[r] = (r0 + r < QP - 1) ? row(r0 + r) : make_float2(0.f, 0.f);
+                for (int r = 0; r < 8; r++) pro[r] = (r0 + r < QP - 1) ? row(r0 + r) : make_float2(0.f, 0.f);
 #pragma unroll
-            for (int r = 0; r < 8; r++)
-                if (r0 + r < QP - 1) (void)step(xlate(pro[r], r0 + r));
+                for (int r = 0; r < 8; r++)
+                    if (r0 + r < QP - 1) (void)step(xlate(pro[r], r0 + r));
+            }
         }
         float2 ylast = make_float2(0.f, 0.f);   // QUAD: the group's previous output
 #pragma unroll 1
         for (int bt = 0; bt < RS / BT; bt++) {
             float2 v[BT];
+            if constexpr (ONE) {
+                float2 pro[QP > 1 ? QP - 1 : 1];
 #pragma unroll
-            for (int i = 0; i < BT; i++) v[i] = row(QP - 1 + BT * bt + i);   // BT row loads in flight
+                for (int r = 0; r < QP - 1; r++) pro[r] = row(r);
+#pragma unroll
+                for (int i = 0; i < BT; i++) v[i] = row(QP - 1 + i);
+#pragma unroll
+                for (int r = 0; r < QP - 1; r++) (void)step(xlate(pro[r], r));
+            } else {
+#pragma unroll
+                for (int i = 0; i < BT; i++) v[i] = row(QP - 1 + BT * bt + i);   // BT row loads in flight
+            }
 #pragma unroll
             for (int i = 0; i < BT; i++) v[i] = step(xlate(v[i], QP - 1 + BT * bt + i));
 #pragma unroll
