@@ -739,17 +739,54 @@ struct Nco {
 };
 
 // ----------------------------------------------------------- quadrature
+// demod/quadrature.h:41-56: arg(y * conj(d)) / dev (one expression for every kernel using it)
+__device__ __forceinline__ float quad_value(float2 y, float2 d, float invDev) {
+    const float br = d.x, bi = -d.y;
+    const float re = (y.x * br) - (y.y * bi);
+    const float im = (y.y * br) + (y.x * bi);
+    return atan2f(im, re) * invDev;
+}
 __global__ void quad_kernel(const float2* __restrict__ in, float* __restrict__ out, int n, const float2* __restrict__ din,
                             float2* __restrict__ dinNext, float invDev) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float2 y = in[i];
-    const float2 d = i ? in[i - 1] : din[0];
-    const float br = d.x, bi = -d.y;
-    const float re = (y.x * br) - (y.y * bi);
-    const float im = (y.y * br) + (y.x * bi);
-    out[i] = atan2f(im, re) * invDev;
+    out[i] = quad_value(y, i ? in[i - 1] : din[0], invDev);
     if (i == n - 1) dinNext[0] = y;
+}
+
+// BroadcastFM mono for short calls (a reference block: 307,200 / 256 = 1,200 samples at
+// 240 kS/s): the quadrature and the audio FIR (+ LRToStereo) in one launch instead of two
+// 5-7 us ones. Workgroup b computes outputs [256 b, 256 b + 256) from the quadrature values of
+// its window of [hist || quad(in)] (halo recomputed), with the FIR's tap order and fmaf chain
+// (fir_kernel at D = 1), so the outputs are bit-identical to the two-launch path; the last
+// workgroup writes the next call's FIR history and y[-1].
+constexpr int WFM_TM = 256;
+__global__ __launch_bounds__(WFM_TM) void wfm_short_kernel(
+    const float2* __restrict__ in, int count, const float2* __restrict__ din, float2* __restrict__ dinNext,
+    const float* __restrict__ hist, float* __restrict__ histNext, const float* __restrict__ taps, int Q, int H,
+    float invDev, float2* __restrict__ out) {
+    extern __shared__ float X[];
+    const int tid = threadIdx.x;
+    auto qv = [&](long long b) -> float {   // [hist || quad(in)][b], zero past the end
+        if (b < H) return hist[b];
+        const long long i = b - H;
+        if (i >= count) return 0.0f;
+        return quad_value(in[i], i ? in[i - 1] : din[0], invDev);
+    };
+    if (blockIdx.x == gridDim.x - 1) {
+        for (int k = tid; k < H; k += WFM_TM) histNext[k] = qv((long long)count + k);
+        if (tid == 0) dinNext[0] = in[count - 1];
+        return;
+    }
+    const int m0 = blockIdx.x * WFM_TM;
+    for (int j = tid; j < WFM_TM + Q; j += WFM_TM) X[j] = qv((long long)m0 + j);
+    __syncthreads();
+    const int m = m0 + tid;
+    if (m >= count) return;
+    float acc = 0.0f;
+    for (int q = 0; q < Q; q++) acc = fmaf(X[tid + q], taps[q], acc);
+    out[m] = make_float2(acc, acc);
 }
 
 // ------------------------------------------------ polyphase resampler
@@ -1715,11 +1752,33 @@ extern "C" int sdrgpu_fm_create(sdrgpu_block** h, int device, double samplerate,
     return wrap(h, c, rc);
 }
 
+// [quadrature, stereo FIR at D = 1] with wfm_short_kernel for calls up to kShortMax samples
+struct WfmBlock : ChainBlock {
+    static constexpr int kShortMax = 1 << 15;
+    int run(const void* in, int count, void* out, hipStream_t s) override {
+        if (kids.size() != 2) return ChainBlock::run(in, count, out, s);
+        auto* qb = static_cast<QuadBlock*>(kids[0].get());
+        auto* fb = static_cast<FirBlock*>(kids[1].get());
+        if (count <= 0 || count > kShortMax || fb->D != 1) return ChainBlock::run(in, count, out, s);
+        SDRGPU_SET_DEVICE(device);
+        const int blocks = (count + WFM_TM - 1) / WFM_TM;
+        const size_t lds = sizeof(float) * (size_t)(WFM_TM + fb->Q);
+        hipLaunchKernelGGL(wfm_short_kernel, dim3(blocks + 1), dim3(WFM_TM), lds, s, (const float2*)in, count,
+                           qb->din[qb->cur].as<float2>(), qb->din[qb->cur ^ 1].as<float2>(), fb->hist[fb->cur].as<float>(),
+                           fb->hist[fb->cur ^ 1].as<float>(), fb->taps.as<float>(), fb->Q, fb->ntaps - 1, qb->invDev,
+                           (float2*)out);
+        SDRGPU_HIP(hipGetLastError());
+        qb->cur ^= 1;
+        fb->cur ^= 1;
+        return count;
+    }
+};
+
 // BroadcastFM, stereo == false (demod/broadcast_fm.h:144-215): quadrature(dev) ->
 // 228-tap (at 240 kS/s) audio LPF lowPass(15 kHz, 4 kHz) -> LRToStereo(l = r)
 extern "C" int sdrgpu_wfm_create(sdrgpu_block** h, int device, double deviation, double samplerate, int lowPass) {
     if (!h) { set_error("null out-handle"); return SDRGPU_EARG; }
-    auto* c = new ChainBlock();
+    auto* c = new WfmBlock();
     c->device = device; c->in_dtype = SDRGPU_C64; c->out_dtype = SDRGPU_C64;
     int rc = c->init_stream();
     sdrgpu_block* qh = nullptr;

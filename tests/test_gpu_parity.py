@@ -400,6 +400,26 @@ def test_wfm_mono_vs_oracle(rng):
         np.testing.assert_array_equal(yg["l"], yg["r"])
 
 
+def test_wfm_short_call_launch_bit_exact(rng):
+    """Calls of up to 32,768 samples run BroadcastFM mono as one launch (quadrature + audio FIR +
+    LRToStereo, wfm_short_kernel); longer calls run the quadrature and FIR kernels. Same tap order
+    and fmaf chain, same quadrature expression: the stream is bit-identical whichever way it is
+    cut, including the state handed between the two paths (FIR history, y[-1])."""
+    x = iq(rng, 200000)
+    one = dsp.BroadcastFM(100000, 240000).process(x)            # one long call: two launches
+    g = dsp.BroadcastFM(100000, 240000)
+    cuts = [1200, 1, 255, 256, 257, 40000, 1200, 32768, 32769, 999]
+    parts, i = [], 0
+    for n in cuts:
+        parts.append(g.process(x[i:i + n]))
+        i += n
+    parts.append(g.process(x[i:]))
+    got = np.concatenate(parts)
+    assert got.shape == one.shape
+    for ch in ("l", "r"):
+        assert np.array_equal(got[ch].view(np.uint32), one[ch].view(np.uint32)), ch
+
+
 @pytest.mark.parametrize("stereo", [False, True])
 def test_broadcast_fm_rds_branch(stereo):
     """BroadcastFM's RDS output (broadcast_fm.h:164-171, 193-203): MPX -> FrequencyXlator(-57 kHz)
