@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c5", choices=["c5", "c2", "c3", "c4"])
+    ap.add_argument("--config", default="c5", choices=["c5", "c2", "c3", "c4", "c4g"])
     ap.add_argument("--log2-batch", type=int, default=28, help="IQ samples per GPU per step = 2^k (c5/c3)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline leg (1-core, all-core)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -165,6 +165,28 @@ class C4:
         pass
 
 
+class C4G(C4):
+    """C4 with the per-frame DFT "cast as batched MFMA GEMM" (SURVEY 8(d) C4 asks for both forms):
+    the same branch FIRs, then two complex 32x32 products per frame on v_mfma_f32_16x16x4_f32."""
+
+    def __init__(self, B, shard, dev):
+        super().__init__(B, shard, dev)
+        taps = dsp.windowed_sinc(16 * self.M, np.pi / self.M)
+        self.ch = dsp.PolyphaseChannelizer(self.M, taps, device=dev, dft="gemm")
+        self.kernel_name = "chan2_kernel<1024,GEMM> (16-tap branch FIRs + DFT as 2 complex 32x32 MFMA GEMMs per frame)"
+
+    def flop_roofline(self, kern_ms):
+        # executed: 64 flop/sample of branch FIR (VALU) + 512 flop/sample of DFT-GEMM (MFMA: 2 x 128
+        # v_mfma_f32_16x16x4_f32 of 2048 flop per 1024-sample frame) + the twiddle (6 flop)
+        tf = (64 + 512) * self.B / (kern_ms * 1e-3) / 1e12
+        mf = 512 * self.B / (kern_ms * 1e-3) / 1e12
+        return {"bound": "mfma-fp32", "achieved": round(tf, 2), "peak": 157.3, "unit": "TFLOP/s",
+                "frac": round(tf / 157.3, 4), "flop_per_sample": 576, "mfma_TFLOPs": round(mf, 2),
+                "note": "dense fp32 matrix-core peak 157.3 TF (MI355X_MICROARCH.md; 156 TF/s sustained measured, "
+                        "tools/ubench/mfma_f32_peak.hip): this form is compute-bound at >= 0.88 ms of pure MFMA per "
+                        "2^28 samples, the FFT form (c4) HBM-bound"}
+
+
 def _run_generic(wl, x, s, timed_call):
     timed_call(lambda: wl.dominant(x, s))
     wl.rest(x, s)
@@ -208,7 +230,9 @@ WORKLOADS = {"c5": "C5 per-GPU slice: 64k BH7 FFT+log-mag (back-to-back) + 2048-
                    "61.44M->240k + BroadcastFM mono",
              "c2": "C2: 1M-point BH7 FFT + log-mag, nz=1e6 zero-padded, 256 frames/step",
              "c3": "C3: xlator + 256-tap FIR /8 + FM quadrature (fused), 2^28 samples/step",
-             "c4": "C4: 1024-channel polyphase channelizer (16384-tap prototype), 2^28 samples/step"}
+             "c4": "C4: 1024-channel polyphase channelizer (16384-tap prototype), 2^28 samples/step",
+             "c4g": "C4 as batched MFMA GEMM: 1024-channel polyphase channelizer, per-frame DFT as two complex "
+                    "32x32 f32 MFMA products, 2^28 samples/step"}
 
 
 def run_config(config, a, shard, dev, stream):
@@ -217,7 +241,7 @@ def run_config(config, a, shard, dev, stream):
     B = 1 << a.log2_batch
     if config == "c2":
         B = 256 * 1000000
-    wl = {"c5": C5, "c2": C2, "c3": C3, "c4": C4}[config](B, shard, dev)
+    wl = {"c5": C5, "c2": C2, "c3": C3, "c4": C4, "c4g": C4G}[config](B, shard, dev)
     B = wl.B
     g = torch.Generator(device="cuda")
     g.manual_seed(shard.seed())
@@ -405,7 +429,7 @@ def main():
     # C2 and C3 carry the north_star's >= 10x / >= 40% targets, C4 the channelizer)
     subs = {}
     if world == 1 and not a.no_sub:
-        for c in ("c2", "c3", "c4", "c5"):
+        for c in ("c2", "c3", "c4", "c4g", "c5"):
             if c == a.config:
                 continue
             torch.cuda.empty_cache()
@@ -427,10 +451,14 @@ def main():
         if "roofline_flops" in head:
             out["roofline_flops"] = head["roofline_flops"]
         if world == 1 and not a.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(a.config, a.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline("c4" if a.config == "c4g" else a.config, a.cpu_seconds)
             out["speedup_vs_cpu_all_cores"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+            cpu_cache = {}
             for c, r in subs.items():
-                r["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds)
+                ck = "c4" if c == "c4g" else c   # both C4 forms against the same CPU channelizer
+                if ck not in cpu_cache:
+                    cpu_cache[ck] = cpu_baseline(ck, a.cpu_seconds)
+                r["cpu_baseline"] = cpu_cache[ck]
                 r["speedup_vs_cpu_all_cores"] = round(r["value"] / r["cpu_baseline"]["value"], 1)
         if subs:
             out["configs"] = subs

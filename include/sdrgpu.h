@@ -176,6 +176,10 @@ int sdrgpu_deemphasis_set(sdrgpu_block* h, double tau, double samplerate);   /* 
  * decimating_fir.h:45) with an exact NCO; taps <= 16 M (bank layout polyphase_bank.h:32).
  * Output: frames x M complex, out[m*M + k]; out_count = frames * M. M in {256, 512, 1024}. */
 int sdrgpu_channelizer_create(sdrgpu_block** h, int device, int channels, const float* taps, int ntaps);
+/* The channelizer's per-frame M-point DFT (same definition as above): mode 0 = LDS FFT (default),
+ * 1 = the polyphase filterbank "cast as batched MFMA GEMM" (BASELINE C4): 1024 = 32 x 32, two
+ * complex 32x32 products per frame on v_mfma_f32_16x16x4_f32. M = 1024 only. */
+int sdrgpu_channelizer_set_dft(sdrgpu_block* h, int mode);
 
 int sdrgpu_block_process(sdrgpu_block* h, const void* in, int count, void* out);      /* host buffers */
 int sdrgpu_block_process_dev(sdrgpu_block* h, const void* in, int count, void* out, void* stream);

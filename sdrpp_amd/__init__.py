@@ -91,6 +91,7 @@ def _load():
         "sdrgpu_fm_create": (i, [pp, i, d, d, i, i]),
         "sdrgpu_wfm_create": (i, [pp, i, d, d, i]),
         "sdrgpu_channelizer_create": (i, [pp, i, i, fp, i]),
+        "sdrgpu_channelizer_set_dft": (i, [vp, i]),
         "sdrgpu_broadcast_fm_create": (i, [pp, i, d, d, i, i]),
         "sdrgpu_deemphasis_create": (i, [pp, i, i, d, d]),
         "sdrgpu_deemphasis_set": (i, [vp, d, d]),

@@ -103,10 +103,109 @@ __global__ __launch_bounds__(L) void chan_kernel(const float2* __restrict__ hist
     }
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// The M = 1024 DFT of the 16 branch vectors of a batch as dense matrix products on the f32
+// matrix cores (the "filterbank cast as batched MFMA GEMM" form of BASELINE C4). With
+// c = 32 a + b and k = k1 + 32 k2, W_1024^(kc) = W_32^(k1 a) W_1024^(k1 b) W_32^(k2 b), so per
+// frame (viewed as the 32 x 32 matrix X[a][b] = v[32 a + b]):
+//   Z = F X  (F[k1][a] = W_32^(k1 a)),  Z'[k1][b] = Z[k1][b] W_1024^(k1 b),  Y = Z' F  (F symmetric),
+// and Y[k1][k2] is channel k1 + 32 k2: two complex 32 x 32 x 32 products = 2 x 128
+// v_mfma_f32_16x16x4_f32 per frame (512 flop per sample against the FFT's ~50). Wave w of the
+// 8 owns frames w and w + 8 of the batch: all its LDS traffic stays inside its own sequences,
+// so the stages need no workgroup barrier. MFMA operand layout (as fir_mfma_kernel): A[i][k]
+// from lane (i = lane & 15, k = lane >> 4), B[k][j] from lane (j = lane & 15, k = lane >> 4),
+// accumulator e of a lane = D[4 (lane >> 4) + e][lane & 15]. The W_32 operand of lane (i, kk)
+// at k-step s of block x is W_32^((16 x + i)(4 s + kk)) in both products.
+template <int L>
+__device__ __forceinline__ void chan_dft_gemm(float2* lds, const float2* twl, int tid, int mb, int m1, float2* __restrict__ out) {
+    static_assert(L == 1024, "DFT-GEMM channelizer: 1024 = 32 x 32");
+    constexpr int LS = Lds<L>::LS;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int i = lane & 15, kk = lane >> 4;
+    // W_32^n = W_1024^(32 n), read from the staged twiddles at each k-step (as registers the 16
+    // values per lane push the kernel past 256 VGPRs)
+    auto Wv = [&](int x, int s) { return twl[32 * (((16 * x + i) * (4 * s + kk)) & 31)]; };
+#pragma unroll 1
+    for (int fr = 0; fr < 2; fr++) {
+        const int sF = wv + 8 * fr;
+        float2* X = lds + sF * LS;
+        f32x4 ar[2][2], ai[2][2];   // [row block][column block]
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 2; y++) ar[x][y] = ai[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // Z = F X: A = F (rows k1 = 16 bi + i), B = X (k = a = 4 s + kk, columns b = 16 bj + i)
+#pragma unroll
+        for (int s = 0; s < 8; s++)
+#pragma unroll
+            for (int bj = 0; bj < 2; bj++) {
+                const float2 xb = X[pad16(32 * (4 * s + kk) + 16 * bj + i)];
+#pragma unroll
+                for (int bi = 0; bi < 2; bi++) {
+                    const float2 w = Wv(bi, s);
+                    ar[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, xb.x, ar[bi][bj], 0, 0, 0);
+                    ar[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(-w.y, xb.y, ar[bi][bj], 0, 0, 0);
+                    ai[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, xb.y, ai[bi][bj], 0, 0, 0);
+                    ai[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, xb.x, ai[bi][bj], 0, 0, 0);
+                }
+            }
+        // Z'[k1][b] = Z[k1][b] W_1024^(k1 b) (k1 b < 1024), written over X[k1][b]: this wave has
+        // read every element of its sequence above (LDS operations of a wave complete in order)
+#pragma unroll
+        for (int bi = 0; bi < 2; bi++)
+#pragma unroll
+            for (int bj = 0; bj < 2; bj++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int k1 = 16 * bi + 4 * kk + e, b = 16 * bj + i;
+                    X[pad16(32 * k1 + b)] = cmul(make_float2(ar[bi][bj][e], ai[bi][bj][e]), twl[k1 * b]);
+                }
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 2; y++) ar[x][y] = ai[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // Y = Z' F: A = Z' (rows k1 = 16 bi + i, k = b = 4 s + kk), B = F (columns k2 = 16 bj + i)
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            float2 za[2];
+#pragma unroll
+            for (int bi = 0; bi < 2; bi++) za[bi] = X[pad16(32 * (16 * bi + i) + 4 * s + kk)];
+#pragma unroll
+            for (int bi = 0; bi < 2; bi++)
+#pragma unroll
+                for (int bj = 0; bj < 2; bj++) {
+                    const float2 g = Wv(bj, s);
+                    ar[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(za[bi].x, g.x, ar[bi][bj], 0, 0, 0);
+                    ar[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(-za[bi].y, g.y, ar[bi][bj], 0, 0, 0);
+                    ai[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(za[bi].x, g.y, ai[bi][bj], 0, 0, 0);
+                    ai[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(za[bi].y, g.x, ai[bi][bj], 0, 0, 0);
+                }
+        }
+        // channel k = k1 + 32 k2 into the sequence (natural order), then one coalesced row store
+#pragma unroll
+        for (int bi = 0; bi < 2; bi++)
+#pragma unroll
+            for (int bj = 0; bj < 2; bj++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int k1 = 16 * bi + 4 * kk + e, k2 = 16 * bj + i;
+                    X[pad16(k1 + 32 * k2)] = make_float2(ar[bi][bj][e], ai[bi][bj][e]);
+                }
+        const int m = mb + sF;
+        if (m < m1) {
+            float2* o = out + (long long)m * L;
+#pragma unroll
+            for (int q = 0; q < L / 64; q++) o[lane + 64 * q] = X[pad16(lane + 64 * q)];
+        }
+    }
+}
+
 // Two branches per thread (L/2 threads): the kernel above needs ~180 VGPRs and spills at
 // 1024 threads (128-VGPR cap); here each lane owns branches r and r + L/2 and plays two FFT
-// roles in turn (sequences sF and sF + 8), with a 256-VGPR cap at L/2 threads.
-template <int L>
+// roles in turn (sequences sF and sF + 8), with a 256-VGPR cap at L/2 threads. GEMM: the
+// per-frame DFT runs as chan_dft_gemm (matrix cores) instead of the LDS FFT.
+template <int L, bool GEMM = false>
 __global__ __launch_bounds__(L / 2) void chan2_kernel(const float2* __restrict__ hist, const float2* __restrict__ in, int H,
                                                       int count, const float* __restrict__ taps, long long offset0,
                                                       int rot, int frames, int fpw, const float2* __restrict__ tw,
@@ -167,6 +266,11 @@ __global__ __launch_bounds__(L / 2) void chan2_kernel(const float2* __restrict__
             }
         }
         __syncthreads();
+        if constexpr (GEMM) {
+            chan_dft_gemm<L>(lds, twl, tid, mb, m1, out);
+            __syncthreads();
+            continue;
+        }
 #pragma unroll 1
         for (int half = 0; half < 2; half++) {
             const int sF = tid / T + 8 * half, tF = tid % T;
@@ -199,6 +303,7 @@ struct ChannelizerBlock : Block {
     // two branches per thread (chan2_kernel, no spill): 1.17 vs 1.63 ms per 2^28 samples
     // against the one-branch kernel on one box; SDRGPU_CHAN_TWO=0 selects chan_kernel
     bool two = true;
+    int dft = 0;             // 0: LDS FFT (chan2_kernel); 1: DFT-GEMM on the matrix cores (M = 1024)
     long long phase = 0;     // absolute input index mod M of the next sample
     DevBuf taps, tw, hist[2];
     int cur = 0;
@@ -246,10 +351,13 @@ struct ChannelizerBlock : Block {
     template <int L>
     int launch(const void* in, int count, int frames, long long offset0, int rot, void* out, hipStream_t s) {
         auto k = two ? chan2_kernel<L> : chan_kernel<L>;
+        if constexpr (L == 1024) {
+            if (dft == 1) k = chan2_kernel<L, true>;
+        }
         const size_t lds = sizeof(float2) * (16 * Lds<L>::LS + L);
         SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         const int grid = (frames + fpw - 1) / fpw;
-        hipLaunchKernelGGL(k, dim3(grid), dim3(two ? L / 2 : L), lds, s, hist[cur].as<float2>(), (const float2*)in, Hp, count,
+        hipLaunchKernelGGL(k, dim3(grid), dim3(two || dft ? L / 2 : L), lds, s, hist[cur].as<float2>(), (const float2*)in, Hp, count,
                            taps.as<float>(), offset0, rot, frames, fpw, tw.as<float2>(), (float2*)out);
         SDRGPU_HIP(hipGetLastError());
         return SDRGPU_OK;
@@ -293,5 +401,16 @@ extern "C" int sdrgpu_channelizer_create(sdrgpu_block** h, int device, int chann
     const int rc = b->setup(device, channels, taps, ntaps);
     if (rc < 0) { delete b; return rc; }
     *h = new sdrgpu_block{b};
+    return SDRGPU_OK;
+}
+
+// C4's two forms: 0 = branch FIRs + LDS FFT (default, HBM-bound), 1 = branch FIRs + DFT as
+// batched f32 MFMA GEMMs (1024 channels only)
+extern "C" int sdrgpu_channelizer_set_dft(sdrgpu_block* h, int mode) {
+    auto* b = h ? dynamic_cast<ChannelizerBlock*>(h->impl) : nullptr;
+    if (!b) { set_error("channelizer_set_dft: not a channelizer"); return SDRGPU_EARG; }
+    if (mode != 0 && mode != 1) { set_error("channelizer_set_dft: mode %d (0 FFT, 1 MFMA GEMM)", mode); return SDRGPU_EARG; }
+    if (mode == 1 && b->M != 1024) { set_error("channelizer_set_dft: the MFMA GEMM form needs 1024 channels (have %d)", b->M); return SDRGPU_EARG; }
+    b->dft = mode;
     return SDRGPU_OK;
 }

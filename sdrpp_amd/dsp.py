@@ -358,14 +358,19 @@ def windowed_sinc(count, omega, norm=1.0):
 class PolyphaseChannelizer(Block):
     """M-channel critically sampled polyphase channelizer (BASELINE C4): channel k of frame m is
     FrequencyXlator(-k fs/M) -> DecimatingFIR(taps, M) with an exact NCO. ``process`` returns
-    complex64 [frames * M] laid out out[m * M + k]."""
+    complex64 [frames * M] laid out out[m * M + k]. ``dft="gemm"`` (M = 1024) computes each
+    frame's DFT as two complex 32x32 matrix products on the f32 matrix cores instead of the LDS
+    FFT (sdrgpu_channelizer_set_dft)."""
 
-    def __init__(self, channels, taps, device=0):
+    def __init__(self, channels, taps, device=0, dft="fft"):
         t = np.ascontiguousarray(taps, np.float32)
         self._taps = t
         self.channels = int(channels)
         h = _make(lib.sdrgpu_channelizer_create, device, int(channels), _fptr(t), int(t.shape[0]))
         super().__init__(h, np.complex64, np.complex64)
+        if dft not in ("fft", "gemm"):
+            raise ValueError(f"dft must be 'fft' or 'gemm', not {dft!r}")
+        check(lib.sdrgpu_channelizer_set_dft(self._h, 1 if dft == "gemm" else 0))
 
 
 class AGC(Block):

@@ -141,3 +141,57 @@ def test_channelizer_reset_and_empty(_gpu, rng):
     ch.reset()
     b = ch.process(x)
     assert np.array_equal(a, b)
+
+
+# ---------------------------------------------------------------- MFMA DFT-GEMM form (C4)
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [48 * 1024 + 333, 700 * 1024 + 5])
+def test_channelizer_gemm_vs_definition(_gpu, n, rng):
+    """dft="gemm" (the filterbank's DFT as two complex 32x32 products per frame on the matrix
+    cores): every channel of every frame against the fp64 definition at the same `chan_tol` bar
+    as the FFT form; 700 frames span several workgroups (256 frames each) and a ragged last one."""
+    M = 1024
+    h = dsp.windowed_sinc(16 * M, np.pi / M)
+    x = iq(rng, n)
+    y = dsp.PolyphaseChannelizer(M, h, dft="gemm").process(x)
+    frames = (n + M - 1) // M
+    assert y.shape[0] == frames * M
+    yf = _frames(y, M)
+    if n < 100 * M:
+        check_frames(yf, oracle.channelize(x, h, M, list(range(M))), M, "gemm all channels")
+    else:
+        chans = sorted(set([0, 1, 31, 32, 33, 511, 512, 1023] + list(rng.integers(0, M, 8))))
+        check_frames(yf[chans], oracle.channelize(x, h, M, chans), M, "gemm multi-workgroup")
+    # same branch FIRs as the FFT form: the two DFTs agree to the same bar
+    yfft = _frames(dsp.PolyphaseChannelizer(M, h).process(x), M)
+    check_frames(yf, yfft.astype(np.complex128), M, "gemm vs fft")
+
+
+@pytest.mark.gpu
+def test_channelizer_gemm_tone_and_split(_gpu, rng):
+    """A tone at the centre of channel k0 lands in k0 only (gemm form), and ragged calls give
+    the same output stream as one call, bit for bit."""
+    M = 1024
+    h = dsp.windowed_sinc(16 * M, np.pi / M)
+    k0, n = 777, 64 * M
+    t = np.arange(n)
+    x = (0.5 * np.exp(2j * np.pi * k0 * t / M)).astype(np.complex64)
+    y = _frames(dsp.PolyphaseChannelizer(M, h, dft="gemm").process(x), M)
+    steady = y[:, 20:]
+    assert np.allclose(np.abs(steady[k0]), 0.5 * h.sum(), rtol=1e-4)
+    assert np.delete(np.abs(steady), k0, axis=0).max() < 1e-3 * 0.5
+    xr = iq(rng, 40 * M + 5)
+    one = dsp.PolyphaseChannelizer(M, h, dft="gemm").process(xr)
+    ch = dsp.PolyphaseChannelizer(M, h, dft="gemm")
+    parts, i = [], 0
+    for c in [1, M - 1, 3 * M + 7, 0, 5 * M, 17, 2 * M]:
+        parts.append(ch.process(xr[i:i + c]))
+        i += c
+    parts.append(ch.process(xr[i:]))
+    assert np.array_equal(np.concatenate(parts), one)
+
+
+@pytest.mark.gpu
+def test_channelizer_gemm_needs_1024(_gpu):
+    with pytest.raises(Exception):
+        dsp.PolyphaseChannelizer(256, dsp.windowed_sinc(16 * 256, np.pi / 256), dft="gemm")
