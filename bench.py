@@ -31,7 +31,7 @@ import torch.distributed as dist  # noqa: E402
 
 import sdrpp_amd  # noqa: E402
 from sdrpp_amd import dsp  # noqa: E402
-from sdrpp_amd.multistream import StreamShard  # noqa: E402
+from sdrpp_amd.multistream import CudaGather, GatherPipeline, StreamShard  # noqa: E402
 
 METRIC = "IQ Msamples/s through FFT+FIR+demod chain; % HBM roofline at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
@@ -213,6 +213,25 @@ def cpu_baseline(config, seconds):
             "host": {"nproc": h["nproc"], "affinity_cpus": h["affinity"], "model": h["model"]}}
 
 
+def spectrum_ulp_report():
+    """The spectrum's dB error in fp32 ulps vs the correctly rounded fp64 DFT (bins within 60 dB
+    of the frame peak): the newest report test_spectrum_ulp_distribution wrote (profiles/)."""
+    for path in ("profiles/r3/spectrum_ulp_r3a.jsonl", "profiles/r2/spectrum_ulp.jsonl"):
+        try:
+            with open(os.path.join(ROOT, path)) as f:
+                rows = [json.loads(l) for l in f if l.strip()]
+        except OSError:
+            continue
+        out = {f"{r['case']}_N{r['N']}": {"max_ulp": r["gpu"]["max"], "frac_le_1ulp": round(r["gpu"]["frac_le_1ulp"], 4),
+                                          "p99_ulp": r["gpu"]["p99"],
+                                          "pocketfft_max_ulp": r["pocketfft_f32"]["max"],
+                                          "pocketfft_frac_le_1ulp": round(r["pocketfft_f32"]["frac_le_1ulp"], 4)}
+               for r in rows}
+        out["source"] = path
+        return out
+    return None
+
+
 def traffic_per_sample(config):
     """HBM bytes per input sample of the dominant launch group, from the newest committed
     rocprofv3 PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/pmc_bytes_per_sample.py)."""
@@ -248,13 +267,12 @@ def run_config(config, a, shard, dev, stream):
     x = (torch.rand(2 * B, device="cuda", generator=g) * 2 - 1).contiguous()   # complex_t interleaved
     # N > 1: every step's waterfall rows go to rank 0 over RCCL (libsdrgpu's C-ABI gather) on a
     # stream of their own, overlapping the next step; the zoom rows are double-buffered and a step
-    # waits only for the gather that last used its buffer
-    gather = shard.rccl_gather(dev) if (world > 1 and hasattr(wl, "zoom")) else None
-    if gather is not None:
-        gstream = torch.cuda.Stream()
-        gout = torch.empty(world * wl.zoom_count, dtype=torch.float32, device="cuda") if rank == 0 else None
-    done = [None, None]   # gather-finished events per zoom buffer
-    nstep = [0]
+    # waits only for the gather that last used its buffer (multistream.GatherPipeline; the same
+    # protocol runs on the CPU over gloo in tests/test_multistream_gloo.py)
+    pipe = None
+    if world > 1 and hasattr(wl, "zoom"):
+        pipe = GatherPipeline(shard, wl.zoom_count, CudaGather(shard, dev))
+        wl.zoom = pipe.bufs
 
     ev = []
     # One stream for the whole step. Forking the spectrum and the VFO chain onto two streams
@@ -265,8 +283,6 @@ def run_config(config, a, shard, dev, stream):
     # (1.58 -> 1.89 ms), so the roofline numbers would stop describing the kernel.
     def step(timed):
         evs = []
-        buf = nstep[0] & 1
-        nstep[0] += 1
 
         def timed_call(fn):   # HIP events around the dominant kernel's launches, on their stream
             if timed:
@@ -276,28 +292,19 @@ def run_config(config, a, shard, dev, stream):
             if timed:
                 e1.record(stream)
                 evs.append((e0, e1))
-        if gather is not None and done[buf] is not None:
-            stream.wait_event(done[buf])
+        buf = pipe.acquire(stream) if pipe is not None else 0
         if hasattr(wl, "run"):
             wl.run(x, stream.cuda_stream, timed_call, buf)
         else:
             _run_generic(wl, x, stream.cuda_stream, timed_call)
         if timed:
             ev.append(evs)
-        if gather is not None:
-            ready = torch.cuda.Event()
-            ready.record(stream)
-            gstream.wait_event(ready)
-            gather.gather_dev(wl.zoom[buf].data_ptr(), wl.zoom_count, gout.data_ptr() if rank == 0 else 0,
-                              gstream.cuda_stream)
-            fin = torch.cuda.Event()
-            fin.record(gstream)
-            done[buf] = fin
+        if pipe is not None:
+            pipe.publish(buf, stream, timed=timed)
 
     def drain():
-        for e in done:
-            if e is not None:
-                stream.wait_event(e)
+        if pipe is not None:
+            pipe.drain(stream)
 
     for _ in range(a.warmup):
         step(False)
@@ -313,8 +320,14 @@ def run_config(config, a, shard, dev, stream):
     elapsed = time.perf_counter() - t0
     kern_ms = sum(sum(e0.elapsed_time(e1) for e0, e1 in evs) for evs in ev) / max(len(ev), 1)
     elapsed, kern_ms = shard.max_over_ranks([elapsed, kern_ms], device="cuda")
-    if gather is not None:
-        gather.close()
+    if pipe is not None:
+        # the first multi-GPU run proves the gather: rank 0's received rows of the last step carry
+        # each sender's own checksum; the gather's own time is reported next to the step time
+        ok, det = pipe.verify()
+        gms = shard.max_over_ranks([pipe.gather_ms() or 0.0], device="cuda")[0]
+        wl.gather_report = {"verified": bool(ok), "ms_per_gather_max_rank": round(gms, 4),
+                            "bytes_per_rank_per_step": 4 * wl.zoom_count, **(det or {})}
+        pipe.close()
     del x
     return B, elapsed, kern_ms, wl
 
@@ -383,14 +396,44 @@ def per_call_c5(dev, stream, calls=300, block=307200, single_only=False):
     n_host = max(calls // 3, 20)
     for _ in range(n_host):
         fe.push(xh)
+    sync_us = (time.perf_counter() - t0) / n_host * 1e6
+    # the drop-in worker's call style (IQFrontEnd drop-in): blocks from the pinned input ring
+    # (sdrgpu_host_alloc) submitted without waiting, two in flight, each block's rows and VFO output
+    # copied out of the pinned result slot when collected (the hand-off to acquireFFTBuffer / the
+    # VFO stream)
+    import ctypes
+    ring = []
+    for k in range(4):
+        hp = ctypes.c_void_p()
+        sdrpp_amd.check(sdrpp_amd.lib.sdrgpu_host_alloc(ctypes.byref(hp), 8 * block))
+        ctypes.memmove(hp.value, xh.ctypes.data, 8 * block)
+        ring.append(hp)
+
+    def pipelined(n):
+        pend = []
+        for k in range(n):
+            pend.append(fe.submit(None, ptr=ring[k % 4].value, count=block))
+            if len(pend) == 2:
+                fe.collect(pend.pop(0), vfos=[vid])
+        for t in pend:
+            fe.collect(t, vfos=[vid])
+    pipelined(20)
+    t0 = time.perf_counter()
+    pipelined(n_host)
     host_us = (time.perf_counter() - t0) / n_host * 1e6
+    for hp in ring:
+        sdrpp_amd.lib.sdrgpu_host_free(hp)
     fe.close()
+    # PCIe floor of a block: its 2.46 MB H2D + the rows / VFO read-back, at the measured copy rate
     return {"block": block, "us_per_call_device": round(dev_us, 1), "MSps_device": round(block / dev_us, 1),
             "concurrent_streams": K, "MSps_device_concurrent": round(K * block / multi_us, 1),
             "us_per_call_host_dropin": round(host_us, 1), "MSps_host_dropin": round(block / host_us, 1),
+            "us_per_call_host_sync": round(sync_us, 1),
             "note": "one 307,200-sample block per call (fs/200 at 61.44 MS/s) through the device front end "
-                    "(spectrum + 1 VFO) + WFM; concurrent: K independent front ends on K HIP streams; the host "
-                    "drop-in adds the pinned H2D and a synchronise per block"}
+                    "(spectrum + 1 VFO) + WFM; concurrent: K independent front ends on K HIP streams; host drop-in: "
+                    "the IQFrontEnd drop-in's pipelined call style (sdrgpu_frontend_submit/collect, blocks from "
+                    "pinned ring slots, two in flight, rows + VFO output copied out per block); host sync: one "
+                    "synchronous push per block (staging memcpy, H2D, kernels, read-back)"}
 
 
 def config_result(config, a, world, B, elapsed, kern_ms, wl):
@@ -408,6 +451,8 @@ def config_result(config, a, world, B, elapsed, kern_ms, wl):
          "chain_hbm_GBs": round(wl.bytes_per_sample * value * 1e6 / world / 1e9, 1)}
     if hasattr(wl, "flop_roofline"):
         r["roofline_flops"] = wl.flop_roofline(kern_ms)
+    if getattr(wl, "gather_report", None):
+        r["gather"] = wl.gather_report
     return r
 
 
@@ -450,6 +495,9 @@ def main():
         }
         if "roofline_flops" in head:
             out["roofline_flops"] = head["roofline_flops"]
+        if "gather" in head:
+            out["gather"] = head["gather"]
+        out["spectrum_ulp"] = spectrum_ulp_report()
         if world == 1 and not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline("c4" if a.config == "c4g" else a.config, a.cpu_seconds)
             out["speedup_vs_cpu_all_cores"] = round(out["value"] / out["cpu_baseline"]["value"], 1)

@@ -68,6 +68,8 @@ int         sdrgpu_stream_destroy(void* stream);
 int         sdrgpu_stream_synchronize(void* stream);
 int         sdrgpu_host_register(void* ptr, size_t bytes);   /* pin a dsp::stream buffer */
 int         sdrgpu_host_unregister(void* ptr);
+int         sdrgpu_host_alloc(void** ptr, size_t bytes);   /* pinned + registered (DMA'd directly) */
+int         sdrgpu_host_free(void* ptr);
 
 /* ------------------------------------------- host-side design (exact) ---- */
 /* Bit-exact restatements evaluated on the host, as the reference does. */
@@ -214,6 +216,19 @@ int sdrgpu_frontend_vfo_dev(sdrgpu_frontend* f, int id, const void** out, int* n
 int sdrgpu_frontend_read_vfo(sdrgpu_frontend* f, int id, void* out, int max);
 /* host copy of the last push's preprocessed IQ (what bound IQ streams receive, iq_frontend.cpp:114-120) */
 int sdrgpu_frontend_read_iq(sdrgpu_frontend* f, void* out, int max);
+/* Pipelined host call style (the IQFrontEnd drop-in's worker, round 3): submit enqueues a host
+ * block's H2D on the front end's copy stream, its processing and the read-back of its rows, VFO
+ * outputs and (flags & SDRGPU_FE_IQ) preprocessed IQ into pinned result slots, and returns a
+ * ticket without waiting; block k + 1's H2D overlaps block k's kernels and read-back. collect
+ * waits for a ticket and returns its row count with pinned host pointers to its results (valid
+ * until release). At most two tickets are in flight: release(k) before submitting block k + 2.
+ * A registered (sdrgpu_host_register / sdrgpu_host_alloc) `in` is DMA'd directly and must stay
+ * untouched until its ticket is collected; any other `in` is staged and may be reused at once. */
+#define SDRGPU_FE_IQ 1
+int sdrgpu_frontend_submit(sdrgpu_frontend* f, const void* in, int count, int kind, int flags);
+int sdrgpu_frontend_collect(sdrgpu_frontend* f, int ticket, const float** rows, const void** iq, int* niq);
+int sdrgpu_frontend_collected_vfo(sdrgpu_frontend* f, int ticket, int id, const void** out, int* n);
+int sdrgpu_frontend_release(sdrgpu_frontend* f, int ticket);
 
 /* ------------------------------------------ spectra gather (multi-GPU) ---- */
 /* Independent IQ streams run one per GPU; the only collective is a gather of their

@@ -116,6 +116,12 @@ def _load():
         "sdrgpu_frontend_read_spectra": (i, [vp, fp, i]),
         "sdrgpu_frontend_vfo_dev": (i, [vp, i, pp, ctypes.POINTER(i)]),
         "sdrgpu_frontend_read_vfo": (i, [vp, i, vp, i]),
+        "sdrgpu_frontend_submit": (i, [vp, vp, i, i, i]),
+        "sdrgpu_frontend_collect": (i, [vp, i, pp, pp, ctypes.POINTER(i)]),
+        "sdrgpu_frontend_collected_vfo": (i, [vp, i, i, pp, ctypes.POINTER(i)]),
+        "sdrgpu_frontend_release": (i, [vp, i]),
+        "sdrgpu_host_alloc": (i, [pp, ctypes.c_size_t]),
+        "sdrgpu_host_free": (i, [vp]),
         "sdrgpu_agc_create": (i, [pp, i, i, d, d, d, d, d, d]),
         "sdrgpu_agc_set_enabled": (i, [vp, i]),
         "sdrgpu_agc_set_gain": (i, [vp, ctypes.c_float]),

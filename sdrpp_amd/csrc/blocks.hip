@@ -876,11 +876,13 @@ PinnedBuf::~PinnedBuf() {
 }
 
 int StreamOrder::follow(hipStream_t s) {
-    if (last != nullptr && last != s) {
-        if (!ev) SDRGPU_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        SDRGPU_HIP(hipEventRecord(ev, last));
-        SDRGPU_HIP(hipStreamWaitEvent(s, ev, 0));
-    }
+    if (recorded && last != s) SDRGPU_HIP(hipStreamWaitEvent(s, ev, 0));
+    return SDRGPU_OK;
+}
+int StreamOrder::done(hipStream_t s) {
+    if (!ev) SDRGPU_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    SDRGPU_HIP(hipEventRecord(ev, s));
+    recorded = true;
     last = s;
     return SDRGPU_OK;
 }
@@ -1807,7 +1809,14 @@ extern "C" int sdrgpu_block_process_dev(sdrgpu_block* h, const void* in, int cou
     const hipStream_t s = stream ? (hipStream_t)stream : b->own;
     SDRGPU_SET_DEVICE(b->device);
     SDRGPU_CHECK(b->order.follow(s));
+    OrderScope od(b->order, s);
     return b->run(in, count, out, s);
+}
+
+int sdrgpu::block_run_owned(sdrgpu_block* h, const void* in, int count, void* out, hipStream_t s) {
+    NEED_HANDLE(h);
+    if (count < 0 || (count > 0 && (!in || !out))) { set_error("process: bad buffers"); return SDRGPU_EARG; }
+    return h->impl->run(in, count, out, s);
 }
 
 extern "C" int sdrgpu_block_process(sdrgpu_block* h, const void* in, int count, void* out) {
@@ -1827,15 +1836,13 @@ extern "C" int sdrgpu_block_process(sdrgpu_block* h, const void* in, int count, 
     const bool inPinned = host_pinned(in, (size_t)count * esize(b->in_dtype));
     const bool outPinned = host_pinned(out, (size_t)mExp * esize(b->out_dtype));
     if (count > 0) {
-        const void* src = in;
-        if (!inPinned) {
-            std::memcpy(b->pin_in.p, in, (size_t)count * esize(b->in_dtype));
-            src = b->pin_in.p;
-        }
-        SDRGPU_CHECK(b->order.follow(b->own));
-        SDRGPU_HIP(hipMemcpyAsync(b->dev_in.p, src, (size_t)count * esize(b->in_dtype), hipMemcpyHostToDevice, b->own));
+        if (!inPinned) std::memcpy(b->pin_in.p, in, (size_t)count * esize(b->in_dtype));
     }
     SDRGPU_CHECK(b->order.follow(b->own));
+    OrderScope od(b->order, b->own);
+    if (count > 0)
+        SDRGPU_HIP(hipMemcpyAsync(b->dev_in.p, inPinned ? in : b->pin_in.p, (size_t)count * esize(b->in_dtype),
+                                  hipMemcpyHostToDevice, b->own));
     int m = b->run(b->dev_in.p, count, b->dev_out.p, b->own);
     if (m < 0) return m;
     void* dst = (outPinned && m <= mExp) ? out : b->pin_out.p;

@@ -81,6 +81,23 @@ extern "C" int sdrgpu_host_register(void* ptr, size_t bytes) {
     g_pinned[(uintptr_t)ptr] = bytes;
     return SDRGPU_OK;
 }
+extern "C" int sdrgpu_host_alloc(void** ptr, size_t bytes) {
+    if (!ptr || bytes == 0) { set_error("host_alloc: bad argument"); return SDRGPU_EARG; }
+    *ptr = nullptr;
+    SDRGPU_HIP(hipHostMalloc(ptr, bytes, hipHostMallocDefault));
+    std::lock_guard<std::mutex> lk(g_pinMtx);
+    g_pinned[(uintptr_t)*ptr] = bytes;
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_host_free(void* ptr) {
+    if (!ptr) return SDRGPU_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_pinMtx);
+        g_pinned.erase((uintptr_t)ptr);
+    }
+    SDRGPU_HIP(hipHostFree(ptr));
+    return SDRGPU_OK;
+}
 extern "C" int sdrgpu_host_unregister(void* ptr) {
     {
         std::lock_guard<std::mutex> lk(g_pinMtx);

@@ -117,6 +117,16 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // from lane (i = lane & 15, k = lane >> 4), B[k][j] from lane (j = lane & 15, k = lane >> 4),
 // accumulator e of a lane = D[4 (lane >> 4) + e][lane & 15]. The W_32 operand of lane (i, kk)
 // at k-step s of block x is W_32^((16 x + i)(4 s + kk)) in both products.
+// Cross-lane LDS hand-off inside one wave: the HIP memory model does not order one lane's LDS
+// store before another lane's later LDS load, so every write phase of chan_dft_gemm is closed by
+// a wave-scope release fence + wave barrier + acquire fence (no workgroup barrier is needed: each
+// wave touches only its own sequences). Costs a few cycles per phase.
+__device__ __forceinline__ void wave_lds_handoff() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int L>
 __device__ __forceinline__ void chan_dft_gemm(float2* lds, const float2* twl, int tid, int mb, int m1, float2* __restrict__ out) {
     static_assert(L == 1024, "DFT-GEMM channelizer: 1024 = 32 x 32");
@@ -150,8 +160,9 @@ __device__ __forceinline__ void chan_dft_gemm(float2* lds, const float2* twl, in
                     ai[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, xb.x, ai[bi][bj], 0, 0, 0);
                 }
             }
-        // Z'[k1][b] = Z[k1][b] W_1024^(k1 b) (k1 b < 1024), written over X[k1][b]: this wave has
-        // read every element of its sequence above (LDS operations of a wave complete in order)
+        // Z'[k1][b] = Z[k1][b] W_1024^(k1 b) (k1 b < 1024), written over X[k1][b] once every lane
+        // of this wave has read its operands of X above
+        wave_lds_handoff();
 #pragma unroll
         for (int bi = 0; bi < 2; bi++)
 #pragma unroll
@@ -165,6 +176,7 @@ __device__ __forceinline__ void chan_dft_gemm(float2* lds, const float2* twl, in
         for (int x = 0; x < 2; x++)
 #pragma unroll
             for (int y = 0; y < 2; y++) ar[x][y] = ai[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+        wave_lds_handoff();   // Z' stored by other lanes, read below as A operands
         // Y = Z' F: A = Z' (rows k1 = 16 bi + i, k = b = 4 s + kk), B = F (columns k2 = 16 bj + i)
 #pragma unroll
         for (int s = 0; s < 8; s++) {
@@ -183,6 +195,7 @@ __device__ __forceinline__ void chan_dft_gemm(float2* lds, const float2* twl, in
                 }
         }
         // channel k = k1 + 32 k2 into the sequence (natural order), then one coalesced row store
+        wave_lds_handoff();   // every lane's Z' reads done before the sequence is overwritten
 #pragma unroll
         for (int bi = 0; bi < 2; bi++)
 #pragma unroll
@@ -192,12 +205,14 @@ __device__ __forceinline__ void chan_dft_gemm(float2* lds, const float2* twl, in
                     const int k1 = 16 * bi + 4 * kk + e, k2 = 16 * bj + i;
                     X[pad16(k1 + 32 * k2)] = make_float2(ar[bi][bj][e], ai[bi][bj][e]);
                 }
+        wave_lds_handoff();   // channel vector stored by other lanes, read for the row store
         const int m = mb + sF;
         if (m < m1) {
             float2* o = out + (long long)m * L;
 #pragma unroll
             for (int q = 0; q < L / 64; q++) o[lane + 64 * q] = X[pad16(lane + 64 * q)];
         }
+        wave_lds_handoff();   // row store's reads done before the next frame's sequence is used
     }
 }
 

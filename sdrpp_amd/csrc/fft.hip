@@ -864,6 +864,13 @@ extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long f
     SDRGPU_SET_DEVICE(p.device);
     hipStream_t s = stream ? (hipStream_t)stream : p.own;
     SDRGPU_CHECK(p.order.follow(s));
+    OrderScope od(p.order, s);
+    return fft_execute(h, in, frameStride, frames, out, nullptr, s);
+}
+
+int sdrgpu::fft_execute_owned(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, hipStream_t s) {
+    if (!h || !in || !out || frames < 0 || frameStride < 0) { set_error("fft_execute: bad argument"); return SDRGPU_EARG; }
+    if (frames == 0) return 0;
     return fft_execute(h, in, frameStride, frames, out, nullptr, s);
 }
 
@@ -882,6 +889,7 @@ extern "C" int sdrgpu_fft_execute_zoom_dev(sdrgpu_fft* h, const void* in, long l
     SDRGPU_SET_DEVICE(p.device);
     hipStream_t s = stream ? (hipStream_t)stream : p.own;
     SDRGPU_CHECK(p.order.follow(s));
+    OrderScope od(p.order, s);
     if (zoom_fusable(p, zoomSize)) return fft_execute(h, in, frameStride, frames, out, zoomOut, s);
     SDRGPU_CHECK(fft_execute(h, in, frameStride, frames, out, nullptr, s));
     if (!p.zoom || p.zoomSize != zoomSize) {
@@ -904,6 +912,12 @@ extern "C" int sdrgpu_fft_execute_vfo_dev(sdrgpu_fft* h, const void* in, int fra
     if (!h || !in || !out || !vfo || !vfoOut || frames < 0) { set_error("fft_execute_vfo: bad argument"); return SDRGPU_EARG; }
     const long long count = (long long)frames * h->p.N;
     if (count > 0x7fffffffLL) { set_error("fft_execute_vfo: %lld samples per call (max 2^31 - 1)", count); return SDRGPU_EARG; }
+    // back-to-back frames: the spectrum must cover every sample the VFO consumes, on one device
+    if (h->p.nz != h->p.N) { set_error("fft_execute_vfo: plan nz %d != N %d (frames must be back to back)", h->p.nz, h->p.N); return SDRGPU_EARG; }
+    if (vfo->impl && vfo->impl->device != h->p.device) {
+        set_error("fft_execute_vfo: VFO on device %d, spectrum plan on device %d", vfo->impl->device, h->p.device);
+        return SDRGPU_EARG;
+    }
     hipStream_t s = stream ? (hipStream_t)stream : h->p.own;
     SDRGPU_CHECK(sdrgpu_fft_execute_dev(h, in, h->p.N, frames, out, s));
     return sdrgpu_block_process_dev(vfo, in, (int)count, vfoOut, s);

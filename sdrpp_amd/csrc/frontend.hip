@@ -37,6 +37,20 @@ struct VfoSlot {
     DevBuf out;
     PinnedBuf pin;
     int n = 0;
+    PinnedBuf res[2];   // pipelined call style: this VFO's output of the block in result slot k
+    int resN[2] = {0, 0};
+};
+// One in-flight block of the pipelined host call style (sdrgpu_frontend_submit / collect).
+struct PipeSlot {
+    PinnedBuf stage;             // the host block, when the caller's buffer is not registered
+    DevBuf raw;                  // its device copy
+    PinnedBuf rows, iq;          // results: dB rows, preprocessed IQ
+    int nrows = 0, niq = 0;
+    long long ticket = -1;       // block in this slot (-1: free)
+    bool collected = true;
+    hipEvent_t h2d = nullptr;    // H2D done (staging reusable)
+    hipEvent_t consumed = nullptr;   // the block's kernels have read `raw`
+    hipEvent_t ready = nullptr;      // results are in the pinned buffers
 };
 const int kConvSize[] = {1, 2, 3, 4, 8, 1, 4};   // bytes per real value of SDRGPU_CONV_U8..F32
 }  // namespace
@@ -63,6 +77,10 @@ struct sdrgpu_frontend {
     int nextVfoId = 1;
     std::map<int, VfoSlot> vfos;
     long long stride() const { return (long long)nz + skip; }
+    // pipelined host call style: a copy stream for the H2D of block k + 1 while block k computes
+    hipStream_t cs = nullptr;
+    PipeSlot pipe[2];
+    long long nextTicket = 0;
 };
 
 static void destroy_parts(sdrgpu_frontend* f) {
@@ -130,9 +148,14 @@ extern "C" int sdrgpu_frontend_create(sdrgpu_frontend** out, int device, double 
 extern "C" int sdrgpu_frontend_destroy(sdrgpu_frontend* f) {
     if (!f) return SDRGPU_OK;
     (void)hipSetDevice(f->device);
+    if (f->cs) (void)hipStreamSynchronize(f->cs);
     if (f->s) (void)hipStreamSynchronize(f->s);
     for (auto& [id, v] : f->vfos) sdrgpu_block_destroy(v.vfo);
     destroy_parts(f);
+    for (auto& ps : f->pipe)
+        for (hipEvent_t e : {ps.h2d, ps.consumed, ps.ready})
+            if (e) (void)hipEventDestroy(e);
+    if (f->cs) (void)hipStreamDestroy(f->cs);
     if (f->s) (void)hipStreamDestroy(f->s);
     delete f;
     return SDRGPU_OK;
@@ -145,6 +168,7 @@ extern "C" int sdrgpu_frontend_configure(sdrgpu_frontend* f, double sampleRate, 
     NEED_FE(f);
     if (!(sampleRate > 0) || decimRatio < 1) { set_error("frontend_configure: bad argument"); return SDRGPU_EARG; }
     SDRGPU_SET_DEVICE(f->device);
+    if (f->cs) SDRGPU_HIP(hipStreamSynchronize(f->cs));
     SDRGPU_HIP(hipStreamSynchronize(f->s));
     f->sampleRate = sampleRate;
     f->decim = decimRatio;
@@ -242,7 +266,7 @@ static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s)
         const int want = sdrgpu_block_out_count(v.vfo, m);
         if (want < 0) return want;
         SDRGPU_CHECK(v.out.ensure(sizeof(float2) * (size_t)std::max(want, 1)));
-        const int n = m > 0 ? sdrgpu_block_process_dev(v.vfo, x, m, v.out.p, s) : 0;
+        const int n = m > 0 ? block_run_owned(v.vfo, x, m, v.out.p, s) : 0;
         if (n < 0) return n;
         v.n = n;
     }
@@ -291,12 +315,12 @@ static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s)
     }
     SDRGPU_CHECK(cs.launch(s));
     if (straddle) {
-        SDRGPU_CHECK(sdrgpu_fft_execute_dev(f->fft, f->stitch.p, f->nz, 1 + gathered, spec, s));
+        SDRGPU_CHECK(fft_execute_owned(f->fft, f->stitch.p, f->nz, 1 + gathered, spec, s));
         done = 1 + gathered;
     }
     if (nf > done) {   // frames entirely inside this block, read in place with the reshaper's stride
         const long long first = f->nextFrame + done * st - T;
-        SDRGPU_CHECK(sdrgpu_fft_execute_dev(f->fft, x + first, st, nf - done, spec + (size_t)done * f->fftSize, s));
+        SDRGPU_CHECK(fft_execute_owned(f->fft, x + first, st, nf - done, spec + (size_t)done * f->fftSize, s));
     }
     f->nSpec = nf;
     f->nextFrame = nextAfter;
@@ -314,7 +338,7 @@ static int fe_preproc(sdrgpu_frontend* f, const float2* in, int n, hipStream_t s
         const int want = sdrgpu_block_out_count(f->decimB, n);
         if (want < 0) return want;
         SDRGPU_CHECK(f->pre.ensure(sizeof(float2) * (size_t)std::max(want, 1)));
-        m = n > 0 ? sdrgpu_block_process_dev(f->decimB, x, n, f->pre.p, s) : 0;
+        m = n > 0 ? block_run_owned(f->decimB, x, n, f->pre.p, s) : 0;
         if (m < 0) return m;
         x = f->pre.as<float2>();
     }
@@ -324,7 +348,7 @@ static int fe_preproc(sdrgpu_frontend* f, const float2* in, int n, hipStream_t s
         x = f->pre.as<float2>();
     }
     if (f->dcb && m > 0) {
-        const int r = sdrgpu_block_process_dev(f->dcb, x, m, (void*)x, s);
+        const int r = block_run_owned(f->dcb, x, m, (void*)x, s);
         if (r < 0) return r;
     }
     if (f->invertIQ && m > 0) {
@@ -343,6 +367,7 @@ extern "C" int sdrgpu_frontend_push_dev(sdrgpu_frontend* f, const void* in, int 
     SDRGPU_SET_DEVICE(f->device);
     hipStream_t s = stream ? (hipStream_t)stream : f->s;
     SDRGPU_CHECK(f->order.follow(s));
+    OrderScope od(f->order, s);
     const float2* x = (const float2*)in;
     if (kind >= 0 && count > 0) {
         SDRGPU_CHECK(f->conv.ensure(sizeof(float2) * count));
@@ -423,4 +448,118 @@ extern "C" int sdrgpu_frontend_read_vfo(sdrgpu_frontend* f, int id, void* out, i
     SDRGPU_HIP(hipStreamSynchronize(f->s));
     SDRGPU_HIP(hipMemcpy(out, it->second.out.p, sizeof(float2) * (size_t)n, hipMemcpyDeviceToHost));
     return n;
+}
+
+// ---- pipelined host call style (the IQFrontEnd drop-in) ------------------------------------
+// submit(k): [stage the host block in pinned memory unless it is registered] -> H2D on the copy
+// stream into slot k % 2 -> (compute stream waits for it) push_dev -> D2H of the block's rows,
+// VFO outputs and, with SDRGPU_FE_IQ, preprocessed IQ into the slot's pinned results -> event.
+// Nothing waits for the device: block k + 1's H2D runs on the copy stream while block k's kernels
+// and read-back run on the compute stream, and the host hands block k - 1's results on meanwhile.
+// collect(k) waits for block k's results. Calls on one front end come from one thread at a time.
+static int pipe_slot_init(sdrgpu_frontend* f, PipeSlot& ps) {
+    if (!f->cs) SDRGPU_HIP(hipStreamCreateWithFlags(&f->cs, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&ps.h2d, &ps.consumed, &ps.ready})
+        if (!*e) SDRGPU_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return SDRGPU_OK;
+}
+
+extern "C" int sdrgpu_frontend_submit(sdrgpu_frontend* f, const void* in, int count, int kind, int flags) {
+    NEED_FE(f);
+    if (count < 0 || (count > 0 && !in) || kind < -1 || kind > SDRGPU_CONV_F32) { set_error("frontend_submit: bad argument"); return SDRGPU_EARG; }
+    SDRGPU_SET_DEVICE(f->device);
+    const long long t = f->nextTicket;
+    PipeSlot& ps = f->pipe[t & 1];
+    if (!ps.collected) { set_error("frontend_submit: ticket %lld not collected (at most 2 blocks in flight)", ps.ticket); return SDRGPU_ESTATE; }
+    SDRGPU_CHECK(pipe_slot_init(f, ps));
+    const size_t bytes = (size_t)count * (kind < 0 ? sizeof(float2) : 2 * kConvSize[kind]);
+    const void* raw = nullptr;
+    if (count > 0) {
+        SDRGPU_CHECK(ps.raw.ensure(bytes));
+        // the slot's last H2D finished (its staging is reusable), and its last block's kernels
+        // have read `raw` (copy stream waits: device side)
+        const void* src = in;
+        if (!host_pinned(in, bytes)) {
+            SDRGPU_HIP(hipEventSynchronize(ps.h2d));
+            SDRGPU_CHECK(ps.stage.ensure(bytes));
+            std::memcpy(ps.stage.p, in, bytes);
+            src = ps.stage.p;
+        }
+        SDRGPU_HIP(hipStreamWaitEvent(f->cs, ps.consumed, 0));
+        SDRGPU_HIP(hipMemcpyAsync(ps.raw.p, src, bytes, hipMemcpyHostToDevice, f->cs));
+        SDRGPU_HIP(hipEventRecord(ps.h2d, f->cs));
+        SDRGPU_HIP(hipStreamWaitEvent(f->s, ps.h2d, 0));
+        raw = ps.raw.p;
+    }
+    const int nf = sdrgpu_frontend_push_dev(f, raw, count, kind, f->s);
+    if (nf < 0) return nf;
+    SDRGPU_HIP(hipEventRecord(ps.consumed, f->s));
+    // read-back into the slot's pinned results (sizes are host-side state of this push)
+    ps.nrows = nf;
+    if (nf > 0) {
+        const size_t rb = sizeof(float) * (size_t)nf * f->fftSize;
+        SDRGPU_CHECK(ps.rows.ensure(rb));
+        SDRGPU_HIP(hipMemcpyAsync(ps.rows.p, f->spectra.p, rb, hipMemcpyDeviceToHost, f->s));
+    }
+    for (auto& [id, v] : f->vfos) {
+        const int k = (int)(t & 1);
+        v.resN[k] = v.n;
+        if (v.n > 0) {
+            SDRGPU_CHECK(v.res[k].ensure(sizeof(float2) * (size_t)v.n));
+            SDRGPU_HIP(hipMemcpyAsync(v.res[k].p, v.out.p, sizeof(float2) * (size_t)v.n, hipMemcpyDeviceToHost, f->s));
+        }
+    }
+    ps.niq = 0;
+    if ((flags & SDRGPU_FE_IQ) && f->lastIQn > 0 && f->lastIQ) {
+        ps.niq = f->lastIQn;
+        SDRGPU_CHECK(ps.iq.ensure(sizeof(float2) * (size_t)ps.niq));
+        SDRGPU_HIP(hipMemcpyAsync(ps.iq.p, f->lastIQ, sizeof(float2) * (size_t)ps.niq, hipMemcpyDeviceToHost, f->s));
+    }
+    SDRGPU_HIP(hipEventRecord(ps.ready, f->s));
+    ps.ticket = t;
+    ps.collected = false;
+    f->nextTicket = t + 1;
+    return (int)(t & 0x7fffffff);
+}
+
+static PipeSlot* pipe_find(sdrgpu_frontend* f, int ticket) {
+    PipeSlot& ps = f->pipe[ticket & 1];
+    if (ps.ticket < 0 || (int)(ps.ticket & 0x7fffffff) != ticket) {
+        set_error("frontend: ticket %d is not in flight", ticket);
+        return nullptr;
+    }
+    return &ps;
+}
+
+extern "C" int sdrgpu_frontend_collect(sdrgpu_frontend* f, int ticket, const float** rows, const void** iq, int* niq) {
+    NEED_FE(f);
+    PipeSlot* ps = pipe_find(f, ticket);
+    if (!ps) return SDRGPU_EARG;
+    SDRGPU_SET_DEVICE(f->device);
+    SDRGPU_HIP(hipEventSynchronize(ps->ready));
+    if (rows) *rows = ps->nrows > 0 ? ps->rows.as_const<float>() : nullptr;
+    if (iq) *iq = ps->niq > 0 ? ps->iq.p : nullptr;
+    if (niq) *niq = ps->niq;
+    return ps->nrows;
+}
+
+extern "C" int sdrgpu_frontend_collected_vfo(sdrgpu_frontend* f, int ticket, int id, const void** out, int* n) {
+    NEED_FE(f);
+    PipeSlot* ps = pipe_find(f, ticket);
+    if (!ps) return SDRGPU_EARG;
+    auto it = f->vfos.find(id);
+    if (it == f->vfos.end()) { set_error("frontend: no VFO %d", id); return SDRGPU_EARG; }
+    const int k = ticket & 1;
+    if (out) *out = it->second.resN[k] > 0 ? it->second.res[k].p : nullptr;
+    if (n) *n = it->second.resN[k];
+    return it->second.resN[k];
+}
+
+// the host is done with the ticket's results: its slot may take a new block
+extern "C" int sdrgpu_frontend_release(sdrgpu_frontend* f, int ticket) {
+    NEED_FE(f);
+    PipeSlot* ps = pipe_find(f, ticket);
+    if (!ps) return SDRGPU_EARG;
+    ps->collected = true;
+    return SDRGPU_OK;
 }

@@ -13,6 +13,7 @@
 // there (rank 0's own rows are a device copy), on the caller's stream: asynchronous, ordered
 // after the producer of the rows on that stream.
 #include <dlfcn.h>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <rccl/rccl.h>
@@ -36,6 +37,7 @@ struct Rccl {
 const Rccl* rccl() {
     static Rccl r;
     static std::once_flag once;
+    static char why[256] = "missing symbols";
     std::call_once(once, [] {
         // an RCCL already in the process first (RTLD_NOLOAD), then the ROCm one
         const char* names[] = {"librccl.so", "librccl.so.1"};
@@ -43,7 +45,12 @@ const Rccl* rccl() {
             if (!r.lib) r.lib = dlopen(n, RTLD_NOW | RTLD_NOLOAD | RTLD_GLOBAL);
         for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
             if (!r.lib) r.lib = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
-        if (!r.lib) return;
+        if (!r.lib) {
+            // dlerror() clears the error state on every call: read it once
+            const char* e = dlerror();
+            std::snprintf(why, sizeof(why), "%s", e ? e : "dlopen failed");
+            return;
+        }
         r.getUniqueId = (decltype(r.getUniqueId))dlsym(r.lib, "ncclGetUniqueId");
         r.commInitRank = (decltype(r.commInitRank))dlsym(r.lib, "ncclCommInitRank");
         r.commDestroy = (decltype(r.commDestroy))dlsym(r.lib, "ncclCommDestroy");
@@ -55,7 +62,7 @@ const Rccl* rccl() {
     });
     if (!r.lib || !r.getUniqueId || !r.commInitRank || !r.commDestroy || !r.send || !r.recv || !r.groupStart ||
         !r.groupEnd || !r.errorString) {
-        set_error("gather: RCCL (librccl.so) not available: %s", dlerror() ? dlerror() : "missing symbols");
+        set_error("gather: RCCL (librccl.so) not available: %s", why);
         return nullptr;
     }
     return &r;
@@ -69,6 +76,25 @@ const Rccl* rccl() {
             return SDRGPU_EHIP;                                                              \
         }                                                                                    \
     } while (0)
+// closes an RCCL group on every exit path (an error inside the group must not leave the thread's
+// group open for later RCCL calls)
+struct GroupGuard {
+    const Rccl* R;
+    bool open = false;
+    explicit GroupGuard(const Rccl* r) : R(r) {}
+    ncclResult_t start() {
+        const ncclResult_t e = R->groupStart();
+        open = e == ncclSuccess;
+        return e;
+    }
+    ncclResult_t end() {
+        open = false;
+        return R->groupEnd();
+    }
+    ~GroupGuard() {
+        if (open) (void)R->groupEnd();
+    }
+};
 }  // namespace
 
 struct sdrgpu_gather {
@@ -118,22 +144,23 @@ extern "C" int sdrgpu_gather_rows(sdrgpu_gather* g, const float* rows, long long
     if (!R) return SDRGPU_ESTATE;
     SDRGPU_SET_DEVICE(g->device);
     hipStream_t s = (hipStream_t)stream;
+    GroupGuard grp(R);
     if (g->world == 1) {   // one stream: a send/recv to itself (exercises the communicator like world > 1)
-        RCCL_CALL(R, R->groupStart());
+        RCCL_CALL(R, grp.start());
         RCCL_CALL(R, R->send(rows, (size_t)count, ncclFloat32, 0, g->comm, s));
         RCCL_CALL(R, R->recv(out, (size_t)count, ncclFloat32, 0, g->comm, s));
-        RCCL_CALL(R, R->groupEnd());
+        RCCL_CALL(R, grp.end());
         return SDRGPU_OK;
     }
     if (g->rank == 0) SDRGPU_HIP(hipMemcpyAsync(out, rows, sizeof(float) * count, hipMemcpyDeviceToDevice, s));
-    RCCL_CALL(R, R->groupStart());
+    RCCL_CALL(R, grp.start());
     if (g->rank == 0) {
         for (int r = 1; r < g->world; r++)
             RCCL_CALL(R, R->recv(out + (size_t)r * count, (size_t)count, ncclFloat32, r, g->comm, s));
     } else {
         RCCL_CALL(R, R->send(rows, (size_t)count, ncclFloat32, 0, g->comm, s));
     }
-    RCCL_CALL(R, R->groupEnd());
+    RCCL_CALL(R, grp.end());
     return SDRGPU_OK;
 }
 

@@ -62,19 +62,33 @@ struct PinnedBuf {
     size_t bytes = 0;
     int ensure(size_t want);
     ~PinnedBuf();
+    template <typename T> const T* as_const() const { return reinterpret_cast<const T*>(p); }
 };
 
 inline size_t esize(int dtype) { return dtype == SDRGPU_C64 ? 8 : 4; }
 
 // A handle's device state is rewritten by every call (NCO coarse table, history / quadrature
 // ping-pong buffers, FFT scratch), so calls must not overlap. Calls on one stream are ordered by
-// the stream; a call on another stream than the previous one first makes its stream wait for
-// the previous call's work (one event, recorded only on a stream change).
+// the stream. Every public entry point records `ev` on its own stream when it has enqueued its
+// work (done); a call on another stream first makes its stream wait for that event (follow). The
+// event therefore always belongs to a stream that was live when it was recorded (a caller may
+// destroy a stream after its call), and the new stream waits for exactly the previous call's
+// work. Handles driven only through another handle (a front end's VFOs and FFT plan) skip this:
+// the owner orders them.
 struct StreamOrder {
-    hipStream_t last = nullptr;
-    hipEvent_t ev = nullptr;
+    hipStream_t last = nullptr;   // stream of the previous call
+    hipEvent_t ev = nullptr;      // recorded on `last` at the end of the previous call
+    bool recorded = false;
     int follow(hipStream_t s);
+    int done(hipStream_t s);
     ~StreamOrder();
+};
+// follow() at the start of an entry point, done() when the scope ends
+struct OrderScope {
+    StreamOrder& o;
+    hipStream_t s;
+    OrderScope(StreamOrder& o_, hipStream_t s_) : o(o_), s(s_) {}
+    ~OrderScope() { (void)o.done(s); }
 };
 
 // ---- host-side design (host_design.cpp) -----------------------------------
@@ -123,3 +137,10 @@ struct FirState;   // defined in fir.hip
 struct sdrgpu_block {
     sdrgpu::Block* impl;
 };
+struct sdrgpu_fft;
+
+namespace sdrgpu {
+// entry points without the cross-stream ordering, for a handle owned by another handle
+int block_run_owned(sdrgpu_block* h, const void* in, int count, void* out, hipStream_t s);
+int fft_execute_owned(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, hipStream_t s);
+}  // namespace sdrgpu

@@ -472,6 +472,39 @@ class IQFrontEnd:
     def push_dev(self, ptr, count, kind=-1, stream=None):
         return check(lib.sdrgpu_frontend_push_dev(self._h, _vp(ptr), int(count), int(kind), _vp(stream or 0)))
 
+    # pipelined host call style (the C++ drop-in's worker): submit returns a ticket at once; collect
+    # waits for it and copies its results out of the pinned result slot; at most two in flight
+    def submit(self, block, kind=-1, want_iq=False, ptr=None, count=None):
+        """Host block (numpy array, or `ptr`/`count` of host memory) -> ticket."""
+        if ptr is None:
+            a = np.ascontiguousarray(block)
+            ptr, count = a.ctypes.data, (a.shape[0] if kind < 0 else a.size // 2)
+        return check(lib.sdrgpu_frontend_submit(self._h, _vp(ptr), int(count), int(kind), 1 if want_iq else 0))
+
+    def collect(self, ticket, vfos=(), copy=True):
+        """(rows [nrows, N] float32, {vid: complex64 output}, iq complex64 or None) of a ticket; the
+        ticket is released afterwards. copy=False only waits and releases (timing)."""
+        rows_p, iq_p, niq = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int()
+        nf = check(lib.sdrgpu_frontend_collect(self._h, int(ticket), ctypes.byref(rows_p), ctypes.byref(iq_p),
+                                               ctypes.byref(niq)))
+        rows, outs, iq = None, {}, None
+        if copy:
+            rows = np.empty((nf, self.fft_size), np.float32)
+            if nf:
+                ctypes.memmove(rows.ctypes.data, rows_p.value, rows.nbytes)
+            for vid in vfos:
+                p, n = ctypes.c_void_p(), ctypes.c_int()
+                check(lib.sdrgpu_frontend_collected_vfo(self._h, int(ticket), int(vid), ctypes.byref(p), ctypes.byref(n)))
+                o = np.empty(n.value, np.complex64)
+                if n.value:
+                    ctypes.memmove(o.ctypes.data, p.value, o.nbytes)
+                outs[vid] = o
+            if niq.value:
+                iq = np.empty(niq.value, np.complex64)
+                ctypes.memmove(iq.ctypes.data, iq_p.value, iq.nbytes)
+        check(lib.sdrgpu_frontend_release(self._h, int(ticket)))
+        return rows, outs, iq
+
     def vfo_dev(self, vid):
         """(device pointer, count) of the VFO's output for the last push."""
         ptr, n = ctypes.c_void_p(), ctypes.c_int()

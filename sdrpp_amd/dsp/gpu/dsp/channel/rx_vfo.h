@@ -24,25 +24,25 @@ public:
     }
     void setInSamplerate(double inSamplerate) {
         std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx);
-        base_type::tempStop();
+        pause();
         _inSamplerate = inSamplerate;
         rebuild();
-        base_type::tempStart();
+        resume();
     }
     void setOutSamplerate(double outSamplerate, double bandwidth) {
         std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx);
-        base_type::tempStop();
+        pause();
         _outSamplerate = outSamplerate;
         _bandwidth = bandwidth;
         rebuild();
-        base_type::tempStart();
+        resume();
     }
     void setBandwidth(double bandwidth) {
         std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx);
-        base_type::tempStop();
+        pause();
         _bandwidth = bandwidth;
         rebuild();
-        base_type::tempStart();
+        resume();
     }
     // keeps the running NCO phase (frequency_xlator.h:25-29); latched at the next process()
     void setOffset(double offset) {
@@ -59,11 +59,12 @@ public:
     // the front end runs this VFO on the block it already holds on the device and writes `out`
     // (this block's own worker does nothing); the setters re-plan it there, under the front
     // end's lock. `in` is an idle placeholder input (the block API needs one).
-    void attach(stream<complex_t>* in, sdrgpu_frontend* fe, int id, std::mutex* feMtx, double inSamplerate,
+    void attach(stream<complex_t>* in, sdrgpu_frontend* fe, int id, std::mutex* feMtx, block* feWorker, double inSamplerate,
                 double outSamplerate, double bandwidth, double offset) {
         _fe = fe;
         _feId = id;
         _feMtx = feMtx;
+        _feWorker = feWorker;
         _inSamplerate = inSamplerate;
         _outSamplerate = outSamplerate;
         _bandwidth = bandwidth;
@@ -73,19 +74,19 @@ public:
     int frontEndId() const { return _feId; }
     void reset() {
         std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx);
-        base_type::tempStop();
+        pause();
         if (_fe) rebuild();
         else gpu::ok(sdrgpu_block_reset(_h.h), "rxvfo_reset");
-        base_type::tempStart();
+        resume();
     }
     // GPU placement (sdrgpu_handle.h): this VFO's device; setDevice moves it (state restarts)
     int getDevice() const { return _h.dev; }
     void setDevice(int device) {
         std::lock_guard<std::recursive_mutex> lck(base_type::ctrlMtx);
-        base_type::tempStop();
+        pause();
         _h.dev = device;
         rebuild();
-        base_type::tempStart();
+        resume();
     }
     inline int process(int count, const complex_t* in, complex_t* out) { return _h.process(in, count, out, "rxvfo"); }
     int run() override {
@@ -100,6 +101,18 @@ public:
     }
 
 protected:
+    // Park the producer of `out` around a re-plan. Standalone, that is this block's own worker
+    // (block.h tempStop). Attached, the front end's worker writes `out`: it is parked instead, and
+    // this block's own streams are left alone -- stopping `out`'s writer here would make the
+    // front end's next swap() fail and end its worker for good.
+    void pause() {
+        if (_fe && _feWorker) _feWorker->tempStop();
+        else if (!_fe) base_type::tempStop();
+    }
+    void resume() {
+        if (_fe && _feWorker) _feWorker->tempStart();
+        else if (!_fe) base_type::tempStart();
+    }
     void rebuild() {
         if (_fe) {   // attached: the front end's VFO is re-planned (its filter state restarts)
             std::lock_guard<std::mutex> fl(*_feMtx);
@@ -118,5 +131,6 @@ protected:
     sdrgpu_frontend* _fe = nullptr;   // attached mode
     int _feId = -1;
     std::mutex* _feMtx = nullptr;
+    block* _feWorker = nullptr;   // attached: the front end's worker (writes `out`)
 };
 }  // namespace dsp::channel

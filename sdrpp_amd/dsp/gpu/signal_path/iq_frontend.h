@@ -1,25 +1,40 @@
 // GPU-backed IQFrontEnd -- drop-in for core/src/signal_path/iq_frontend.{h,cpp}: the same class
-// name and public interface (init, setSampleRate, setDecimation, setInvertIQ, setDCBlocking,
-// bindIQStream, addVFO / removeVFO, setFFTSize / Rate / Window, start / stop, ...), header-only.
+// name and public interface (init, setSampleRate, setBuffering, setDecimation, setInvertIQ,
+// setDCBlocking, bindIQStream, addVFO / removeVFO, setFFTSize / Rate / Window, flushInputBuffer,
+// start / stop, ...), header-only.
 //
 // The whole data path runs in libsdrgpu's device front end (sdrgpu_frontend_*, include/sdrgpu.h):
 // one H2D per input block, then on the device the preprocessing (PowerDecimator, DCBlocker,
 // Conjugate), the reshaper's keep / skip framing (genReshapeParams, iq_frontend.h:56-60),
 // window * FFT * log-power (iq_frontend.cpp:230-249), and every VFO reading the block in place
 // (addVFO, :122-142) -- instead of the SampleFrameBuffer -> Splitter -> Reshaper memcpy fan-out.
-// One worker thread (a dsp::block) moves each block of the input stream to the device and hands
-// back, in order:
-//   * each dB row through acquire / releaseFFTBuffer (a NULL buffer skips the copy but release
-//     is still called, as in handler);
-//   * each VFO's output into that VFO's `out` stream (the VFO is an RxVFO attached to the front
-//     end: its own worker is idle, its setters re-plan it on the device);
-//   * the preprocessed IQ into every bound stream (bindIQStream: the recorder, IQ exporters).
-// Buffering (SampleFrameBuffer) is not needed: blocks are consumed as they come, losslessly.
+//
+// Two threads, as the reference's SampleFrameBuffer has (buffer/frame_buffer.h:52-94):
+//   * the input buffer (InputRing, "dspBuf:loop") copies each block of the input stream into a
+//     slot of a 32-slot ring of pinned host buffers. With buffering on (the reference's default,
+//     gui/main_window.cpp:89) it never blocks the source: when every slot is taken, the oldest
+//     queued block is dropped (the reference overwrites slots, frame_buffer.h:64-71; its ring
+//     then also looks empty for a whole lap, which drops 32 blocks at once -- here exactly the
+//     oldest one goes). With buffering off (bypass) the source waits for a free slot;
+//   * the device worker (Worker, a dsp::block) takes queued slots and submits them to the device
+//     front end without waiting (sdrgpu_frontend_submit: the slot is DMA'd straight to the GPU);
+//     while blocks are queued it submits block k + 1 before it collects block k, so the H2D of one
+//     block overlaps the kernels and read-back of the previous one and the host hand-off of the
+//     results. The results of a block go out, in order:
+//       - each dB row through acquire / releaseFFTBuffer (a NULL buffer skips the copy but release
+//         is still called, as in handler);
+//       - each VFO's output into that VFO's `out` stream (the VFO is an RxVFO attached to the
+//         front end: its own worker is idle, its setters re-plan it on the device and pause this
+//         worker instead of stopping the VFO's own streams);
+//       - the preprocessed IQ into every bound stream (bindIQStream: the recorder, IQ exporters).
 // Inside the SDR++ tree (core.h present) it keeps the reference's couplings:
 // core::setInputSampleRate on a rate change and gui::waterfall.setRawFFTSize on an FFT change.
 #pragma once
+#include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <string>
@@ -44,6 +59,8 @@
 
 class IQFrontEnd {
 public:
+    static constexpr int RING_SLOTS = 32;   // TEST_BUFFER_SIZE (frame_buffer.h:3)
+
     ~IQFrontEnd() {
         if (!_init) return;
         stop();
@@ -68,13 +85,16 @@ public:
         _acquireFFTBuffer = acquireFFTBuffer;
         _releaseFFTBuffer = releaseFFTBuffer;
         _fftCtx = fftCtx;
-        (void)buffering;
         dsp::gpu::ok(sdrgpu_frontend_create(&_fe, dsp::gpu::device(), sampleRate, decimRatio, dcBlocking, fftSize, fftRate,
                                             (int)fftWindow),
                      "frontend_create");
         refreshFraming();
+        _ring.lossy = buffering;
+        _inBuf.ring = &_ring;
+        _inBuf.setInput(in);
         _worker.fe = this;
-        _worker.setInput(in);
+        _worker.ring = &_ring;
+        _worker.init();
         _init = true;
     }
 
@@ -85,7 +105,7 @@ public:
         refreshFraming();
     }
 
-    void setInput(dsp::stream<dsp::complex_t>* in) { _worker.setInput(in); }
+    void setInput(dsp::stream<dsp::complex_t>* in) { _inBuf.setInput(in); }
     void setSampleRate(double sampleRate) {
         _worker.tempStop();
         {
@@ -100,7 +120,8 @@ public:
     }
     inline double getSampleRate() { return _sampleRate / _decimRatio; }
 
-    void setBuffering(bool enabled) { (void)enabled; }   // blocks are consumed losslessly
+    // SampleFrameBuffer bypass = !enabled (iq_frontend.cpp:27-28)
+    void setBuffering(bool enabled) { _ring.setLossy(enabled); }
     void setDecimation(int ratio) {
         _decimRatio = ratio;
         setSampleRate(_sampleRate);
@@ -146,7 +167,7 @@ public:
         }
         auto* in = new dsp::stream<dsp::complex_t>;
         auto* vfo = new dsp::channel::RxVFO();
-        vfo->attach(in, _fe, id, &_mtx, effectiveSr, sampleRate, bandwidth, offset);
+        vfo->attach(in, _fe, id, &_mtx, &_worker, effectiveSr, sampleRate, bandwidth, offset);
         vfos[name] = {vfo, in};
         _worker.addOutput(&vfo->out);
         _worker.tempStart();
@@ -193,13 +214,22 @@ public:
         _worker.tempStart();
     }
 
-    void flushInputBuffer() {}   // no input buffer to flush
-    void start() { _worker.start(); }
-    void stop() { _worker.stop(); }
+    // SampleFrameBuffer::flush (frame_buffer.h:46-49): drop every queued block
+    void flushInputBuffer() { _ring.flush(); }
+    void start() {
+        _worker.start();
+        _inBuf.start();
+    }
+    void stop() {
+        _inBuf.stop();
+        _worker.stop();
+    }
     double getEffectiveSamplerate() { return effectiveSr; }
 
     // (not in the reference) the device front end under this object, for sdrgpu_frontend_* calls
     sdrgpu_frontend* device_frontend() { return _fe; }
+    // (not in the reference) input blocks dropped by the lossy ring since init
+    long long droppedBlocks() { return _ring.droppedCount(); }
 
 protected:
     struct Vfo {
@@ -207,10 +237,122 @@ protected:
         dsp::stream<dsp::complex_t>* in;   // idle placeholder input of the attached VFO
     };
 
-    // the worker: one input block per run()
-    class Worker : public dsp::block {
+    // 32 pinned block slots: free -> queued (FIFO) -> in flight on the device -> free
+    class InputRing {
     public:
-        IQFrontEnd* fe = nullptr;
+        bool lossy = true;
+        ~InputRing() {
+            for (auto& s : slots)
+                if (s.buf) sdrgpu_host_free(s.buf);
+        }
+        void setLossy(bool l) {
+            std::lock_guard<std::mutex> lk(mtx);
+            lossy = l;
+            cv.notify_all();
+        }
+        // writer (input thread): one block; false when stopped
+        bool push(const dsp::complex_t* data, int count) {
+            std::unique_lock<std::mutex> lk(mtx);
+            int idx = -1;
+            for (;;) {
+                if (wstop) return false;
+                if (!freeList.empty()) {
+                    idx = freeList.back();
+                    freeList.pop_back();
+                    break;
+                }
+                if (lossy && !queue.empty()) {   // drop the oldest queued block
+                    idx = queue.front();
+                    queue.pop_front();
+                    dropped++;
+                    break;
+                }
+                cv.wait(lk);   // bypass (or every slot in flight): wait for the device worker
+            }
+            Slot& s = slots[idx];
+            if (s.cap < count) {
+                if (s.buf) sdrgpu_host_free(s.buf);
+                s.buf = nullptr;
+                s.cap = 0;
+                void* p = nullptr;
+                const int cap = std::max(count, 1 << 16);
+                if (!dsp::gpu::ok(sdrgpu_host_alloc(&p, sizeof(dsp::complex_t) * (size_t)cap), "host_alloc")) {
+                    freeList.push_back(idx);
+                    return false;
+                }
+                s.buf = (dsp::complex_t*)p;
+                s.cap = cap;
+            }
+            // the copy runs under the lock: flush() / the worker never see a half-written slot
+            std::memcpy(s.buf, data, sizeof(dsp::complex_t) * (size_t)count);
+            s.count = count;
+            queue.push_back(idx);
+            cv.notify_all();
+            return true;
+        }
+        // device worker: next queued slot (wait = block until one arrives); -1 when stopped / none
+        int pop(bool wait) {
+            std::unique_lock<std::mutex> lk(mtx);
+            if (wait) cv.wait(lk, [this] { return !queue.empty() || rstop; });
+            if (rstop || queue.empty()) return -1;
+            const int idx = queue.front();
+            queue.pop_front();
+            return idx;
+        }
+        bool empty() {
+            std::lock_guard<std::mutex> lk(mtx);
+            return queue.empty();
+        }
+        void release(int idx) {
+            std::lock_guard<std::mutex> lk(mtx);
+            freeList.push_back(idx);
+            cv.notify_all();
+        }
+        void flush() {
+            std::lock_guard<std::mutex> lk(mtx);
+            for (int i : queue) freeList.push_back(i);
+            queue.clear();
+            cv.notify_all();
+        }
+        void stopWriter(bool v) {
+            std::lock_guard<std::mutex> lk(mtx);
+            wstop = v;
+            cv.notify_all();
+        }
+        void stopReader(bool v) {
+            std::lock_guard<std::mutex> lk(mtx);
+            rstop = v;
+            cv.notify_all();
+        }
+        long long droppedCount() {
+            std::lock_guard<std::mutex> lk(mtx);
+            return dropped;
+        }
+        const dsp::complex_t* data(int idx) const { return slots[idx].buf; }
+        int count(int idx) const { return slots[idx].count; }
+
+    private:
+        struct Slot {
+            dsp::complex_t* buf = nullptr;
+            int cap = 0, count = 0;
+        };
+        Slot slots[RING_SLOTS];
+        std::vector<int> freeList = [] {
+            std::vector<int> v;
+            for (int i = RING_SLOTS - 1; i >= 0; i--) v.push_back(i);
+            return v;
+        }();
+        std::deque<int> queue;
+        std::mutex mtx;
+        std::condition_variable cv;
+        bool wstop = false, rstop = false;
+        long long dropped = 0;
+    };
+
+    // input stream -> ring (SampleFrameBuffer::run, frame_buffer.h:52-75)
+    class InputBuffer : public dsp::block {
+    public:
+        InputRing* ring = nullptr;
         void setInput(dsp::stream<dsp::complex_t>* in) {
             std::lock_guard<std::recursive_mutex> lk(ctrlMtx);
             tempStop();
@@ -220,6 +362,29 @@ protected:
             _block_init = true;
             tempStart();
         }
+        int run() override {
+            const int count = _in->read();
+            if (count < 0) return -1;
+            const bool ok = ring->push(_in->readBuf, count);
+            _in->flush();
+            return ok ? count : -1;
+        }
+
+    protected:
+        void doStop() override {
+            ring->stopWriter(true);
+            dsp::block::doStop();
+            ring->stopWriter(false);
+        }
+        dsp::stream<dsp::complex_t>* _in = nullptr;
+    };
+
+    // ring -> device front end -> rows / VFO outputs / bound IQ streams
+    class Worker : public dsp::block {
+    public:
+        IQFrontEnd* fe = nullptr;
+        InputRing* ring = nullptr;
+        void init() { _block_init = true; }
         void addOutput(dsp::stream<dsp::complex_t>* s) { registerOutput(s); }
         void removeOutput(dsp::stream<dsp::complex_t>* s) { unregisterOutput(s); }
         void bind(dsp::stream<dsp::complex_t>* s) {
@@ -230,45 +395,96 @@ protected:
             bound.erase(std::remove(bound.begin(), bound.end(), s), bound.end());
             unregisterOutput(s);
         }
-        int run() override { return fe->iteration(_in, bound); }
-        dsp::stream<dsp::complex_t>* _in = nullptr;
+        int run() override { return fe->iteration(*this); }
         std::vector<dsp::stream<dsp::complex_t>*> bound;
+        // the block submitted but not yet handed on (ticket, ring slot)
+        int pendingTicket = -1, pendingSlot = -1;
+
+    protected:
+        void doStop() override {
+            ring->stopReader(true);
+            dsp::block::doStop();
+            ring->stopReader(false);
+            fe->dropPending(*this);   // a block in flight when the worker parks is dropped
+        }
     };
 
-    // one block: push it to the device, then hand back rows, VFO outputs and preprocessed IQ
-    int iteration(dsp::stream<dsp::complex_t>* in, const std::vector<dsp::stream<dsp::complex_t>*>& bound) {
-        const int count = in->read();
-        if (count < 0) return -1;
-        int nf = 0, niq = 0;
-        std::vector<std::pair<dsp::channel::RxVFO*, int>> outs;
+    // one worker step: submit the next block, hand on the previous one's results
+    int iteration(Worker& w) {
+        // nothing queued: hand on the block in flight first (no extra latency when keeping up)
+        if (w.pendingTicket >= 0 && _ring.empty()) {
+            if (!deliver(w, w.pendingTicket, w.pendingSlot)) return -1;
+            w.pendingTicket = w.pendingSlot = -1;
+        }
+        const int slot = _ring.pop(true);
+        if (slot < 0) return -1;
+        int ticket;
         {
             std::lock_guard<std::mutex> l(_mtx);
-            nf = sdrgpu_frontend_push(_fe, in->readBuf, count, -1);
-            in->flush();
-            if (!dsp::gpu::ok(nf, "frontend_push")) return -1;
-            if (nf > 0) {
-                _rows.resize((size_t)nf * _fftSize);
-                sdrgpu_frontend_read_spectra(_fe, _rows.data(), nf);
-            }
-            for (auto& [name, v] : vfos) {
-                const int n = sdrgpu_frontend_read_vfo(_fe, v.vfo->frontEndId(), v.vfo->out.writeBuf, STREAM_BUFFER_SIZE);
-                if (!dsp::gpu::ok(n, "frontend_read_vfo")) return -1;
-                outs.emplace_back(v.vfo, n);
-            }
-            if (!bound.empty()) niq = sdrgpu_frontend_read_iq(_fe, bound[0]->writeBuf, STREAM_BUFFER_SIZE);
+            ticket = sdrgpu_frontend_submit(_fe, _ring.data(slot), _ring.count(slot), -1, w.bound.empty() ? 0 : SDRGPU_FE_IQ);
         }
-        for (int r = 0; r < nf; r++) {   // IQFrontEnd::handler's acquire -> write -> release per row
+        if (!dsp::gpu::ok(ticket, "frontend_submit")) {
+            _ring.release(slot);
+            return -1;
+        }
+        if (w.pendingTicket >= 0 && !deliver(w, w.pendingTicket, w.pendingSlot)) {
+            w.pendingTicket = w.pendingSlot = -1;
+            dropTicket(ticket, slot);
+            return -1;
+        }
+        w.pendingTicket = ticket;
+        w.pendingSlot = slot;
+        return _ring.count(slot);
+    }
+
+    // collect a block's results and hand them on; false when an output stream was stopped
+    bool deliver(Worker& w, int ticket, int slot) {
+        const float* rows = nullptr;
+        const void* iq = nullptr;
+        int niq = 0, nf;
+        std::vector<std::pair<dsp::channel::RxVFO*, std::pair<const void*, int>>> outs;
+        {
+            std::lock_guard<std::mutex> l(_mtx);
+            nf = sdrgpu_frontend_collect(_fe, ticket, &rows, &iq, &niq);
+            for (auto& [name, v] : vfos) {
+                const void* p = nullptr;
+                int n = 0;
+                if (sdrgpu_frontend_collected_vfo(_fe, ticket, v.vfo->frontEndId(), &p, &n) >= 0) outs.push_back({v.vfo, {p, n}});
+            }
+        }
+        _ring.release(slot);   // the block's H2D is done
+        bool ok = dsp::gpu::ok(nf, "frontend_collect");
+        for (int r = 0; ok && r < nf; r++) {   // IQFrontEnd::handler's acquire -> write -> release per row
             float* buf = _acquireFFTBuffer(_fftCtx);
-            if (buf) std::memcpy(buf, _rows.data() + (size_t)r * _fftSize, sizeof(float) * _fftSize);
+            if (buf) std::memcpy(buf, rows + (size_t)r * _fftSize, sizeof(float) * _fftSize);
             _releaseFFTBuffer(_fftCtx);
         }
-        for (auto& [vfo, n] : outs)
-            if (n > 0 && !vfo->out.swap(n)) return -1;
-        for (size_t k = 0; k < bound.size() && niq > 0; k++) {
-            if (k > 0) std::memcpy(bound[k]->writeBuf, bound[0]->writeBuf, sizeof(dsp::complex_t) * niq);
-            if (!bound[k]->swap(niq)) return -1;
+        for (auto& [vfo, pn] : outs) {
+            if (!ok || pn.second <= 0) continue;
+            std::memcpy(vfo->out.writeBuf, pn.first, sizeof(dsp::complex_t) * (size_t)pn.second);
+            ok = vfo->out.swap(pn.second);
         }
-        return count;
+        for (size_t k = 0; ok && k < w.bound.size() && niq > 0; k++) {
+            std::memcpy(w.bound[k]->writeBuf, iq, sizeof(dsp::complex_t) * (size_t)niq);
+            ok = w.bound[k]->swap(niq);
+        }
+        std::lock_guard<std::mutex> l(_mtx);
+        sdrgpu_frontend_release(_fe, ticket);
+        return ok;
+    }
+
+    void dropTicket(int ticket, int slot) {
+        {
+            std::lock_guard<std::mutex> l(_mtx);
+            sdrgpu_frontend_collect(_fe, ticket, nullptr, nullptr, nullptr);
+            sdrgpu_frontend_release(_fe, ticket);
+        }
+        _ring.release(slot);
+    }
+    void dropPending(Worker& w) {
+        if (w.pendingTicket < 0) return;
+        dropTicket(w.pendingTicket, w.pendingSlot);
+        w.pendingTicket = w.pendingSlot = -1;
     }
 
     void refreshFraming() {
@@ -279,9 +495,10 @@ protected:
 
     sdrgpu_frontend* _fe = nullptr;
     std::mutex _mtx;   // one thread at a time on the device front end (worker vs setters)
+    InputRing _ring;
+    InputBuffer _inBuf;
     Worker _worker;
     std::map<std::string, Vfo> vfos;
-    std::vector<float> _rows;
 
     double _sampleRate = 0;
     int _decimRatio = 1;

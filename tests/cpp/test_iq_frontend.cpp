@@ -4,8 +4,15 @@
 // through acquire / releaseFFTBuffer, VFO outputs through the RxVFO's `out` stream (read by a
 // consumer thread, as the radio module's demodulator would), and the IQ through a bound stream.
 // Everything is checked against the same blocks pushed straight into a second device front end
-// through the C ABI (same kernels: bit-exact), and the bound stream against the input.
+// through the C ABI (same kernels: bit-exact), against the oracle (every delivered dB row vs the
+// oracle's window * FFT * log-power of its reshaper frame, the VFO output vs the oracle's RxVFO),
+// and the bound stream against the input. A second run checks the lossy input buffer
+// (buffering = true, frame_buffer.h:64-71: a slow consumer makes the front end drop input blocks
+// instead of blocking the source) and re-planning an attached VFO while the front end runs.
 // Built and run by tests/test_cpp_dropin.py.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -14,6 +21,7 @@
 #include <vector>
 
 #include "signal_path/iq_frontend.h"
+#include "sdr_oracle.h"
 
 static int failures = 0;
 #define CHECK(c, ...) do { if (!(c)) { std::printf("FAIL %s:%d ", __FILE__, __LINE__); std::printf(__VA_ARGS__); std::printf("\n"); failures++; } } while (0)
@@ -124,7 +132,91 @@ int main() {
     fe.setFFTSize(8192);
     CHECK(fe.getEffectiveSamplerate() > 0, "after setFFTSize");
     sdrgpu_frontend_destroy(ref);
+
+    // ---- against the oracle: rows (reshaper framing: frame j at j * (nz + skip)) and the VFO
+    {
+        int skip = 0, nz = 0;
+        orc_gen_reshape_params(fs, N, 15.0, &skip, &nz);
+        std::vector<float> win(nz), work(4 * (size_t)N), ref(N);
+        orc_create_window(6, win.data(), nz, 1);
+        double worst = 0;
+        int rr = 0;
+        for (int k = 0; k < nRows; k++) {
+            if ((k + 1) % sink.nullEvery == 0) continue;
+            if ((size_t)(rr + 1) * N > sink.rows.size()) break;
+            orc_fft_logmag((const float*)(x.data() + (size_t)k * (nz + skip)), nz, N, win.data(), work.data(), ref.data());
+            const float* got = sink.rows.data() + (size_t)rr * N;
+            const float peak = *std::max_element(ref.begin(), ref.end());
+            for (int i = 0; i < N; i++)
+                if (ref[i] > peak - 60) worst = std::max(worst, (double)std::fabs(got[i] - ref[i]));
+            rr++;
+        }
+        CHECK(rr > 0 && worst < 1e-3, "dB rows vs oracle: max |err| %g dB over %d rows (bins within 60 dB of peak)", worst, rr);
+        orc_vfo* ov = orc_vfo_create(fs, 48000, 12500, 150e3, 1);
+        std::vector<float> ob(2 * (size_t)blk);
+        std::vector<dsp::complex_t> want;
+        for (int b = 0; b < nblk; b++) {
+            const int m = orc_vfo_process(ov, (const float*)(x.data() + (size_t)b * blk), blk, ob.data());
+            for (int i = 0; i < m; i++) want.push_back({ob[2 * i], ob[2 * i + 1]});
+        }
+        orc_vfo_destroy(ov);
+        double verr = 0;
+        for (size_t i = 0; i < std::min(want.size(), gotVfo.size()); i++)
+            verr = std::max(verr, (double)std::max(std::fabs(want[i].re - gotVfo[i].re), std::fabs(want[i].im - gotVfo[i].im)));
+        CHECK(want.size() == gotVfo.size() && verr < 5e-5, "VFO vs oracle RxVFO: %zu vs %zu samples, max |err| %g",
+              gotVfo.size(), want.size(), verr);
+    }
     std::printf("rows %d (every %d-th acquire NULL), VFO %d samples, IQ %zu samples\n", nRows, sink.nullEvery, nVfo, gotIq.size());
+
+    // ---- lossy input buffer + live re-planning of an attached VFO
+    {
+        RowSink s2;
+        s2.buf.resize(N);
+        dsp::stream<dsp::complex_t> in2;
+        IQFrontEnd fe2;
+        fe2.init(&in2, fs, true, 1, false, N, 15.0, dsp::window::BLACKMAN_HARRIS7, acquire, release, &s2);
+        dsp::channel::RxVFO* v2 = fe2.addVFO("slow", 48000, 12500, 150e3);
+        fe2.start();
+        std::atomic<long long> got{0};
+        std::atomic<bool> quit{false};
+        std::thread slow([&] {   // a demodulator that takes 3 ms per block (the source delivers one per 0.05 ms)
+            while (!quit) {
+                const int n = v2->out.read();
+                if (n < 0) return;
+                got += n;
+                v2->out.flush();
+                std::this_thread::sleep_for(std::chrono::milliseconds(3));
+            }
+        });
+        const int nb2 = 300;
+        const auto t0 = std::chrono::steady_clock::now();
+        long long atSet = -1;
+        int rowsAtSet = -1;
+        for (int b = 0; b < nb2; b++) {
+            std::memcpy(in2.writeBuf, x.data() + (size_t)(b % nblk) * blk, sizeof(dsp::complex_t) * blk);
+            if (!in2.swap(blk)) break;
+            if (b == nb2 / 2) {   // SDR++ re-plans VFOs while the radio runs (bandwidth slider)
+                v2->setBandwidth(25000);
+                v2->setOffset(-100e3);
+                atSet = got.load();
+                rowsAtSet = s2.n;
+            }
+        }
+        const double srcMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        std::this_thread::sleep_for(std::chrono::milliseconds(400));
+        const long long dropped = fe2.droppedBlocks();
+        const long long gotEnd = got.load();
+        const int rowsEnd = s2.n;
+        quit = true;
+        fe2.stop();
+        v2->out.stopReader();
+        slow.join();
+        CHECK(dropped > 0, "lossy buffer dropped no block behind a slow consumer");
+        CHECK(atSet >= 0 && gotEnd > atSet, "VFO output stopped after setBandwidth (%lld -> %lld samples)", atSet, gotEnd);
+        CHECK(rowsAtSet >= 0 && rowsEnd > rowsAtSet, "rows stopped after setBandwidth (%d -> %d)", rowsAtSet, rowsEnd);
+        std::printf("lossy run: %d source blocks in %.1f ms, %lld dropped, VFO %lld -> %lld samples, rows %d -> %d\n", nb2,
+                    srcMs, dropped, atSet, gotEnd, rowsAtSet, rowsEnd);
+    }
     std::printf(failures ? "FAILED (%d)\n" : "ALL OK\n", failures);
     return failures ? 1 : 0;
 }

@@ -53,10 +53,11 @@ def _build_frontend():
            "-I", os.path.join(ROOT, "sdrpp_amd", "dsp", "gpu"),
            "-I", os.path.join(ROOT, "sdrpp_amd", "dsp", "runtime", "dsp"),
            "-I", os.path.join(ROOT, "sdrpp_amd", "dsp", "runtime", "dsp", "buffer"),
-           "-I", os.path.join(ROOT, "include"),
+           "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "oracle"),
            os.path.join(ROOT, "tests", "cpp", "test_iq_frontend.cpp"),
            "-L", os.path.join(ROOT, "sdrpp_amd", "lib"), "-lsdrgpu",
-           "-Wl,-rpath," + os.path.join(ROOT, "sdrpp_amd", "lib"), "-o", FE_BIN]
+           "-L", os.path.join(ROOT, "oracle"), "-lsdr_oracle",
+           "-Wl,-rpath," + os.path.join(ROOT, "sdrpp_amd", "lib") + ":" + os.path.join(ROOT, "oracle"), "-o", FE_BIN]
     subprocess.check_call(cmd)
     return FE_BIN
 

@@ -140,3 +140,68 @@ def test_preproc_decim_dcblock_invert(rng):
     got, want = np.concatenate(got), np.concatenate(want)
     assert got.shape == want.shape
     assert np.abs(got - want).max() <= 2e-5 * np.abs(want).max()
+
+
+def test_pipelined_submit_collect_matches_push():
+    """sdrgpu_frontend_submit / collect (the drop-in worker's pipelined call style: H2D of block
+    k + 1 on the copy stream while block k computes and reads back) gives, block for block, the
+    rows, VFO outputs and preprocessed IQ of the synchronous push -- bit for bit -- for ragged
+    blocks, with two tickets in flight, from pageable and from sdrgpu_host_alloc'ed memory."""
+    import ctypes
+    fs, N = 2.4e6, 8192
+    x = multitone(int(fs * 0.4), fs, seed=11)
+    sizes = [12000, 5000, 31000, 777, 12000]
+    blocks = list(pushes(x, sizes))
+    ref = dsp.IQFrontEnd(fs, fft_size=N, fft_rate=60.0)
+    rv = ref.add_vfo(48000, 12500, 150e3)
+    want = []
+    for b in blocks:
+        r = ref.push(b)
+        want.append((r, ref.vfo_output(rv)))
+    ref.close()
+    # host_alloc'ed staging: DMA'd straight from the caller's buffer
+    hp = ctypes.c_void_p()
+    sdrpp_amd.check(sdrpp_amd.lib.sdrgpu_host_alloc(ctypes.byref(hp), 8 * max(sizes)))
+    pinned = np.ctypeslib.as_array((ctypes.c_float * (2 * max(sizes))).from_address(hp.value)).view(np.complex64)
+    try:
+        for use_pinned in (False, True):
+            fe = dsp.IQFrontEnd(fs, fft_size=N, fft_rate=60.0)
+            vid = fe.add_vfo(48000, 12500, 150e3)
+            got, pend = [], []
+            for k, b in enumerate(blocks):
+                if use_pinned:
+                    if pend:   # the pinned buffer is reused: the previous H2D must be done -> collect first
+                        got.append(fe.collect(pend.pop(0), vfos=[vid]))
+                    pinned[:len(b)] = b
+                    t = fe.submit(None, ptr=pinned.ctypes.data, count=len(b), want_iq=True)
+                else:
+                    t = fe.submit(b, want_iq=True)
+                pend.append(t)
+                if len(pend) == 2:
+                    got.append(fe.collect(pend.pop(0), vfos=[vid]))
+            while pend:
+                got.append(fe.collect(pend.pop(0), vfos=[vid]))
+            with pytest.raises(sdrpp_amd.SdrGpuError):
+                fe.collect(12345)   # not in flight
+            fe.close()
+            assert len(got) == len(blocks)
+            for k, ((r, o, iq_), (wr, wo), b) in enumerate(zip(got, want, blocks)):
+                assert np.array_equal(r, wr), (use_pinned, k)
+                assert np.array_equal(o[vid], wo), (use_pinned, k)
+                assert np.array_equal(iq_, b), (use_pinned, k)
+    finally:
+        sdrpp_amd.lib.sdrgpu_host_free(hp)
+
+
+def test_submit_refuses_a_third_ticket():
+    fe = dsp.IQFrontEnd(2.4e6, fft_size=4096, fft_rate=60.0)
+    b = multitone(12000, 2.4e6)
+    t0 = fe.submit(b)
+    t1 = fe.submit(b)
+    with pytest.raises(sdrpp_amd.SdrGpuError):
+        fe.submit(b)
+    fe.collect(t0)
+    t2 = fe.submit(b)
+    fe.collect(t1)
+    fe.collect(t2)
+    fe.close()

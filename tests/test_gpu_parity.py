@@ -606,6 +606,14 @@ def test_spectrum_ulp_distribution(kind, N, nz, rng):
     if sg["bins"] >= 1000:   # (a tonal frame has only a handful of bins within 60 dB of its peak)
         assert sg["frac_le_1ulp"] >= sr["frac_le_1ulp"] - 0.03, (sg, sr)
     assert sg["p99"] <= 2 * sr["p99"] + 1, (sg, sr)
+    # absolute bars (the literal north_star metric, stated rather than only relative): at least 97%
+    # of the bins within 1 ulp on a full random frame (measured 98.3% at 64k, 99.2% at 1M; 91% on
+    # the 22-bin AES17 table, 94-100% on the tonal frames), p50 0 ulp (1 on those few-bin frames), and the worst bin no more
+    # than 2x pocketfft's worst (or 16 ulp): measured max 11 / 20 / 84 ulp vs pocketfft 11 / 24 / 72
+    # at 4k / 64k / 1M (profiles/r3/spectrum_ulp_r3a.jsonl)
+    assert sg["p50"] <= (0 if sg["bins"] >= 1000 else 1), sg
+    assert sg["frac_le_1ulp"] >= (0.97 if sg["bins"] >= 1000 else 0.85), sg
+    assert sg["max"] <= max(2 * sr["max"], 16), (sg, sr)
 
 
 # ------------------------------------------------- spectrum + VFO fused read
