@@ -204,13 +204,21 @@ def cpu_baseline(config, seconds):
     import cpu_baseline as cb
     r = cb.measure(config, seconds)
     h = r["host"]
-    return {"value": round(r["value_all_cores"], 3), "unit": "MS/s", "cores": r["cores_all"], "kind": "port",
-            "value_1core": round(r["value_1core"], 3),
-            "sample": f"{r['variant']}: {r['cores_all']} independent streams x {seconds:.0f} s (all-core aggregate), "
-                      f"1 stream {r['value_1core']:.2f} MS/s; 1-core variants "
-                      + ", ".join(f"{k} {v:.2f}" for k, v in r["variants_1core"].items())
-                      + f"; {r['build']}; SpeedTester-style 1e6-sample blocks of uniform [-1,1) IQ",
-            "host": {"nproc": h["nproc"], "affinity_cpus": h["affinity"], "model": h["model"]}}
+    out = {"value": round(r["value_all_cores"], 3), "unit": "MS/s", "cores": r["cores_all"], "kind": "port",
+           "cores_source": r["cores_source"], "value_1core": round(r["value_1core"], 3),
+           "sample": f"{r['variant']}: {r['cores_all']} independent streams x {seconds:.0f} s (all-core aggregate), "
+                     f"1 stream {r['value_1core']:.2f} MS/s; 1-core variants "
+                     + ", ".join(f"{k} {v:.2f}" for k, v in r["variants_1core"].items())
+                     + f"; {r['build']}; SpeedTester-style 1e6-sample blocks of uniform [-1,1) IQ",
+           "host": {"nproc": h["nproc"], "affinity_cpus": h["affinity"], "cgroup_cpu_quota": h["cgroup_cpu_quota"],
+                    "model": h["model"], "core_max_mhz": h["core_max_mhz"]}}
+    # the whole machine, extrapolated linearly from one core over every affinity CPU (SMT siblings
+    # counted as cores: an upper bound for the CPU side)
+    out["value_all_affinity_cpus_linear"] = round(r["value_1core"] * h["affinity"], 1)
+    for k in ("gflops_1core", "fma_peak_frac_1core"):
+        if k in r:
+            out[k] = r[k]
+    return out
 
 
 def spectrum_ulp_report():
@@ -501,6 +509,7 @@ def main():
         if world == 1 and not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline("c4" if a.config == "c4g" else a.config, a.cpu_seconds)
             out["speedup_vs_cpu_all_cores"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+            out["speedup_vs_cpu_all_affinity_linear"] = round(out["value"] / out["cpu_baseline"]["value_all_affinity_cpus_linear"], 2)
             cpu_cache = {}
             for c, r in subs.items():
                 ck = "c4" if c == "c4g" else c   # both C4 forms against the same CPU channelizer
@@ -508,6 +517,7 @@ def main():
                     cpu_cache[ck] = cpu_baseline(ck, a.cpu_seconds)
                 r["cpu_baseline"] = cpu_cache[ck]
                 r["speedup_vs_cpu_all_cores"] = round(r["value"] / r["cpu_baseline"]["value"], 1)
+                r["speedup_vs_cpu_all_affinity_linear"] = round(r["value"] / r["cpu_baseline"]["value_all_affinity_cpus_linear"], 2)
         if subs:
             out["configs"] = subs
         if world == 1 and a.config == "c5" and not a.no_sub:

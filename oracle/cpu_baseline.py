@@ -34,16 +34,53 @@ def native_oracle():
     os.makedirs(out_dir, exist_ok=True)
     so = os.path.join(out_dir, "libsdr_oracle_native.so")
     src = os.path.join(HERE, "sdr_oracle.c")
-    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+    fast = os.path.join(HERE, "cpu_fast.c")
+    if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(src), os.path.getmtime(fast)):
         # -ffp-contract=fast: the dot products use FMA like VOLK's *_avx2_fma kernels (this copy
         # is only timed; the in-tree checker build keeps -ffp-contract=off)
         cmd = ["gcc", "-O3", "-march=native", "-ffp-contract=fast", "-fno-fast-math", "-fPIC", "-shared",
-               "-o", so, src, "-lm"]
+               "-o", so, src, fast, "-lm"]
         try:
             subprocess.check_call(cmd, cwd=HERE, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         except (OSError, subprocess.CalledProcessError):
             return None
     return so
+
+
+def cgroup_cpu_quota():
+    """CPUs this process may use per the cgroup v2 CPU controller (cpu.max "quota period"), or None
+    when unlimited / not readable. The GPU box grants 16 (1600000 / 100000) of its 256 CPUs."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q == "max":
+            return None
+        return max(1, int(int(q) // int(p)))
+    except (OSError, ValueError):
+        return None
+
+
+def core_peak_gflops():
+    """fp32 FMA peak of one core: 2 FMA pipes x 16 lanes (AVX-512) x 2 flop x the max clock (lscpu
+    'CPU max MHz', else /proc/cpuinfo 'cpu MHz'). Zen 5 (EPYC 9575F): 2 x 512-bit FMA per cycle."""
+    mhz = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("CPU max MHz"):
+                mhz = float(line.split(":", 1)[1])
+    except (OSError, ValueError, subprocess.SubprocessError):
+        pass
+    if mhz is None:
+        try:
+            with open("/proc/cpuinfo") as f:
+                for line in f:
+                    if line.startswith("cpu MHz"):
+                        mhz = float(line.split(":", 1)[1])
+                        break
+        except (OSError, ValueError):
+            return None, None
+    return (2 * 16 * 2 * mhz / 1e3 if mhz else None), mhz
 
 
 def host_info():
@@ -60,7 +97,9 @@ def host_info():
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = os.cpu_count()
-    return {"nproc": os.cpu_count(), "affinity": aff, "model": model}
+    peak, mhz = core_peak_gflops()
+    return {"nproc": os.cpu_count(), "affinity": aff, "model": model, "cgroup_cpu_quota": cgroup_cpu_quota(),
+            "core_max_mhz": mhz, "core_fp32_peak_gflops": peak}
 
 
 def _iq(rng, n):
@@ -161,12 +200,23 @@ def _spawn(config, seconds, seed, variant, cpu, lib):
     return subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
 
 
-def measure(config, seconds=8.0, max_cores=16):
-    """1-core figure of every variant (in turn), then the fastest variant on all cores."""
+# fp32 flop per input sample of each config's CPU chain (for the FMA-peak fraction of the 1-core leg)
+FLOP_PER_SAMPLE = {
+    "c3": 2 * 256 * 2 / 8 + 6 + 40 / 8,   # 256 complex x real MACs per output / D, rotator, quadrature
+}
+
+
+def measure(config, seconds=8.0, max_cores=None):
+    """1-core figure of every variant (in turn), then the fastest variant on all cores this process
+    may use: the cgroup CPU quota (16 on the GPU box), capped by the affinity mask."""
     lib = native_oracle()
     info = host_info()
     cores_avail = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count()))
-    ncores = max(1, min(max_cores, len(cores_avail)))
+    quota = info["cgroup_cpu_quota"]
+    ncores = len(cores_avail) if quota is None else min(quota, len(cores_avail))
+    if max_cores is not None:
+        ncores = min(ncores, max_cores)
+    ncores = max(1, ncores)
     one = {}
     for name in workloads_names(config):
         p = _spawn(config, seconds, 0, name, cores_avail[0], lib)
@@ -178,9 +228,15 @@ def measure(config, seconds=8.0, max_cores=16):
     for p in procs:
         r = json.loads(p.communicate()[0].strip().splitlines()[-1])[best]
         rates.append(r["samples"] / r["seconds"] / 1e6)
-    return {"value_1core": one[best], "variant": best, "variants_1core": one, "value_all_cores": sum(rates),
-            "cores_all": ncores, "per_stream_min": min(rates), "host": info,
-            "build": "oracle C -O3 -march=native (host-built)" if lib else "oracle C (in-tree build)"}
+    r = {"value_1core": one[best], "variant": best, "variants_1core": one, "value_all_cores": sum(rates),
+         "cores_all": ncores, "cores_source": "cgroup cpu.max quota" if quota is not None else "affinity mask",
+         "per_stream_min": min(rates), "host": info,
+         "build": "oracle C -O3 -march=native (host-built)" if lib else "oracle C (in-tree build)"}
+    if config in FLOP_PER_SAMPLE and info.get("core_fp32_peak_gflops"):
+        gf = one[best] * 1e6 * FLOP_PER_SAMPLE[config] / 1e9
+        r["gflops_1core"] = round(gf, 1)
+        r["fma_peak_frac_1core"] = round(gf / info["core_fp32_peak_gflops"], 3)
+    return r
 
 
 def workloads_names(config):

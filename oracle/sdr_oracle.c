@@ -342,11 +342,18 @@ static void dot_cc(const float* x, const float* h, int n, float* o, int precise)
 
 /* ------------------------------------------------------ FIR / DecimatingFIR */
 /* filter/fir.h:62-83 and filter/decimating_fir.h:45-68 */
+/* CPU-baseline kernels (cpu_fast.c) */
+void cf_rotate(const float* in, float* out, int count, float* pr, float* pi, float dr, float di, int* cnt);
+int  cf_fir_cf_decim(const float* x, const float* hh, int m16, int offset, int D, int count, float* out);
+void cf_quad(const float* in, int count, float* out, float* dre, float* dim, float inv);
+
 struct orc_fir {
     int dtype, ttype, ntaps, decim, offset, precise, cap;
     float* taps;
     float* hh;    /* taps duplicated per (re, im) pair (CPU-baseline complex x real dot) */
-    float* buf;   /* [ntaps-1 history | input], elements of dtype */
+    float* hh16;  /* hh zero-padded to m16 floats (cf_fir_cf_decim) */
+    int m16;
+    float* buf;   /* [ntaps-1 history | input | 16 floats of zero slack], elements of dtype */
 };
 
 static int esz(int dtype) { return dtype == ORC_C64 ? 2 : 1; }
@@ -373,6 +380,13 @@ void orc_fir_set_taps(orc_fir* f, const float* taps, int ntaps) {
     memcpy(f->taps, taps, sizeof(float) * ntaps * esz(f->ttype));
     free(f->hh);
     f->hh = (f->ttype == ORC_F32) ? dup_taps(taps, ntaps) : NULL;
+    free(f->hh16);
+    f->hh16 = NULL;
+    f->m16 = (2 * ntaps + 15) / 16 * 16;
+    if (f->ttype == ORC_F32) {
+        f->hh16 = (float*)calloc((size_t)f->m16, sizeof(float));
+        memcpy(f->hh16, f->hh, sizeof(float) * 2 * (size_t)ntaps);
+    }
     f->ntaps = ntaps;
     f->offset = 0;   /* DecimatingFIR::setTaps (decimating_fir.h:19-26) */
 }
@@ -385,12 +399,19 @@ void orc_fir_reset(orc_fir* f) {
 int orc_fir_process(orc_fir* f, const float* in, int count, float* out) {
     int e = esz(f->dtype), h = f->ntaps - 1;
     if (f->cap < count) {
-        float* nb = (float*)malloc(sizeof(float) * (size_t)(h + count) * e);
+        float* nb = (float*)malloc(sizeof(float) * ((size_t)(h + count) * e + 16));
         memcpy(nb, f->buf, sizeof(float) * h * e);
         free(f->buf); f->buf = nb; f->cap = count;
     }
     memcpy(f->buf + (size_t)h * e, in, sizeof(float) * (size_t)count * e);
     int outCount = 0;
+    if (!f->precise && f->dtype == ORC_C64 && f->ttype == ORC_F32) {   /* CPU baseline (cpu_fast.c) */
+        memset(f->buf + (size_t)(h + count) * e, 0, sizeof(float) * 16);
+        outCount = cf_fir_cf_decim(f->buf, f->hh16, f->m16, f->offset, f->decim, count, out);
+        f->offset += outCount * f->decim - count;
+        memmove(f->buf, f->buf + (size_t)count * e, sizeof(float) * h * e);
+        return outCount;
+    }
     for (; f->offset < count; f->offset += f->decim) {
         const float* x = f->buf + (size_t)f->offset * e;
         float* o = out + (size_t)outCount * e;
@@ -408,7 +429,7 @@ int orc_fir_process(orc_fir* f, const float* in, int count, float* out) {
     return outCount;
 }
 
-void orc_fir_destroy(orc_fir* f) { if (!f) return; free(f->buf); free(f->taps); free(f->hh); free(f); }
+void orc_fir_destroy(orc_fir* f) { if (!f) return; free(f->buf); free(f->taps); free(f->hh); free(f->hh16); free(f); }
 
 /* ------------------------------------------------------------------ xlator */
 /* channel/frequency_xlator.h:15-50. phaseDelta = lv_cmake(cos(w), sin(w)) is
@@ -445,17 +466,8 @@ void orc_xlator_set_offset(orc_xlator* x, double offset_rad) {
 }
 void orc_xlator_reset(orc_xlator* x) { x->n = 0; x->origin = 0; }   /* reset(): phase = 1+0j */
 int orc_xlator_process(orc_xlator* x, const float* in, int count, float* out) {
-    if (x->fast) {
-        float pr = x->pr, pi = x->pi;
-        for (int i = 0; i < count; i++) {
-            float re = in[2 * i], im = in[2 * i + 1];
-            out[2 * i] = re * pr - im * pi;
-            out[2 * i + 1] = re * pi + im * pr;
-            float npr = pr * x->dr - pi * x->di, npi = pr * x->di + pi * x->dr;
-            pr = npr; pi = npi;
-            if (++x->cnt == 512) { float m = hypotf(pr, pi); pr /= m; pi /= m; x->cnt = 0; }
-        }
-        x->pr = pr; x->pi = pi;
+    if (x->fast) {   /* CPU baseline: the rotator on 8 lanes per vector (cpu_fast.c) */
+        cf_rotate(in, out, count, &x->pr, &x->pi, x->dr, x->di, &x->cnt);
         return count;
     }
     const long double twopi = 2.0L * (long double)DB_M_PI;
@@ -474,7 +486,7 @@ void orc_xlator_destroy(orc_xlator* x) { free(x); }
 /* -------------------------------------------------------------- quadrature */
 /* demod/quadrature.h:41-56 (USE_QUAD_FM_DEMOD=1): out = arg(y*conj(d)) / dev.
  * _din is uninitialised until reset(); the restatement uses 0. */
-struct orc_quad { float inv; float dre, dim; };
+struct orc_quad { float inv; float dre, dim; int fast; };
 orc_quad* orc_quad_create(double deviation_rad) {
     orc_quad* q = (orc_quad*)calloc(1, sizeof(orc_quad));
     q->inv = (float)(1.0 / deviation_rad);
@@ -482,6 +494,10 @@ orc_quad* orc_quad_create(double deviation_rad) {
 }
 void orc_quad_reset(orc_quad* q) { q->dre = 0.0f; q->dim = 0.0f; }
 int orc_quad_process(orc_quad* q, const float* in, int count, float* out) {
+    if (q->fast) {   /* CPU baseline: 16 outputs per vector, polynomial atan (cpu_fast.c) */
+        cf_quad(in, count, out, &q->dre, &q->dim, q->inv);
+        return count;
+    }
     for (int i = 0; i < count; i++) {
         float yr = in[2 * i], yi = in[2 * i + 1];
         float br = q->dre, bi = -q->dim;                 /* _din.conj() */
@@ -627,7 +643,7 @@ void orc_rres_destroy(orc_rres* r) { if (!r) return; orc_pdec_destroy(r->pd); or
 
 /* ------------------------------------------------------------------ RxVFO */
 /* channel/rx_vfo.h:24-121 */
-struct orc_vfo { orc_xlator* x; orc_rres* rr; orc_fir* lpf; int filterNeeded; };
+struct orc_vfo { orc_xlator* x; orc_rres* rr; orc_fir* lpf; int filterNeeded; float* tmp; int cap; };
 orc_vfo* orc_vfo_create(double inSr, double outSr, double bw, double offset, int precise) {
     orc_vfo* v = (orc_vfo*)calloc(1, sizeof(orc_vfo));
     v->x = precise ? orc_xlator_create(hz_to_rads(-offset, inSr)) : orc_xlator_create_fast(hz_to_rads(-offset, inSr));
@@ -642,12 +658,26 @@ orc_vfo* orc_vfo_create(double inSr, double outSr, double bw, double offset, int
     return v;
 }
 int orc_vfo_process(orc_vfo* v, const float* in, int count, float* out) {
+    if (!v->lpf->precise) {   /* CPU baseline: L2-sized sub-blocks (same stream, state carried) */
+        const int sub = 32768;
+        if (v->cap < (count < sub ? count : sub)) { free(v->tmp); v->cap = count < sub ? count : sub; v->tmp = (float*)malloc(sizeof(float) * 2 * (size_t)v->cap); }
+        int total = 0;
+        for (int i = 0; i < count; i += sub) {
+            const int c = count - i < sub ? count - i : sub;
+            orc_xlator_process(v->x, in + 2 * (size_t)i, c, v->tmp);
+            int m = orc_rres_process(v->rr, v->tmp, c, v->tmp);
+            if (v->filterNeeded) orc_fir_process(v->lpf, v->tmp, m, v->tmp);
+            memcpy(out + 2 * (size_t)total, v->tmp, sizeof(float) * 2 * (size_t)m);
+            total += m;
+        }
+        return total;
+    }
     orc_xlator_process(v->x, in, count, out);
     count = orc_rres_process(v->rr, out, count, out);
     if (v->filterNeeded) orc_fir_process(v->lpf, out, count, out);
     return count;
 }
-void orc_vfo_destroy(orc_vfo* v) { if (!v) return; orc_xlator_destroy(v->x); orc_rres_destroy(v->rr); orc_fir_destroy(v->lpf); free(v); }
+void orc_vfo_destroy(orc_vfo* v) { if (!v) return; orc_xlator_destroy(v->x); orc_rres_destroy(v->rr); orc_fir_destroy(v->lpf); free(v->tmp); free(v); }
 
 /* ------------------------------------------------------- BroadcastFM mono */
 /* demod/broadcast_fm.h:18-49 (init), :144-215 (process, _stereo == false, no RDS) */
@@ -655,6 +685,7 @@ struct orc_wfm { orc_quad* q; orc_fir* al; int lowPass; float* tmp; int cap; };
 orc_wfm* orc_wfm_create(double deviation, double samplerate, int lowPass, int precise) {
     orc_wfm* w = (orc_wfm*)calloc(1, sizeof(orc_wfm));
     w->q = orc_quad_create(hz_to_rads(deviation, samplerate));
+    w->q->fast = !precise;
     int n = orc_low_pass(15000.0, 4000.0, samplerate, 0, NULL);
     float* t = (float*)malloc(sizeof(float) * n);
     orc_low_pass(15000.0, 4000.0, samplerate, 0, t);
@@ -1193,13 +1224,23 @@ orc_ddcfm* orc_ddcfm_create(double offsetRad, const float* taps, int ntaps, int 
     d->x = precise ? orc_xlator_create(offsetRad) : orc_xlator_create_fast(offsetRad);
     d->f = orc_fir_create(ORC_C64, ORC_F32, taps, ntaps, decim, precise);
     d->q = orc_quad_create(deviationRad);
+    d->q->fast = !precise;
     return d;
 }
 int orc_ddcfm_process(orc_ddcfm* d, const float* in, int count, float* out) {
-    if (d->cap < count) { free(d->a); free(d->b); d->a = (float*)malloc(sizeof(float) * 2 * count); d->b = (float*)malloc(sizeof(float) * 2 * count); d->cap = count; }
-    orc_xlator_process(d->x, in, count, d->a);
-    int m = orc_fir_process(d->f, d->a, count, d->b);
-    return orc_quad_process(d->q, d->b, m, out);
+    /* the CPU baseline (precise = 0) runs the chain in L2-sized sub-blocks so the intermediates
+     * stay in cache (the result is the same stream: every stage carries its state) */
+    const int sub = d->f->precise ? count : 16384;
+    const int cap = count < sub ? count : sub;
+    if (d->cap < cap) { free(d->a); free(d->b); d->a = (float*)malloc(sizeof(float) * 2 * cap); d->b = (float*)malloc(sizeof(float) * 2 * cap); d->cap = cap; }
+    int total = 0;
+    for (int i = 0; i < count; i += sub) {
+        const int c = count - i < sub ? count - i : sub;
+        orc_xlator_process(d->x, in + 2 * (size_t)i, c, d->a);
+        int m = orc_fir_process(d->f, d->a, c, d->b);
+        total += orc_quad_process(d->q, d->b, m, out + total);
+    }
+    return total;
 }
 void orc_ddcfm_destroy(orc_ddcfm* d) {
     if (!d) return;
