@@ -876,13 +876,18 @@ PinnedBuf::~PinnedBuf() {
 }
 
 int StreamOrder::follow(hipStream_t s) {
-    if (recorded && last != s) SDRGPU_HIP(hipStreamWaitEvent(s, ev, 0));
+    if (last == nullptr || last == s) return SDRGPU_OK;
+    if (multi) {
+        SDRGPU_HIP(hipStreamWaitEvent(s, ev, 0));
+        return SDRGPU_OK;
+    }
+    SDRGPU_HIP(hipDeviceSynchronize());   // first stream change: the previous stream may be gone
+    if (!ev) SDRGPU_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    multi = true;
     return SDRGPU_OK;
 }
 int StreamOrder::done(hipStream_t s) {
-    if (!ev) SDRGPU_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    SDRGPU_HIP(hipEventRecord(ev, s));
-    recorded = true;
+    if (multi) SDRGPU_HIP(hipEventRecord(ev, s));
     last = s;
     return SDRGPU_OK;
 }

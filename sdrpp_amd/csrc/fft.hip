@@ -365,6 +365,197 @@ __global__ __launch_bounds__(S / 2 * L / 16) void fft_passA2_kernel(
     passA2_tile<L, S>(lds, blockIdx.x, in, frameStride, frames, win, nz, N2, logN, tw, tfull, scratch);
 }
 
+// ---- 1M pass A, persistent and software-pipelined (N1 = 1024, paired columns) --------------
+// The 1M column FFT needs S x 1024 x 8 B of LDS per tile (139 KB at S = 16), so one workgroup per
+// CU: in the one-shot kernel above each CU alternates "load the tile" and "transform + store it",
+// and HBM idles during the transform. Here a CU's workgroup walks tiles blockIdx.x, +gridDim.x, ...
+// and issues the next tile's input + window loads (96 VGPRs) before it transforms the current one,
+// so the loads fly during the LDS stages and the stores. The stage twiddles are staged in LDS once
+// per workgroup, and the four-step twiddle W_N^(c k1) is generated in fp64 and rounded once
+// (the same single rounding as the table it replaces): for column c and this thread's outputs
+// k1 = t + 64 m, W^(c t) and W^(64 c) come from two 256-entry fp64 tables (W_N^(256 j), W_N^j;
+// c t, 64 c < 2^16) and W^(c (t + 64 m)) = W^(c t) (W^(64 c))^m by an fp64 recurrence over m
+// (15 products: relative error ~1e-15, far below the fp32 rounding). That removes the 8 MB
+// [k1][n2] table read (8 B per sample of L2 / Infinity-Cache traffic).
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+typedef float nt_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 nt_load4(const float2* p) {   // streaming (non-temporal) 16-B load
+    const nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float2 nt_load2(const float2* p) {
+    const nt_f2 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f2*>(p));
+    return make_float2(v.x, v.y);
+}
+__device__ __forceinline__ double2 zmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+// raw buffer resource over `bytes` bytes from p: loads past the end return 0, stores past it are dropped
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+typedef unsigned bu2 __attribute__((ext_vector_type(2)));
+typedef unsigned bu4 __attribute__((ext_vector_type(4)));
+
+template <int S, int CP>   // CP: cache-policy bits of the streaming accesses (0, or 2 = nt; tuning)
+__global__ __launch_bounds__(S / 2 * 1024 / 16) void fft_passA_1m_kernel(
+    const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
+    int logN, const float2* __restrict__ tw, const double2* __restrict__ wt, float2* __restrict__ scratch) {
+    constexpr int L = 1024, P = S / 2, T = L / 16, NT = P * T, LS = Lds<L>::LS;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* twl = lds + S * LS;
+    const int tid = threadIdx.x;
+    const int cp = tid % P, t = tid / P;
+    for (int i = tid; i < L; i += NT) twl[i] = tw[i];   // (first barrier below orders it)
+    const int nb = N2 / S;
+    const int ntiles = nb * frames;
+    // The input / window resources end at nz, so the zero-padded tail loads return 0 (nz even: a
+    // column pair never straddles nz, checked on the host). The row step goes into the per-lane
+    // offset, not the scalar one: the buffer range check covers voffset (+ the instruction offset)
+    // only, so rows past nz addressed through soffset were NOT zeroed -- they read the next frame
+    // and past the window's allocation (a first version did that: wrong and run-to-run varying
+    // rows)
+    const __amdgpu_buffer_rsrc_t rw = brsrc(win, (unsigned)nz * 4u);
+    const int rowB = T * N2 * 8;   // bytes between rows t + 64 r and t + 64 (r + 1)
+    float4 q[16];
+    float2 w[16];
+#define SDRGPU_PA1M_ISSUE(TILE)                                                                                         \
+    do {                                                                                                                \
+        const int b_ = (TILE) % nb;                                                                                     \
+        const long long f_ = (TILE) / nb;                                                                               \
+        const unsigned o_ = (unsigned)(t * N2 + b_ * S + 2 * cp);                                                       \
+        const __amdgpu_buffer_rsrc_t rx_ = brsrc(in + f_ * frameStride, (unsigned)nz * 8u);                            \
+        _Pragma("unroll") for (int r = 0; r < 16; r++) {                                                                \
+            q[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx_, o_ * 8 + r * rowB, 0, CP)); \
+            w[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rw, o_ * 4 + r * rowB / 2, 0, 0));        \
+        }                                                                                                               \
+    } while (0)
+    int tile = blockIdx.x;
+    if (tile < ntiles) SDRGPU_PA1M_ISSUE(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        float2 v0[16], v1[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            v0[r] = make_float2(q[r].x * w[r].x, q[r].y * w[r].x);
+            v1[r] = make_float2(q[r].z * w[r].y, q[r].w * w[r].y);
+        }
+        if (tile + (int)gridDim.x < ntiles) SDRGPU_PA1M_ISSUE(tile + (int)gridDim.x);   // next tile's loads fly now
+        dft16(v0);
+        dft16(v1);
+        int tv = tid;   // laundered thread index: the LDS addresses are recomputed per tile, not hoisted
+        asm volatile("" : "+v"(tv));
+        const int cp2 = tv % P, t2 = tv / P;
+        float2* seq0 = lds + 2 * cp2 * LS;
+        __syncthreads();   // the previous tile's last LDS reads are done (and twl is staged)
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            seq0[pad16(t2 * 16 + r)] = v0[r];
+            seq0[LS + pad16(t2 * 16 + r)] = v1[r];
+        }
+        __syncthreads();
+        stage_lds_v<L, 16, 16, 2>(seq0, twl, t2);   // middle stage (two barriers inside)
+        const int b = tile % nb;
+        const long long f = tile / nb;
+        const int col = b * S + 2 * cp;
+        double2 cur[2], step[2];
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++) {
+            const int c = col + qq;
+            const int e0 = c * t, d = 64 * c;   // < 2^16
+            cur[qq] = zmul(wt[e0 >> 8], wt[256 + (e0 & 255)]);
+            step[qq] = zmul(wt[d >> 8], wt[256 + (d & 255)]);
+        }
+        // last stage (radix 4, NS = 256): outputs k1 = t + 64 m, m = b4 + 4 r, kept in registers
+        float2 y[2][16];
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++)
+#pragma unroll
+            for (int b4 = 0; b4 < 4; b4++) {
+                const int j = t2 + b4 * T;
+                float2 u[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) u[r] = seq0[qq * LS + pad16(j + r * (L / 4))];
+#pragma unroll
+                for (int r = 1; r < 4; r++) u[r] = cmul(u[r], twl[r * j]);
+                dft4v(u);
+#pragma unroll
+                for (int r = 0; r < 4; r++) y[qq][b4 + 4 * r] = u[r];
+            }
+        const __amdgpu_buffer_rsrc_t rs = brsrc(scratch + (f << logN), 0x7fffffffu);
+        const unsigned so = (unsigned)(t * N2 + col) * 8u;
+        // 16-B stores with the row step in the per-lane offset and a ZERO soffset. With the row
+        // step in an SGPR soffset the compiler emits buffer_store_dwordx4 ... s<n> and omits the
+        // wait state a >64-bit store needs before the next VALU instruction overwrites its data
+        // VGPRs (its hazard check skips stores with an SGPR soffset; two 8-B stores get merged
+        // into that same form): the store then wrote already-overwritten data -- rows of some lanes
+        // changing from run to run. The offset is advanced through an opaque
+        // register so the 16 row offsets are not all precomputed (register pressure).
+        unsigned vo = so;
+#pragma unroll
+        for (int m = 0; m < 16; m++) {
+            const float2 a = cmul(y[0][m], make_float2((float)cur[0].x, (float)cur[0].y));
+            const float2 c = cmul(y[1][m], make_float2((float)cur[1].x, (float)cur[1].y));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bu4, make_float4(a.x, a.y, c.x, c.y)), rs, vo, 0, 0);
+            vo += (unsigned)rowB;
+            asm volatile("" : "+v"(vo));
+            if (m < 15) {
+                cur[0] = zmul(cur[0], step[0]);
+                cur[1] = zmul(cur[1], step[1]);
+            }
+        }
+    }
+}
+
+// ---- 1M pass B, persistent and software-pipelined (N2 = 1024) -------------------------------
+// Same transform as fft_passB_kernel<1024, S>, each workgroup walking tiles with the next tile's
+// 16 row values per thread loaded while the current tile is transformed and stored.
+template <int S, int CP>
+__global__ __launch_bounds__(S * 1024 / 16) void fft_passB_1m_kernel(const float2* __restrict__ scratch, int frames, int N1,
+                                                                    int logN, const float2* __restrict__ tw,
+                                                                    float* __restrict__ out) {
+    constexpr int L = 1024, T = L / 16;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* twl = lds + S * Lds<L>::LS;   // stage twiddles, staged once per workgroup
+    const int tid = threadIdx.x;
+    for (int i = tid; i < L; i += S * T) twl[i] = tw[i];   // (first barrier below orders it)
+    const int sF = tid / T, tF = tid % T;
+    const int nb = N1 / S;
+    const int ntiles = nb * frames;
+    float2 fr[16];
+#define SDRGPU_PB1M_ISSUE(TILE)                                                                                       \
+    do {                                                                                                              \
+        const int b_ = (TILE) % nb;                                                                                   \
+        const long long f_ = (TILE) / nb;                                                                             \
+        const __amdgpu_buffer_rsrc_t rs_ = brsrc(scratch + (f_ << logN), 0x7fffffffu);                                \
+        const unsigned o_ = (unsigned)((b_ * S + sF) * L + tF) * 8u;                                                  \
+        _Pragma("unroll") for (int r = 0; r < 16; r++)                                                               \
+            fr[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs_, o_, r * T * 8, CP)); \
+    } while (0)
+    int tile = blockIdx.x;
+    if (tile < ntiles) SDRGPU_PB1M_ISSUE(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        float2 v[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) v[r] = fr[r];
+        if (tile + (int)gridDim.x < ntiles) SDRGPU_PB1M_ISSUE(tile + (int)gridDim.x);
+        // the LDS addresses below are loop-invariant; recomputing them per tile (laundered thread
+        // index) keeps ~40 hoisted address registers from spilling the prefetched tile
+        int tv = tid;
+        asm volatile("" : "+v"(tv));
+        const int sF2 = tv / T, tF2 = tv % T, sL2 = tv % S, tL2 = tv / S;
+        __syncthreads();   // the previous tile's last LDS reads are done
+        stage_first<L>(lds + sF2 * Lds<L>::LS, v, tF2);
+        __syncthreads();
+        const int b = tile % nb;
+        const long long f = tile / nb;
+        const __amdgpu_buffer_rsrc_t ro = brsrc(out + (f << logN) + b * S, 0x7fffffffu);
+        stages_rest<L>(lds, twl, sL2, tL2, [&](int k2, float2 y) {
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, db_of(y)), ro, (unsigned)(sL2 + N1 * k2) * 4u, 0, CP);
+        });
+    }
+}
+
 // ---- pass B: S rows of length N2 per tile, dB out, transposed store -----------------
 // Stage 1 maps threads row-contiguous (coalesced row reads); the last stage maps the row
 // index fastest so the transposed dB store writes S consecutive floats per k2.
@@ -495,6 +686,9 @@ struct FftPlan {
     int sa = 16, sb = 32;             // pass-A columns / pass-B rows per workgroup (tuning)
     float2* cur = nullptr;            // scratch buffer of the chunk being launched
     int sa2 = 0;                      // paired pass-A columns per workgroup (0: paired kernel off)
+    int pipe1m = 1;                   // N1 = N2 = 1024: persistent software-pipelined passes (SDRGPU_FFT_1M=0 off)
+    int gridA = 0, gridB = 0;         // their grids (resident workgroups)
+    DevBuf wt;                        // fp64 W_N^(256 j), W_N^j (j < 256) for the 1M pass A
     hipStream_t own = nullptr;
     PinnedBuf pin_in, pin_out;
     DevBuf dev_in, dev_out;
@@ -595,6 +789,45 @@ static int launch_merged(const FftPlan& p, const float2* scratchB, int framesB, 
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
+
+template <int S, int CP>
+static int launch_passA_1m(FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
+    if (p.N2 % S) { set_error("fft: N2 %d not a multiple of %d columns", p.N2, S); return SDRGPU_ESTATE; }
+    auto k = fft_passA_1m_kernel<S, CP>;
+    size_t lds = sizeof(float2) * (S * Lds<1024>::LS + 1024);
+    SDRGPU_CHECK(set_lds(k, lds));
+    if (!p.gridA) {
+        int per = 0, cus = 0;
+        SDRGPU_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k, S / 2 * 64, lds));
+        SDRGPU_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p.device));
+        p.gridA = std::max(1, per) * cus;
+    }
+    const int ntiles = (p.N2 / S) * frames;
+    hipLaunchKernelGGL(k, dim3(std::min(p.gridA, ntiles)), dim3(S / 2 * 64), lds, s, in, stride, frames, p.win.as<float>(),
+                       p.nz, p.N2, p.logN, p.tw1.as<float2>(), p.wt.as<double2>(), p.cur);
+    SDRGPU_HIP(hipGetLastError());
+    return SDRGPU_OK;
+}
+
+template <int S, int CP>
+static int launch_passB_1m(FftPlan& p, int frames, float* out, hipStream_t s) {
+    auto k = fft_passB_1m_kernel<S, CP>;
+    size_t lds = sizeof(float2) * (S * Lds<1024>::LS + 1024);
+    SDRGPU_CHECK(set_lds(k, lds));
+    if (!p.gridB) {
+        int per = 0, cus = 0;
+        SDRGPU_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k, S * 64, lds));
+        SDRGPU_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p.device));
+        p.gridB = std::max(1, per) * cus;
+    }
+    const int ntiles = (p.N1 / S) * frames;
+    hipLaunchKernelGGL(k, dim3(std::min(p.gridB, ntiles)), dim3(S * 64), lds, s, p.cur, frames, p.N1, p.logN,
+                       p.tw2.as<float2>(), out);
+    SDRGPU_HIP(hipGetLastError());
+    return SDRGPU_OK;
+}
+
+static bool pipe1m_ok(const FftPlan& p, bool paired) { return p.pipe1m && paired && p.N1 == 1024 && p.N2 == 1024 && (p.nz % 2) == 0; }
 
 // merged pass B (chunk c) + pass A (chunk c+1) launches: the 64k split (256 x 256, one-column
 // pass A). The 1M split's merged form (paired pass A, pass B at 8 rows to match its 512
@@ -742,6 +975,21 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         // one box), so it is the default only for N1 >= 512
         p.sa2 = p.N1 >= 512 ? 16 : 0;
         if (const char* e = tuning_env("SDRGPU_FFT_SA2")) p.sa2 = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_1M")) p.pipe1m = atoi(e);
+        if (rc >= 0 && p.N1 == 1024 && p.N2 == 1024) {   // fp64 W_N^(256 j), W_N^j for the 1M pass A
+            std::vector<double2> t(512);
+            for (int j = 0; j < 256; j++) {
+                const double a = -2.0 * M_PI * (double)(256 * j) / (double)fftSize;
+                const double b = -2.0 * M_PI * (double)j / (double)fftSize;
+                t[j] = make_double2(std::cos(a), std::sin(a));
+                t[256 + j] = make_double2(std::cos(b), std::sin(b));
+            }
+            rc = p.wt.ensure(sizeof(double2) * t.size());
+            if (rc >= 0 && hipMemcpy(p.wt.p, t.data(), sizeof(double2) * t.size(), hipMemcpyHostToDevice) != hipSuccess) {
+                set_error("fft: twiddle upload failed");
+                rc = SDRGPU_EHIP;
+            }
+        }
         if (rc >= 0) {   // Tfull[k1][n2] = W_N^(n2 k1), exact argument mod N (both pass-A kernels)
             std::vector<float2> t((size_t)fftSize);
             for (int k1 = 0; k1 < p.N1; k1++)
@@ -841,6 +1089,16 @@ static int fft_execute(sdrgpu_fft* h, const void* in, long long frameStride, int
         const int b = pipe ? (c & 1) : 0;
         p.cur = b ? p.scratch2.as<float2>() : p.scratch.as<float2>();
         if (pipe && c >= 2) SDRGPU_HIP(hipStreamWaitEvent(s, p.evB[b], 0));   // buffer b free again
+        if (pipe1m_ok(p, paired) && !pipe) {
+            if (p.pipe1m == 2) {   // (tuning) non-temporal streaming accesses
+                SDRGPU_CHECK((launch_passA_1m<16, 2>(p, xc, frameStride, nf, s)));
+                SDRGPU_CHECK((launch_passB_1m<16, 2>(p, nf, out + (long long)f0 * p.N, s)));
+            } else {
+                SDRGPU_CHECK((launch_passA_1m<16, 0>(p, xc, frameStride, nf, s)));
+                SDRGPU_CHECK((launch_passB_1m<16, 0>(p, nf, out + (long long)f0 * p.N, s)));
+            }
+            continue;
+        }
         if (paired) SDRGPU_CHECK(dispatch_passA2(p, xc, frameStride, nf, s));
         else SDRGPU_CHECK(dispatch_passA(p, xc, frameStride, nf, s));
         hipStream_t sb = s;

@@ -69,16 +69,20 @@ inline size_t esize(int dtype) { return dtype == SDRGPU_C64 ? 8 : 4; }
 
 // A handle's device state is rewritten by every call (NCO coarse table, history / quadrature
 // ping-pong buffers, FFT scratch), so calls must not overlap. Calls on one stream are ordered by
-// the stream. Every public entry point records `ev` on its own stream when it has enqueued its
-// work (done); a call on another stream first makes its stream wait for that event (follow). The
-// event therefore always belongs to a stream that was live when it was recorded (a caller may
-// destroy a stream after its call), and the new stream waits for exactly the previous call's
-// work. Handles driven only through another handle (a front end's VFOs and FFT plan) skip this:
-// the owner orders them.
+// the stream: a handle driven from one stream (the common case) pays nothing. The first call on
+// another stream cannot know whether the previous stream still exists (a caller may destroy a
+// stream after its call), so it waits with a device-wide synchronise -- the one ordering that
+// needs no handle on that stream -- and the handle switches to multi-stream mode: from then on
+// every entry point records `ev` on its own stream when it has enqueued its work (done), and a
+// call on another stream waits for that event (follow). The event always belongs to a stream that
+// was live when it was recorded, and the new stream waits for exactly the previous call's work.
+// (Recording on every call costs ~2.7 us per entry point in a device-bound call sequence, which is
+// why a single-stream handle does not.) Handles driven only through another handle (a front
+// end's VFOs and FFT plan) skip this: the owner orders them.
 struct StreamOrder {
     hipStream_t last = nullptr;   // stream of the previous call
-    hipEvent_t ev = nullptr;      // recorded on `last` at the end of the previous call
-    bool recorded = false;
+    hipEvent_t ev = nullptr;      // multi-stream mode: recorded on `last` at the end of the previous call
+    bool multi = false;
     int follow(hipStream_t s);
     int done(hipStream_t s);
     ~StreamOrder();

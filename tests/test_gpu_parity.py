@@ -571,6 +571,30 @@ def test_process_dev_across_streams(rng):
     assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
 
 
+def test_stream_destroyed_between_calls(rng):
+    """a handle whose last call ran on a stream the caller then destroyed, called next on
+    another stream (the first stream change synchronises the device instead of touching the dead
+    stream; later changes wait on the end-of-call event), gives the one-stream output stream."""
+    import ctypes
+    import torch
+    x = iq(rng, 300000)
+    d_x = torch.from_numpy(x.view(np.float32)).cuda()
+    ref = dsp.RxVFO(61.44e6, 240000, 200000, 2.5e6).process(x)
+    g = dsp.RxVFO(61.44e6, 240000, 200000, 2.5e6)
+    out = torch.zeros(2 * (len(ref) + 16), dtype=torch.float32, device="cuda")
+    cuts = [0, 70001, 150000, 220000, 300000]
+    m = 0
+    for k in range(len(cuts) - 1):
+        st = ctypes.c_void_p()
+        sdrpp_amd.check(sdrpp_amd.lib.sdrgpu_stream_create(0, ctypes.byref(st)))
+        m += g.process_dev(d_x.data_ptr() + 8 * cuts[k], cuts[k + 1] - cuts[k], out.data_ptr() + 8 * m, st.value)
+        sdrpp_amd.check(sdrpp_amd.lib.sdrgpu_stream_destroy(st))   # gone before the next call
+    torch.cuda.synchronize()
+    assert m == len(ref)
+    got = out[:2 * m].cpu().numpy().view(np.complex64)
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
 SPECTRUM_ULP_CASES = [("random", 4096, 4096), ("random", 65536, 65536), ("random", 1 << 20, 1000000),
                       ("tones", 65536, 65536), ("tones", 1 << 20, 1000000), ("aes17", 0, 0)]
 
