@@ -398,11 +398,54 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, unsigned 
 typedef unsigned bu2 __attribute__((ext_vector_type(2)));
 typedef unsigned bu4 __attribute__((ext_vector_type(4)));
 
-template <int S, int CP>   // CP: cache-policy bits of the streaming accesses (0, or 2 = nt; tuning)
-__global__ __launch_bounds__(S / 2 * 1024 / 16) void fft_passA_1m_kernel(
+// the radix-16 middle stage (NS = 16) of the 1M pass A for one column, thread t: read + twiddle +
+// DFT into v, then (after the caller's barrier) the in-place write
+__device__ __forceinline__ void mid16_read(const float2* seq, const float2* twl, int t, float2 (&v)[16]) {
+    constexpr int L = 1024;
+    const int jm = t % 16;
+#pragma unroll
+    for (int r = 0; r < 16; r++) v[r] = seq[pad16(t + r * (L / 16))];
+#pragma unroll
+    for (int r = 1; r < 16; r++) v[r] = cmul(v[r], twl[r * jm * (L / 256)]);
+    dft16(v);
+}
+__device__ __forceinline__ void mid16_write(float2* seq, int t, const float2 (&v)[16]) {
+    const int idxD = (t / 16) * 256 + (t % 16);
+#pragma unroll
+    for (int r = 0; r < 16; r++) seq[pad16(idxD + r * 16)] = v[r];
+}
+
+// tile -> (frame, block) of the persistent 1M passes. G (the grid, a multiple of 8 G8 and of 8) > 1
+// groups G8 adjacent blocks on one XCD at once: workgroups x, x + 8, ... (same XCD, same round)
+// take blocks b, b + 1, ..., whose row / dB segments share 128-B lines (64-B pass-A segments at 8
+// columns, 32-B dB segments at 8 rows), so a line is filled / written whole in one L2.
+template <int G8>
+__device__ __forceinline__ void tile_fb(int T, int nb, int& b, long long& f) {
+    if constexpr (G8 <= 1) {
+        b = T % nb;
+        f = T / nb;
+    } else {
+        const int g = T / (8 * G8), w = T % (8 * G8);
+        const int P = g * 8 + (w & 7), h = w >> 3;
+        const int npf = nb / G8;
+        f = P / npf;
+        b = G8 * (P % npf) + h;
+    }
+}
+
+// VAR (tuning, SDRGPU_FFT_1M_VAR): bit 0 middle stage one column at a time, bit 3 row offsets
+// advanced through opaque registers (together: no spills, same time as the default, r3 A/B),
+// bit 6 XCD-grouped column blocks (S = 8); bits 4 / 5 measurement only (below). Measured and
+// removed (r3, C2 step, 3 interleaved runs, one box): the last stage + 8-B stores one column at a
+// time (2.22 vs 1.95 ms), the four-step fp64 tables staged in LDS (2.17 vs 1.95 ms).
+template <int S, int CP, int VAR>   // CP: cache-policy bits of the streaming accesses (0, or 2 = nt; tuning)
+__global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_eu(S < 16 ? 2 : 1))) void fft_passA_1m_kernel(
     const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
     int logN, const float2* __restrict__ tw, const double2* __restrict__ wt, float2* __restrict__ scratch) {
     constexpr int L = 1024, P = S / 2, T = L / 16, NT = P * T, LS = Lds<L>::LS;
+    constexpr bool MIDCOL = VAR & 1, LAUNDER = VAR & 8;
+    constexpr bool NOLOAD = VAR & 16, NOSTORE = VAR & 32;   // (measurement only: wrong results)
+    constexpr int XG = ((VAR & 64) && S < 16) ? 16 / S : 1;   // XCD grouping of column blocks (bit 6): 128-B row lines
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     float2* twl = lds + S * LS;
     const int tid = threadIdx.x;
@@ -420,15 +463,29 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) void fft_passA_1m_kernel(
     const int rowB = T * N2 * 8;   // bytes between rows t + 64 r and t + 64 (r + 1)
     float4 q[16];
     float2 w[16];
+    // LAUNDER: the 16 row offsets are advanced through opaque registers; left to itself the
+    // compiler may precompute all 32 and spill them, and every reload from scratch then waits
+    // (vmcnt, in order) for the prefetch loads issued before it
 #define SDRGPU_PA1M_ISSUE(TILE)                                                                                         \
     do {                                                                                                                \
-        const int b_ = (TILE) % nb;                                                                                     \
-        const long long f_ = (TILE) / nb;                                                                               \
+        int b_;                                                                                                         \
+        long long f_;                                                                                                   \
+        tile_fb<XG>((TILE), nb, b_, f_);                                                                                \
+        if (NOLOAD) { b_ = 0; f_ = 0; }                                                                                 \
         const unsigned o_ = (unsigned)(t * N2 + b_ * S + 2 * cp);                                                       \
         const __amdgpu_buffer_rsrc_t rx_ = brsrc(in + f_ * frameStride, (unsigned)nz * 8u);                            \
+        unsigned vq_ = o_ * 8, vw_ = o_ * 4;                                                                            \
         _Pragma("unroll") for (int r = 0; r < 16; r++) {                                                                \
-            q[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx_, o_ * 8 + r * rowB, 0, CP)); \
-            w[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rw, o_ * 4 + r * rowB / 2, 0, 0));        \
+            if constexpr (LAUNDER) {                                                                                    \
+                q[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx_, vq_, 0, CP));              \
+                w[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rw, vw_, 0, 0));                 \
+                vq_ += (unsigned)rowB;                                                                                  \
+                vw_ += (unsigned)rowB / 2;                                                                              \
+                asm volatile("" : "+v"(vq_), "+v"(vw_));                                                                \
+            } else {                                                                                                    \
+                q[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx_, o_ * 8 + r * rowB, 0, CP)); \
+                w[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rw, o_ * 4 + r * rowB / 2, 0, 0)); \
+            }                                                                                                           \
         }                                                                                                               \
     } while (0)
     int tile = blockIdx.x;
@@ -454,67 +511,84 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) void fft_passA_1m_kernel(
             seq0[LS + pad16(t2 * 16 + r)] = v1[r];
         }
         __syncthreads();
-        stage_lds_v<L, 16, 16, 2>(seq0, twl, t2);   // middle stage (two barriers inside)
-        const int b = tile % nb;
-        const long long f = tile / nb;
-        const int col = b * S + 2 * cp;
-        double2 cur[2], step[2];
-#pragma unroll
-        for (int qq = 0; qq < 2; qq++) {
-            const int c = col + qq;
-            const int e0 = c * t, d = 64 * c;   // < 2^16
-            cur[qq] = zmul(wt[e0 >> 8], wt[256 + (e0 & 255)]);
-            step[qq] = zmul(wt[d >> 8], wt[256 + (d & 255)]);
+        // middle stage (radix 16, NS = 16). MIDCOL: one column at a time, 16 values live instead
+        // of 32. Column 1's region is disjoint from column 0's, so its read needs no barrier of its
+        // own.
+        float2 m16[16];
+        if constexpr (MIDCOL) {
+            mid16_read(seq0, twl, t2, m16);
+            __syncthreads();   // every column-0 read is done
+            mid16_write(seq0, t2, m16);
+            mid16_read(seq0 + LS, twl, t2, m16);
+            __syncthreads();   // every column-1 read done
+            mid16_write(seq0 + LS, t2, m16);
+            __syncthreads();
+        } else {
+            stage_lds_v<L, 16, 16, 2>(seq0, twl, t2);   // (two barriers inside)
         }
-        // last stage (radix 4, NS = 256): outputs k1 = t + 64 m, m = b4 + 4 r, kept in registers
-        float2 y[2][16];
+        int b;
+        long long f;
+        tile_fb<XG>(tile, nb, b, f);
+        const int col = b * S + 2 * cp;
+        const __amdgpu_buffer_rsrc_t rs = brsrc(scratch + (f << logN), NOSTORE ? 0u : 0x7fffffffu);
+        // Stores carry the row step in the per-lane offset and a ZERO soffset. A >64-bit buffer
+        // store with an SGPR soffset gets no wait state before the next VALU write of its data
+        // VGPRs (hipcc's hazard check skips that form, and two 8-B stores get merged into it): it
+        // wrote already-overwritten data, rows of some lanes changing from run to run (DESIGN.md
+        // §3). The offset is advanced through an opaque register so the 16 row offsets are not all
+        // precomputed (register pressure).
+        {
+            double2 cur[2], step[2];
 #pragma unroll
-        for (int qq = 0; qq < 2; qq++)
-#pragma unroll
-            for (int b4 = 0; b4 < 4; b4++) {
-                const int j = t2 + b4 * T;
-                float2 u[4];
-#pragma unroll
-                for (int r = 0; r < 4; r++) u[r] = seq0[qq * LS + pad16(j + r * (L / 4))];
-#pragma unroll
-                for (int r = 1; r < 4; r++) u[r] = cmul(u[r], twl[r * j]);
-                dft4v(u);
-#pragma unroll
-                for (int r = 0; r < 4; r++) y[qq][b4 + 4 * r] = u[r];
+            for (int qq = 0; qq < 2; qq++) {
+                const int c = col + qq;
+                const int e0 = c * t2, d = 64 * c;   // < 2^16
+                cur[qq] = zmul(wt[e0 >> 8], wt[256 + (e0 & 255)]);
+                step[qq] = zmul(wt[d >> 8], wt[256 + (d & 255)]);
             }
-        const __amdgpu_buffer_rsrc_t rs = brsrc(scratch + (f << logN), 0x7fffffffu);
-        const unsigned so = (unsigned)(t * N2 + col) * 8u;
-        // 16-B stores with the row step in the per-lane offset and a ZERO soffset. With the row
-        // step in an SGPR soffset the compiler emits buffer_store_dwordx4 ... s<n> and omits the
-        // wait state a >64-bit store needs before the next VALU instruction overwrites its data
-        // VGPRs (its hazard check skips stores with an SGPR soffset; two 8-B stores get merged
-        // into that same form): the store then wrote already-overwritten data -- rows of some lanes
-        // changing from run to run. The offset is advanced through an opaque
-        // register so the 16 row offsets are not all precomputed (register pressure).
-        unsigned vo = so;
+            // last stage (radix 4, NS = 256): outputs k1 = t + 64 m, m = b4 + 4 r, kept in registers
+            float2 y[2][16];
 #pragma unroll
-        for (int m = 0; m < 16; m++) {
-            const float2 a = cmul(y[0][m], make_float2((float)cur[0].x, (float)cur[0].y));
-            const float2 c = cmul(y[1][m], make_float2((float)cur[1].x, (float)cur[1].y));
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bu4, make_float4(a.x, a.y, c.x, c.y)), rs, vo, 0, 0);
-            vo += (unsigned)rowB;
-            asm volatile("" : "+v"(vo));
-            if (m < 15) {
-                cur[0] = zmul(cur[0], step[0]);
-                cur[1] = zmul(cur[1], step[1]);
+            for (int qq = 0; qq < 2; qq++)
+#pragma unroll
+                for (int b4 = 0; b4 < 4; b4++) {
+                    const int j = t2 + b4 * T;
+                    float2 u[4];
+#pragma unroll
+                    for (int r = 0; r < 4; r++) u[r] = seq0[qq * LS + pad16(j + r * (L / 4))];
+#pragma unroll
+                    for (int r = 1; r < 4; r++) u[r] = cmul(u[r], twl[r * j]);
+                    dft4v(u);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) y[qq][b4 + 4 * r] = u[r];
+                }
+            unsigned vo = (unsigned)(t * N2 + col) * 8u;
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                const float2 a = cmul(y[0][m], make_float2((float)cur[0].x, (float)cur[0].y));
+                const float2 c = cmul(y[1][m], make_float2((float)cur[1].x, (float)cur[1].y));
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bu4, make_float4(a.x, a.y, c.x, c.y)), rs, vo, 0, 0);
+                vo += (unsigned)rowB;
+                asm volatile("" : "+v"(vo));
+                if (m < 15) {
+                    cur[0] = zmul(cur[0], step[0]);
+                    cur[1] = zmul(cur[1], step[1]);
+                }
             }
         }
     }
 }
+#undef SDRGPU_PA1M_ISSUE
 
 // ---- 1M pass B, persistent and software-pipelined (N2 = 1024) -------------------------------
 // Same transform as fft_passB_kernel<1024, S>, each workgroup walking tiles with the next tile's
 // 16 row values per thread loaded while the current tile is transformed and stored.
-template <int S, int CP>
+template <int S, int CP, int VAR = 0>   // VAR (measurement only): 16 loads tile 0 only, 32 stores dropped
 __global__ __launch_bounds__(S * 1024 / 16) void fft_passB_1m_kernel(const float2* __restrict__ scratch, int frames, int N1,
                                                                     int logN, const float2* __restrict__ tw,
                                                                     float* __restrict__ out) {
     constexpr int L = 1024, T = L / 16;
+    constexpr int XG = (VAR & 64) ? 32 / S : 1;   // XCD grouping of row blocks (bit 6): 128-B dB lines
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     float2* twl = lds + S * Lds<L>::LS;   // stage twiddles, staged once per workgroup
     const int tid = threadIdx.x;
@@ -525,8 +599,10 @@ __global__ __launch_bounds__(S * 1024 / 16) void fft_passB_1m_kernel(const float
     float2 fr[16];
 #define SDRGPU_PB1M_ISSUE(TILE)                                                                                       \
     do {                                                                                                              \
-        const int b_ = (TILE) % nb;                                                                                   \
-        const long long f_ = (TILE) / nb;                                                                             \
+        int b_;                                                                                                       \
+        long long f_;                                                                                                 \
+        tile_fb<XG>((TILE), nb, b_, f_);                                                                              \
+        if (VAR & 16) { b_ = 0; f_ = 0; }                                                                             \
         const __amdgpu_buffer_rsrc_t rs_ = brsrc(scratch + (f_ << logN), 0x7fffffffu);                                \
         const unsigned o_ = (unsigned)((b_ * S + sF) * L + tF) * 8u;                                                  \
         _Pragma("unroll") for (int r = 0; r < 16; r++)                                                               \
@@ -547,9 +623,10 @@ __global__ __launch_bounds__(S * 1024 / 16) void fft_passB_1m_kernel(const float
         __syncthreads();   // the previous tile's last LDS reads are done
         stage_first<L>(lds + sF2 * Lds<L>::LS, v, tF2);
         __syncthreads();
-        const int b = tile % nb;
-        const long long f = tile / nb;
-        const __amdgpu_buffer_rsrc_t ro = brsrc(out + (f << logN) + b * S, 0x7fffffffu);
+        int b;
+        long long f;
+        tile_fb<XG>(tile, nb, b, f);
+        const __amdgpu_buffer_rsrc_t ro = brsrc(out + (f << logN) + b * S, (VAR & 32) ? 0u : 0x7fffffffu);
         stages_rest<L>(lds, twl, sL2, tL2, [&](int k2, float2 y) {
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, db_of(y)), ro, (unsigned)(sL2 + N1 * k2) * 4u, 0, CP);
         });
@@ -688,6 +765,13 @@ struct FftPlan {
     int sa2 = 0;                      // paired pass-A columns per workgroup (0: paired kernel off)
     int pipe1m = 1;                   // N1 = N2 = 1024: persistent software-pipelined passes (SDRGPU_FFT_1M=0 off)
     int gridA = 0, gridB = 0;         // their grids (resident workgroups)
+    int var1m = 0;                    // pass-A variant (SDRGPU_FFT_1M_VAR, tuning: fft_passA_1m_kernel's VAR)
+    int var1mB = 64;                  // pass-B variant (SDRGPU_FFT_1M_VARB, tuning: 64 XCD grouping; 16 / 32 measurement only)
+    // columns / rows per workgroup of the 1M passes (SDRGPU_FFT_1M_SA / SB, tuning). Pass B at 8
+    // rows (2 workgroups per CU) with XCD-grouped row blocks (4 blocks whose 32-B dB segments share
+    // 128-B lines on one XCD): 1.93 vs 1.97 ms per C2 step (3 interleaved runs on each of two boxes);
+    // without the grouping 2.06. Pass A at 8 columns: 2.24 (XCD-grouped) / 2.70 ms.
+    int sA1m = 16, sB1m = 8;
     DevBuf wt;                        // fp64 W_N^(256 j), W_N^j (j < 256) for the 1M pass A
     hipStream_t own = nullptr;
     PinnedBuf pin_in, pin_out;
@@ -790,10 +874,10 @@ static int launch_merged(const FftPlan& p, const float2* scratchB, int framesB, 
     return SDRGPU_OK;
 }
 
-template <int S, int CP>
+template <int S, int CP, int VAR>
 static int launch_passA_1m(FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
     if (p.N2 % S) { set_error("fft: N2 %d not a multiple of %d columns", p.N2, S); return SDRGPU_ESTATE; }
-    auto k = fft_passA_1m_kernel<S, CP>;
+    auto k = fft_passA_1m_kernel<S, CP, VAR>;
     size_t lds = sizeof(float2) * (S * Lds<1024>::LS + 1024);
     SDRGPU_CHECK(set_lds(k, lds));
     if (!p.gridA) {
@@ -809,9 +893,9 @@ static int launch_passA_1m(FftPlan& p, const float2* in, long long stride, int f
     return SDRGPU_OK;
 }
 
-template <int S, int CP>
+template <int S, int CP, int VAR = 0>
 static int launch_passB_1m(FftPlan& p, int frames, float* out, hipStream_t s) {
-    auto k = fft_passB_1m_kernel<S, CP>;
+    auto k = fft_passB_1m_kernel<S, CP, VAR>;
     size_t lds = sizeof(float2) * (S * Lds<1024>::LS + 1024);
     SDRGPU_CHECK(set_lds(k, lds));
     if (!p.gridB) {
@@ -976,6 +1060,10 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         p.sa2 = p.N1 >= 512 ? 16 : 0;
         if (const char* e = tuning_env("SDRGPU_FFT_SA2")) p.sa2 = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_1M")) p.pipe1m = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_1M_VAR")) p.var1m = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_1M_VARB")) p.var1mB = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_1M_SA")) p.sA1m = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_1M_SB")) p.sB1m = atoi(e);
         if (rc >= 0 && p.N1 == 1024 && p.N2 == 1024) {   // fp64 W_N^(256 j), W_N^j for the 1M pass A
             std::vector<double2> t(512);
             for (int j = 0; j < 256; j++) {
@@ -1091,11 +1179,30 @@ static int fft_execute(sdrgpu_fft* h, const void* in, long long frameStride, int
         if (pipe && c >= 2) SDRGPU_HIP(hipStreamWaitEvent(s, p.evB[b], 0));   // buffer b free again
         if (pipe1m_ok(p, paired) && !pipe) {
             if (p.pipe1m == 2) {   // (tuning) non-temporal streaming accesses
-                SDRGPU_CHECK((launch_passA_1m<16, 2>(p, xc, frameStride, nf, s)));
+                SDRGPU_CHECK((launch_passA_1m<16, 2, 0>(p, xc, frameStride, nf, s)));
                 SDRGPU_CHECK((launch_passB_1m<16, 2>(p, nf, out + (long long)f0 * p.N, s)));
             } else {
-                SDRGPU_CHECK((launch_passA_1m<16, 0>(p, xc, frameStride, nf, s)));
-                SDRGPU_CHECK((launch_passB_1m<16, 0>(p, nf, out + (long long)f0 * p.N, s)));
+                if (p.sA1m == 8) {
+                    if (p.var1m == 73) SDRGPU_CHECK((launch_passA_1m<8, 0, 73>(p, xc, frameStride, nf, s)));
+                    else if (p.var1m & 64) SDRGPU_CHECK((launch_passA_1m<8, 0, 64>(p, xc, frameStride, nf, s)));
+                    else SDRGPU_CHECK((launch_passA_1m<8, 0, 0>(p, xc, frameStride, nf, s)));
+                } else switch (p.var1m) {
+                case 9: SDRGPU_CHECK((launch_passA_1m<16, 0, 9>(p, xc, frameStride, nf, s))); break;
+                case 16: SDRGPU_CHECK((launch_passA_1m<16, 0, 16>(p, xc, frameStride, nf, s))); break;
+                case 32: SDRGPU_CHECK((launch_passA_1m<16, 0, 32>(p, xc, frameStride, nf, s))); break;
+                case 48: SDRGPU_CHECK((launch_passA_1m<16, 0, 48>(p, xc, frameStride, nf, s))); break;
+                default: SDRGPU_CHECK((launch_passA_1m<16, 0, 0>(p, xc, frameStride, nf, s))); break;
+                }
+                if (p.sB1m == 8) {
+                    if (p.var1mB & 64) SDRGPU_CHECK((launch_passB_1m<8, 0, 64>(p, nf, out + (long long)f0 * p.N, s)));
+                    else SDRGPU_CHECK((launch_passB_1m<8, 0, 0>(p, nf, out + (long long)f0 * p.N, s)));
+                } else switch (p.var1mB) {
+                case 64: SDRGPU_CHECK((launch_passB_1m<16, 0, 64>(p, nf, out + (long long)f0 * p.N, s))); break;
+                case 16: SDRGPU_CHECK((launch_passB_1m<16, 0, 16>(p, nf, out + (long long)f0 * p.N, s))); break;
+                case 32: SDRGPU_CHECK((launch_passB_1m<16, 0, 32>(p, nf, out + (long long)f0 * p.N, s))); break;
+                case 48: SDRGPU_CHECK((launch_passB_1m<16, 0, 48>(p, nf, out + (long long)f0 * p.N, s))); break;
+                default: SDRGPU_CHECK((launch_passB_1m<16, 0>(p, nf, out + (long long)f0 * p.N, s))); break;
+                }
             }
             continue;
         }
