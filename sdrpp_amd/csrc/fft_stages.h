@@ -14,6 +14,24 @@ __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 mul_negi(float2 a) { return make_float2(a.y, -a.x); }   // a * (-i)
 
+// a + (-i) b = (a.x + b.y, a.y - b.x) and a - (-i) b = (a.x - b.y, a.y + b.x) as ONE packed add
+// each (src1 halves swapped by op_sel, one half negated). Left to itself the compiler forms both
+// cross sums in two packed adds and assembles the results with four moves (r3: 439 v_mov_b32 in
+// the 1M pass A's 1,900 VALU instructions).
+typedef float pk2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float2 add_negi(float2 a, float2 b) {
+    pk2 r;
+    const pk2 x = {a.x, a.y}, y = {b.x, b.y};
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(x), "v"(y));
+    return make_float2(r.x, r.y);
+}
+__device__ __forceinline__ float2 sub_negi(float2 a, float2 b) {
+    pk2 r;
+    const pk2 x = {a.x, a.y}, y = {b.x, b.y};
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(x), "v"(y));
+    return make_float2(r.x, r.y);
+}
+
 // ---- small forward DFTs in registers (e^{-i}) ------------------------------
 __device__ __forceinline__ void dft2(float2* v) {
     float2 a = v[0], b = v[1];
@@ -21,11 +39,11 @@ __device__ __forceinline__ void dft2(float2* v) {
     v[1] = csub(a, b);
 }
 __device__ __forceinline__ void dft4(float2& x0, float2& x1, float2& x2, float2& x3) {
-    float2 a0 = cadd(x0, x2), a1 = csub(x0, x2), a2 = cadd(x1, x3), a3 = mul_negi(csub(x1, x3));
+    float2 a0 = cadd(x0, x2), a1 = csub(x0, x2), a2 = cadd(x1, x3), d13 = csub(x1, x3);
     x0 = cadd(a0, a2);
     x2 = csub(a0, a2);
-    x1 = cadd(a1, a3);
-    x3 = csub(a1, a3);
+    x1 = add_negi(a1, d13);   // a1 + (-i)(x1 - x3)
+    x3 = sub_negi(a1, d13);
 }
 __device__ __forceinline__ void dft4v(float2* v) { dft4(v[0], v[1], v[2], v[3]); }
 
@@ -36,11 +54,10 @@ __device__ __forceinline__ void dft8(float2* v) {
     dft4(e0, e1, e2, e3);
     dft4(o0, o1, o2, o3);
     o1 = make_float2(R2 * (o1.x + o1.y), R2 * (o1.y - o1.x));   // * W8^1 = (1-i)/sqrt2
-    o2 = mul_negi(o2);                                           // * W8^2 = -i
     o3 = make_float2(R2 * (o3.y - o3.x), -R2 * (o3.x + o3.y));   // * W8^3 = (-1-i)/sqrt2
     v[0] = cadd(e0, o0); v[4] = csub(e0, o0);
     v[1] = cadd(e1, o1); v[5] = csub(e1, o1);
-    v[2] = cadd(e2, o2); v[6] = csub(e2, o2);
+    v[2] = add_negi(e2, o2); v[6] = sub_negi(e2, o2);            // o2 * W8^2 = o2 * (-i)
     v[3] = cadd(e3, o3); v[7] = csub(e3, o3);
 }
 
@@ -58,7 +75,6 @@ __device__ __forceinline__ void dft16(float2* v) {
     y[1][2] = cmul(y[1][2], make_float2(R2, -R2));
     y[1][3] = cmul(y[1][3], make_float2(S1, -C1));
     y[2][1] = cmul(y[2][1], make_float2(R2, -R2));
-    y[2][2] = mul_negi(y[2][2]);
     y[2][3] = cmul(y[2][3], make_float2(-R2, -R2));
     y[3][1] = cmul(y[3][1], make_float2(S1, -C1));
     y[3][2] = cmul(y[3][2], make_float2(-R2, -R2));
@@ -66,7 +82,15 @@ __device__ __forceinline__ void dft16(float2* v) {
 #pragma unroll
     for (int k1 = 0; k1 < 4; k1++) {
         float2 a = y[0][k1], b = y[1][k1], c = y[2][k1], d = y[3][k1];
-        dft4(a, b, c, d);
+        if (k1 == 2) {   // c = y[2][2] * W16^4 = y[2][2] * (-i), folded into the first butterfly
+            const float2 a0 = add_negi(a, c), a1 = sub_negi(a, c), a2 = cadd(b, d), d13 = csub(b, d);
+            a = cadd(a0, a2);
+            c = csub(a0, a2);
+            b = add_negi(a1, d13);
+            d = sub_negi(a1, d13);
+        } else {
+            dft4(a, b, c, d);
+        }
         v[k1] = a; v[k1 + 4] = b; v[k1 + 8] = c; v[k1 + 12] = d;
     }
 }
