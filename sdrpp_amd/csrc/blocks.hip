@@ -552,21 +552,29 @@ __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
     float2 ph0 = make_float2(1.f, 0.f);
     // the row-step table through the constant address space: scalar (SMEM) loads
     const __attribute__((address_space(4))) float* nstep = (const __attribute__((address_space(4))) float*)a.nstep;
-    if constexpr (XL) {
-        if (interior) ph0 = nco_inline(a, b0 - a.H + p);
-    }
+    // phasor of the segment's first input sample (index b0 - H + p of `in`; negative inside the
+    // history, where the formula still holds: coarse index floor(i / 4096), fine index i mod 4096)
+    if constexpr (XL) ph0 = nco_inline(a, b0 - a.H + p);
     float2* __restrict__ out2 = reinterpret_cast<float2*>(a.out);
     float* __restrict__ outf = reinterpret_cast<float*>(a.out);
     // interior segments load unconditionally (BT row loads in flight); the few segments touching
     // the history or the end of the call fetch element-wise
     auto body = [&](auto fast) {
         constexpr bool F = decltype(fast)::value;
-        auto row = [&](int r) -> float2 {   // raw row sample (the slow path applies the xlator itself)
+        auto row = [&](int r) -> float2 {   // raw row sample (history samples are stored translated)
             if constexpr (F) return src[D * r];
-            else return fir_fetch<float2, XL, false>(a, b0 + (long long)D * r + p);
+            else return fir_fetch<float2, false, false>(a, b0 + (long long)D * r + p);
         };
-        auto xlate = [&](float2 x, int r) -> float2 {   // fused xlator of the fast path: e^{i w D r}
-            if constexpr (F && XL) x = cmulf(x, cmulf(ph0, make_float2(nstep[2 * r], nstep[2 * r + 1])));
+        // fused xlator: e^{i w (i0 + D r)} = ph0 e^{i w D r} on `in` samples. Edge segments (the
+        // history at the front, the call's end) use the same phasors: forming each one in fp64
+        // (nco_inline per sample) made the two edge segments of a reference-size block take
+        // ~3x as long as the rest of the launch (r3 per-call trace)
+        auto xlate = [&](float2 x, int r) -> float2 {
+            if constexpr (XL) {
+                const float2 y = cmulf(x, cmulf(ph0, make_float2(nstep[2 * r], nstep[2 * r + 1])));
+                if constexpr (F) x = y;
+                else x = (b0 + (long long)D * r + p >= a.H) ? y : x;
+            }
             return x;
         };
         float2 P[QP];   // P[k], k >= 1: the open partial of output (r - k) before row r

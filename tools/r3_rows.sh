@@ -1,0 +1,13 @@
+#!/bin/bash
+# Stage-1 rows kernel with row-step phasors on the edge segments: full -m gpu suite, per-call
+# timing, a kernel trace of the per-call sequence, and the C5 bench.
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; OUT=$R/gpurun_out; TAG=${1:-rows}; mkdir -p $OUT
+st() { echo "$1 rc=$2 $(date +%T)" >> $OUT/${TAG}_status.txt; case "$2" in 0) ;; *) exit "$2";; esac; }
+echo "start $(date +%T)" > $OUT/${TAG}_status.txt
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/${TAG}_tests.log 2>&1
+st tests $?
+for k in 1 2; do timeout -k 10 300 python tools/per_call.py 300 single > $OUT/${TAG}_pc_$k.json 2>&1; st pc$k $?; done
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/${TAG}_trace -o run -- python3 $R/tools/per_call.py 60 single > $OUT/${TAG}_trace.log 2>&1)
+st trace $?
+for k in 1 2; do timeout -k 10 300 python bench.py --config c5 --steps 20 --no-cpu --no-sub > $OUT/${TAG}_c5_$k.json 2>&1; st c5_$k $?; done
+echo "all done $(date +%T)" >> $OUT/${TAG}_status.txt
