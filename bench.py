@@ -367,11 +367,13 @@ def per_call_c5(dev, stream, calls=300, block=307200, single_only=False):
     t0 = time.perf_counter()
     for k in range(calls):
         one(k)
+    issue_us = (time.perf_counter() - t0) / calls * 1e6   # host time to issue a call's launches
     torch.cuda.synchronize()
     dev_us = (time.perf_counter() - t0) / calls * 1e6
     if single_only:
         fe.close()
-        return {"block": block, "us_per_call_device": round(dev_us, 1), "MSps_device": round(block / dev_us, 1)}
+        return {"block": block, "us_per_call_device": round(dev_us, 1), "MSps_device": round(block / dev_us, 1),
+                "us_per_call_host_issue": round(issue_us, 1)}
     # K independent block streams on K HIP streams (one SDR each): each call's kernels fill only a
     # few CUs, so concurrent streams overlap on the device
     K = 16
@@ -398,6 +400,7 @@ def per_call_c5(dev, stream, calls=300, block=307200, single_only=False):
     multi_us = (time.perf_counter() - t0) / rounds * 1e6
     for f in fes:
         f.close()
+    out_issue = round(issue_us, 1)
     xh = x[:2 * block].cpu().numpy().view(np.complex64)
     fe.push(xh)
     t0 = time.perf_counter()
@@ -434,7 +437,7 @@ def per_call_c5(dev, stream, calls=300, block=307200, single_only=False):
     fe.close()
     # PCIe floor of a block: its 2.46 MB H2D + the rows / VFO read-back, at the measured copy rate
     return {"block": block, "us_per_call_device": round(dev_us, 1), "MSps_device": round(block / dev_us, 1),
-            "concurrent_streams": K, "MSps_device_concurrent": round(K * block / multi_us, 1),
+            "us_per_call_host_issue": out_issue, "concurrent_streams": K, "MSps_device_concurrent": round(K * block / multi_us, 1),
             "us_per_call_host_dropin": round(host_us, 1), "MSps_host_dropin": round(block / host_us, 1),
             "us_per_call_host_sync": round(sync_us, 1),
             "note": "one 307,200-sample block per call (fs/200 at 61.44 MS/s) through the device front end "
