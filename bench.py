@@ -101,7 +101,8 @@ class C2:
         self.spectra = torch.empty(self.frames * self.N, dtype=torch.float32, device="cuda")
         self.bytes_per_sample = 8 + 4 * self.N / self.NZ
         self.kernel_bytes = self.bytes_per_sample * self.B
-        self.kernel_name = "spectrum N=2^20, nz=1e6: fft_passA2_kernel<1024,16> + fft_passB_kernel<1024,16> per 16-frame chunk"
+        self.kernel_name = ("spectrum N=2^20, nz=1e6: fft_passA_1m_kernel<16,0,128> (persistent, tile-major intermediate) + "
+                            "fft_passB_1m_kernel<8,0,192> (persistent, XCD-grouped rows) per 16-frame chunk")
 
     def dominant(self, x, s):
         self.fft.execute_dev(x.data_ptr(), self.NZ, self.frames, self.spectra.data_ptr(), s)

@@ -446,6 +446,9 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_
     constexpr bool MIDCOL = VAR & 1, LAUNDER = VAR & 8;
     constexpr bool NOLOAD = VAR & 16, NOSTORE = VAR & 32;   // (measurement only: wrong results)
     constexpr int XG = ((VAR & 64) && S < 16) ? 16 / S : 1;   // XCD grouping of column blocks (bit 6): 128-B row lines
+    // bit 7: tile-major intermediate [b][k1][c] (each tile's 128 KB written contiguously; pass B
+    // then reads 128-B pieces of 16 columns) instead of row-major [k1][n2]
+    constexpr bool TMAJ = VAR & 128;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     float2* twl = lds + S * LS;
     const int tid = threadIdx.x;
@@ -562,13 +565,14 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_
 #pragma unroll
                     for (int r = 0; r < 4; r++) y[qq][b4 + 4 * r] = u[r];
                 }
-            unsigned vo = (unsigned)(t * N2 + col) * 8u;
+            unsigned vo = TMAJ ? (unsigned)(b * L * S + t * S + 2 * cp) * 8u : (unsigned)(t * N2 + col) * 8u;
+            const unsigned mstep = TMAJ ? (unsigned)(T * S * 8) : (unsigned)rowB;
 #pragma unroll
             for (int m = 0; m < 16; m++) {
                 const float2 a = cmul(y[0][m], make_float2((float)cur[0].x, (float)cur[0].y));
                 const float2 c = cmul(y[1][m], make_float2((float)cur[1].x, (float)cur[1].y));
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bu4, make_float4(a.x, a.y, c.x, c.y)), rs, vo, 0, 0);
-                vo += (unsigned)rowB;
+                vo += mstep;
                 asm volatile("" : "+v"(vo));
                 if (m < 15) {
                     cur[0] = zmul(cur[0], step[0]);
@@ -589,6 +593,7 @@ __global__ __launch_bounds__(S * 1024 / 16) void fft_passB_1m_kernel(const float
                                                                     float* __restrict__ out) {
     constexpr int L = 1024, T = L / 16;
     constexpr int XG = (VAR & 64) ? 32 / S : 1;   // XCD grouping of row blocks (bit 6): 128-B dB lines
+    constexpr bool TMAJ = VAR & 128;              // bit 7: the tile-major intermediate of pass A at 16 columns
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     float2* twl = lds + S * Lds<L>::LS;   // stage twiddles, staged once per workgroup
     const int tid = threadIdx.x;
@@ -604,9 +609,10 @@ __global__ __launch_bounds__(S * 1024 / 16) void fft_passB_1m_kernel(const float
         tile_fb<XG>((TILE), nb, b_, f_);                                                                              \
         if (VAR & 16) { b_ = 0; f_ = 0; }                                                                             \
         const __amdgpu_buffer_rsrc_t rs_ = brsrc(scratch + (f_ << logN), 0x7fffffffu);                                \
-        const unsigned o_ = (unsigned)((b_ * S + sF) * L + tF) * 8u;                                                  \
+        const unsigned o_ = TMAJ ? (unsigned)((tF / 16) * L * 16 + (b_ * S + sF) * 16 + tF % 16) * 8u                 \
+                                 : (unsigned)((b_ * S + sF) * L + tF) * 8u;                                            \
         _Pragma("unroll") for (int r = 0; r < 16; r++)                                                               \
-            fr[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs_, o_, r * T * 8, CP)); \
+            fr[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs_, o_, r * (TMAJ ? 4 * L * 16 * 8 : T * 8), CP)); \
     } while (0)
     int tile = blockIdx.x;
     if (tile < ntiles) SDRGPU_PB1M_ISSUE(tile);
@@ -765,7 +771,11 @@ struct FftPlan {
     int sa2 = 0;                      // paired pass-A columns per workgroup (0: paired kernel off)
     int pipe1m = 1;                   // N1 = N2 = 1024: persistent software-pipelined passes (SDRGPU_FFT_1M=0 off)
     int gridA = 0, gridB = 0;         // their grids (resident workgroups)
-    int var1m = 0;                    // pass-A variant (SDRGPU_FFT_1M_VAR, tuning: fft_passA_1m_kernel's VAR)
+    // pass-A variant (SDRGPU_FFT_1M_VAR, tuning: fft_passA_1m_kernel's VAR). Default 128: the
+    // tile-major intermediate (each pass-A tile's 128 KB written contiguously, 1 KB per store
+    // instruction instead of eight 128-B row pieces; pass B reads 16-column pieces of 128 B):
+    // 1.89 vs 1.94 ms per C2 step (3 interleaved runs, one box)
+    int var1m = 128;
     int var1mB = 64;                  // pass-B variant (SDRGPU_FFT_1M_VARB, tuning: 64 XCD grouping; 16 / 32 measurement only)
     // columns / rows per workgroup of the 1M passes (SDRGPU_FFT_1M_SA / SB, tuning). Pass B at 8
     // rows (2 workgroups per CU) with XCD-grouped row blocks (4 blocks whose 32-B dB segments share
@@ -909,6 +919,40 @@ static int launch_passB_1m(FftPlan& p, int frames, float* out, hipStream_t s) {
                        p.tw2.as<float2>(), out);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
+}
+
+// the persistent 1M passes for one chunk, with the tuning variants. Pass B reads the layout pass A
+// wrote: tile-major (pass A VAR 128, the default) or row-major (every other variant).
+static int dispatch_1m(FftPlan& p, const float2* xc, long long stride, int nf, float* o, hipStream_t s) {
+    if (p.pipe1m == 2) {   // (tuning) non-temporal streaming accesses, row-major
+        SDRGPU_CHECK((launch_passA_1m<16, 2, 0>(p, xc, stride, nf, s)));
+        return launch_passB_1m<16, 2>(p, nf, o, s);
+    }
+    bool tm = false;
+    if (p.sA1m == 8) {
+        if (p.var1m == 73) SDRGPU_CHECK((launch_passA_1m<8, 0, 73>(p, xc, stride, nf, s)));
+        else if (p.var1m & 64) SDRGPU_CHECK((launch_passA_1m<8, 0, 64>(p, xc, stride, nf, s)));
+        else SDRGPU_CHECK((launch_passA_1m<8, 0, 0>(p, xc, stride, nf, s)));
+    } else {
+        switch (p.var1m) {
+        case 128: SDRGPU_CHECK((launch_passA_1m<16, 0, 128>(p, xc, stride, nf, s))); tm = true; break;
+        case 137: SDRGPU_CHECK((launch_passA_1m<16, 0, 137>(p, xc, stride, nf, s))); tm = true; break;
+        case 9: SDRGPU_CHECK((launch_passA_1m<16, 0, 9>(p, xc, stride, nf, s))); break;
+        case 16: SDRGPU_CHECK((launch_passA_1m<16, 0, 16>(p, xc, stride, nf, s))); break;
+        case 32: SDRGPU_CHECK((launch_passA_1m<16, 0, 32>(p, xc, stride, nf, s))); break;
+        case 48: SDRGPU_CHECK((launch_passA_1m<16, 0, 48>(p, xc, stride, nf, s))); break;
+        default: SDRGPU_CHECK((launch_passA_1m<16, 0, 0>(p, xc, stride, nf, s))); break;
+        }
+    }
+    if (tm) return p.sB1m == 8 ? launch_passB_1m<8, 0, 64 | 128>(p, nf, o, s) : launch_passB_1m<16, 0, 128>(p, nf, o, s);
+    if (p.sB1m == 8) return (p.var1mB & 64) ? launch_passB_1m<8, 0, 64>(p, nf, o, s) : launch_passB_1m<8, 0, 0>(p, nf, o, s);
+    switch (p.var1mB) {
+    case 64: return launch_passB_1m<16, 0, 64>(p, nf, o, s);
+    case 16: return launch_passB_1m<16, 0, 16>(p, nf, o, s);
+    case 32: return launch_passB_1m<16, 0, 32>(p, nf, o, s);
+    case 48: return launch_passB_1m<16, 0, 48>(p, nf, o, s);
+    default: return launch_passB_1m<16, 0>(p, nf, o, s);
+    }
 }
 
 static bool pipe1m_ok(const FftPlan& p, bool paired) { return p.pipe1m && paired && p.N1 == 1024 && p.N2 == 1024 && (p.nz % 2) == 0; }
@@ -1178,32 +1222,7 @@ static int fft_execute(sdrgpu_fft* h, const void* in, long long frameStride, int
         p.cur = b ? p.scratch2.as<float2>() : p.scratch.as<float2>();
         if (pipe && c >= 2) SDRGPU_HIP(hipStreamWaitEvent(s, p.evB[b], 0));   // buffer b free again
         if (pipe1m_ok(p, paired) && !pipe) {
-            if (p.pipe1m == 2) {   // (tuning) non-temporal streaming accesses
-                SDRGPU_CHECK((launch_passA_1m<16, 2, 0>(p, xc, frameStride, nf, s)));
-                SDRGPU_CHECK((launch_passB_1m<16, 2>(p, nf, out + (long long)f0 * p.N, s)));
-            } else {
-                if (p.sA1m == 8) {
-                    if (p.var1m == 73) SDRGPU_CHECK((launch_passA_1m<8, 0, 73>(p, xc, frameStride, nf, s)));
-                    else if (p.var1m & 64) SDRGPU_CHECK((launch_passA_1m<8, 0, 64>(p, xc, frameStride, nf, s)));
-                    else SDRGPU_CHECK((launch_passA_1m<8, 0, 0>(p, xc, frameStride, nf, s)));
-                } else switch (p.var1m) {
-                case 9: SDRGPU_CHECK((launch_passA_1m<16, 0, 9>(p, xc, frameStride, nf, s))); break;
-                case 16: SDRGPU_CHECK((launch_passA_1m<16, 0, 16>(p, xc, frameStride, nf, s))); break;
-                case 32: SDRGPU_CHECK((launch_passA_1m<16, 0, 32>(p, xc, frameStride, nf, s))); break;
-                case 48: SDRGPU_CHECK((launch_passA_1m<16, 0, 48>(p, xc, frameStride, nf, s))); break;
-                default: SDRGPU_CHECK((launch_passA_1m<16, 0, 0>(p, xc, frameStride, nf, s))); break;
-                }
-                if (p.sB1m == 8) {
-                    if (p.var1mB & 64) SDRGPU_CHECK((launch_passB_1m<8, 0, 64>(p, nf, out + (long long)f0 * p.N, s)));
-                    else SDRGPU_CHECK((launch_passB_1m<8, 0, 0>(p, nf, out + (long long)f0 * p.N, s)));
-                } else switch (p.var1mB) {
-                case 64: SDRGPU_CHECK((launch_passB_1m<16, 0, 64>(p, nf, out + (long long)f0 * p.N, s))); break;
-                case 16: SDRGPU_CHECK((launch_passB_1m<16, 0, 16>(p, nf, out + (long long)f0 * p.N, s))); break;
-                case 32: SDRGPU_CHECK((launch_passB_1m<16, 0, 32>(p, nf, out + (long long)f0 * p.N, s))); break;
-                case 48: SDRGPU_CHECK((launch_passB_1m<16, 0, 48>(p, nf, out + (long long)f0 * p.N, s))); break;
-                default: SDRGPU_CHECK((launch_passB_1m<16, 0>(p, nf, out + (long long)f0 * p.N, s))); break;
-                }
-            }
+            SDRGPU_CHECK(dispatch_1m(p, xc, frameStride, nf, out + (long long)f0 * p.N, s));
             continue;
         }
         if (paired) SDRGPU_CHECK(dispatch_passA2(p, xc, frameStride, nf, s));

@@ -4,7 +4,7 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; OUT=$R/gpurun_out; TAG=${1:-c2s}; mkdir -p $OUT
 st() { echo "$1 rc=$2 $(date +%T)" >> $OUT/${TAG}_status.txt; case "$2" in 0) ;; *) exit "$2";; esac; }
 echo "start $(date +%T)" > $OUT/${TAG}_status.txt
-CFGS="${CFGS:-base:16:0:16:0 b8x:16:0:8:64 a8x:8:64:16:0 a8x73:8:73:16:0 a8x73b8x:8:73:8:64}"
+CFGS="${CFGS:-base:16:128:8:64 b16:16:128:16:0 a137:16:137:8:64 rowmaj:16:0:8:64}"
 for c in $CFGS; do IFS=: read n sa va sb vb <<< "$c"
   SDRGPU_TUNING=1 SDRGPU_FFT_1M_SA=$sa SDRGPU_FFT_1M_VAR=$va SDRGPU_FFT_1M_SB=$sb SDRGPU_FFT_1M_VARB=$vb timeout -k 10 300 \
     python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "1m or c2 or multi_chunk" > $OUT/${TAG}_tests_$n.log 2>&1
