@@ -937,6 +937,9 @@ static int dispatch_1m(FftPlan& p, const float2* xc, long long stride, int nf, f
         switch (p.var1m) {
         case 128: SDRGPU_CHECK((launch_passA_1m<16, 0, 128>(p, xc, stride, nf, s))); tm = true; break;
         case 137: SDRGPU_CHECK((launch_passA_1m<16, 0, 137>(p, xc, stride, nf, s))); tm = true; break;
+        case 144: SDRGPU_CHECK((launch_passA_1m<16, 0, 144>(p, xc, stride, nf, s))); tm = true; break;   // (measurement)
+        case 160: SDRGPU_CHECK((launch_passA_1m<16, 0, 160>(p, xc, stride, nf, s))); tm = true; break;
+        case 176: SDRGPU_CHECK((launch_passA_1m<16, 0, 176>(p, xc, stride, nf, s))); tm = true; break;
         case 9: SDRGPU_CHECK((launch_passA_1m<16, 0, 9>(p, xc, stride, nf, s))); break;
         case 16: SDRGPU_CHECK((launch_passA_1m<16, 0, 16>(p, xc, stride, nf, s))); break;
         case 32: SDRGPU_CHECK((launch_passA_1m<16, 0, 32>(p, xc, stride, nf, s))); break;
@@ -944,7 +947,14 @@ static int dispatch_1m(FftPlan& p, const float2* xc, long long stride, int nf, f
         default: SDRGPU_CHECK((launch_passA_1m<16, 0, 0>(p, xc, stride, nf, s))); break;
         }
     }
-    if (tm) return p.sB1m == 8 ? launch_passB_1m<8, 0, 64 | 128>(p, nf, o, s) : launch_passB_1m<16, 0, 128>(p, nf, o, s);
+    if (tm) {
+        switch (p.var1mB) {   // (16 / 32 / 48: measurement only)
+        case 16: return launch_passB_1m<8, 0, 64 | 128 | 16>(p, nf, o, s);
+        case 32: return launch_passB_1m<8, 0, 64 | 128 | 32>(p, nf, o, s);
+        case 48: return launch_passB_1m<8, 0, 64 | 128 | 48>(p, nf, o, s);
+        }
+        return p.sB1m == 8 ? launch_passB_1m<8, 0, 64 | 128>(p, nf, o, s) : launch_passB_1m<16, 0, 128>(p, nf, o, s);
+    }
     if (p.sB1m == 8) return (p.var1mB & 64) ? launch_passB_1m<8, 0, 64>(p, nf, o, s) : launch_passB_1m<8, 0, 0>(p, nf, o, s);
     switch (p.var1mB) {
     case 64: return launch_passB_1m<16, 0, 64>(p, nf, o, s);
