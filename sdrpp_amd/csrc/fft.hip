@@ -41,9 +41,10 @@ __device__ __forceinline__ float db_of(float2 X) {
 // blockIdx.x, +gridDim.x, ...; the 16 raw loads of tile i+1 (Frag) are issued before tile i
 // is transformed and stored, so HBM latency overlaps the LDS exchange, the math and the
 // stores of the previous tile (one register fragment in flight per thread).
-template <int L, class Frag, class Issue, class Finish, class Store>
+template <int L, class Frag, bool T16 = false, class Issue, class Finish, class Store>
 __device__ __forceinline__ void tile_loop(float2* lds, const float2* __restrict__ tw, int tile, int ntiles, int sF, int tF,
-                                          int sL, int tL, Issue&& issue, Finish&& finish, Store&& store) {
+                                          int sL, int tL, Issue&& issue, Finish&& finish, Store&& store,
+                                          const float2* tw16 = nullptr) {
     // One tile per workgroup (grid = tiles). A persistent variant with a ping-pong register
     // prefetch of the next tile was measured at the same 64k throughput with a quarter of the
     // occupancy (and spills at N1 = 1024), so the simple form is kept.
@@ -55,10 +56,10 @@ __device__ __forceinline__ void tile_loop(float2* lds, const float2* __restrict_
     finish(fr, v);
     stage_first<L>(lds + sF * LS, v, tF);
     __syncthreads();
-    stages_rest<L>(lds, tw, sL, tL, [&](int k, float2 y, int slot) {
+    stages_rest<L, T16>(lds, tw, sL, tL, [&](int k, float2 y, int slot) {
         if constexpr (std::is_invocable_v<Store&, int, int, float2, int>) store(tile, k, y, slot);
         else store(tile, k, y);
-    });
+    }, tw16);
 }
 
 struct FragW {   // raw input + window values for 16 samples
@@ -162,6 +163,8 @@ __device__ __forceinline__ void passA_tile(
             }
         }
         for (int i = tid; i < L; i += S * T) twl[i] = tw[i];
+        float2* tw16 = twl + L;   // twl[r t] as tw16[16 r + t]: conflict-free across t (stage_lds)
+        stage16_twiddles<L>(tw16, tw, tid, S * T);
 #pragma unroll
         for (int r = 0; r < 16; r++)   // exact W_N^(n2 k1), k1 = t + 16 r: same offsets as the input rows
             tt[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rt, o0 * 8, r * rowB, 0));
@@ -174,7 +177,7 @@ __device__ __forceinline__ void passA_tile(
 #pragma unroll
         for (int r = 0; r < 16; r++) v[r] = seq[pad16(t + 16 * r)];
 #pragma unroll
-        for (int r = 1; r < 16; r++) v[r] = cmul(v[r], twl[r * t]);
+        for (int r = 1; r < 16; r++) v[r] = cmul(v[r], tw16[16 * r + t]);
         dft16(v);
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc((void*)(scratch + (f << logN)), (short)0, 0x7fffffff, 0x00020000);
@@ -230,8 +233,8 @@ __global__ __launch_bounds__(S * L / 16) __attribute__((amdgpu_waves_per_eu(4)))
 // LDS, and one 16-B load of the exact four-step twiddle pair W_N^(n2 k1) from an N-entry
 // [k1][n2] table (L2-resident) instead of a product of two table values. Requires an even
 // frame stride and a 16-B aligned input (checked on the host).
-template <int L, int R, int NS, int V>
-__device__ __forceinline__ void stage_lds_v(float2* seq0, const float2* twl, int t) {
+template <int L, int R, int NS, int V, bool T16 = false>
+__device__ __forceinline__ void stage_lds_v(float2* seq0, const float2* twl, int t, const float2* tw16 = nullptr) {
     constexpr int T = L / 16, BPT = 16 / R, LS = Lds<L>::LS;
     float2 v[V][BPT][R];
 #pragma unroll
@@ -241,8 +244,13 @@ __device__ __forceinline__ void stage_lds_v(float2* seq0, const float2* twl, int
             const int j = t + b * T, jm = j % NS;
 #pragma unroll
             for (int r = 0; r < R; r++) v[q][b][r] = seq0[q * LS + pad16(j + r * (L / R))];
+            if constexpr (T16 && R == 16 && NS == 16) {   // conflict-free layout (stage_lds, fft_stages.h)
 #pragma unroll
-            for (int r = 1; r < R; r++) v[q][b][r] = cmul(v[q][b][r], twl[r * jm * (L / (NS * R))]);
+                for (int r = 1; r < R; r++) v[q][b][r] = cmul(v[q][b][r], tw16[16 * r + jm]);
+            } else {
+#pragma unroll
+                for (int r = 1; r < R; r++) v[q][b][r] = cmul(v[q][b][r], twl[r * jm * (L / (NS * R))]);
+            }
             dft<R>(v[q][b]);
         }
     __syncthreads();
@@ -400,13 +408,13 @@ typedef unsigned bu4 __attribute__((ext_vector_type(4)));
 
 // the radix-16 middle stage (NS = 16) of the 1M pass A for one column, thread t: read + twiddle +
 // DFT into v, then (after the caller's barrier) the in-place write
-__device__ __forceinline__ void mid16_read(const float2* seq, const float2* twl, int t, float2 (&v)[16]) {
+__device__ __forceinline__ void mid16_read(const float2* seq, const float2* tw16, int t, float2 (&v)[16]) {
     constexpr int L = 1024;
     const int jm = t % 16;
 #pragma unroll
     for (int r = 0; r < 16; r++) v[r] = seq[pad16(t + r * (L / 16))];
 #pragma unroll
-    for (int r = 1; r < 16; r++) v[r] = cmul(v[r], twl[r * jm * (L / 256)]);
+    for (int r = 1; r < 16; r++) v[r] = cmul(v[r], tw16[16 * r + jm]);   // (stage_lds's tw16 layout)
     dft16(v);
 }
 __device__ __forceinline__ void mid16_write(float2* seq, int t, const float2 (&v)[16]) {
@@ -451,9 +459,11 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_
     constexpr bool TMAJ = VAR & 128;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     float2* twl = lds + S * LS;
+    float2* tw16 = twl + L;   // the middle stage's twiddles, bank-conflict-free (stage_lds)
     const int tid = threadIdx.x;
     const int cp = tid % P, t = tid / P;
-    for (int i = tid; i < L; i += NT) twl[i] = tw[i];   // (first barrier below orders it)
+    for (int i = tid; i < L; i += NT) twl[i] = tw[i];   // (first barrier below orders both)
+    for (int i = tid; i < 256; i += NT) tw16[i] = tw[(i >> 4) * (i & 15) * (L / 256)];
     const int nb = N2 / S;
     const int ntiles = nb * frames;
     // The input / window resources end at nz, so the zero-padded tail loads return 0 (nz even: a
@@ -519,15 +529,15 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_
         // own.
         float2 m16[16];
         if constexpr (MIDCOL) {
-            mid16_read(seq0, twl, t2, m16);
+            mid16_read(seq0, tw16, t2, m16);
             __syncthreads();   // every column-0 read is done
             mid16_write(seq0, t2, m16);
-            mid16_read(seq0 + LS, twl, t2, m16);
+            mid16_read(seq0 + LS, tw16, t2, m16);
             __syncthreads();   // every column-1 read done
             mid16_write(seq0 + LS, t2, m16);
             __syncthreads();
         } else {
-            stage_lds_v<L, 16, 16, 2>(seq0, twl, t2);   // (two barriers inside)
+            stage_lds_v<L, 16, 16, 2, true>(seq0, twl, t2, tw16);   // (two barriers inside)
         }
         int b;
         long long f;
@@ -596,8 +606,10 @@ __global__ __launch_bounds__(S * 1024 / 16) void fft_passB_1m_kernel(const float
     constexpr bool TMAJ = VAR & 128;              // bit 7: the tile-major intermediate of pass A at 16 columns
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     float2* twl = lds + S * Lds<L>::LS;   // stage twiddles, staged once per workgroup
+    float2* tw16 = twl + L;                // the middle stage's, bank-conflict-free (stage_lds)
     const int tid = threadIdx.x;
-    for (int i = tid; i < L; i += S * T) twl[i] = tw[i];   // (first barrier below orders it)
+    for (int i = tid; i < L; i += S * T) twl[i] = tw[i];   // (first barrier below orders both)
+    for (int i = tid; i < 256; i += S * T) tw16[i] = tw[(i >> 4) * (i & 15) * (L / 256)];
     const int sF = tid / T, tF = tid % T;
     const int nb = N1 / S;
     const int ntiles = nb * frames;
@@ -633,9 +645,9 @@ __global__ __launch_bounds__(S * 1024 / 16) void fft_passB_1m_kernel(const float
         long long f;
         tile_fb<XG>(tile, nb, b, f);
         const __amdgpu_buffer_rsrc_t ro = brsrc(out + (f << logN) + b * S, (VAR & 32) ? 0u : 0x7fffffffu);
-        stages_rest<L>(lds, twl, sL2, tL2, [&](int k2, float2 y) {
+        stages_rest<L, true>(lds, twl, sL2, tL2, [&](int k2, float2 y) {
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, db_of(y)), ro, (unsigned)(sL2 + N1 * k2) * 4u, 0, CP);
-        });
+        }, tw16);
     }
 }
 
@@ -690,7 +702,10 @@ __device__ __forceinline__ void passB_tile(
     const int nb = N1 / S;
     const int ntiles = nb * frames;
     float dbv[16];   // ZM: this lane's dB values, r = k2 >> 4
-    tile_loop<L, FragC>(
+    constexpr bool T16 = L >= 256;   // the radix-16 NS = 16 stage's twiddles from LDS, conflict-free
+    float2* tw16 = lds + S * Lds<L>::LS;
+    if constexpr (T16) stage16_twiddles<L>(tw16, tw, tid, S * T);   // (tile_loop's barrier orders it)
+    tile_loop<L, FragC, T16>(
         lds, tw, tile, ntiles, sF, tF, sL, tL,
         [&](FragC& fr, int tile) {
             const int b = tile % nb;
@@ -709,7 +724,7 @@ __device__ __forceinline__ void passB_tile(
             const float d = db_of(y);
             out[(f << logN) + b * S + sL + (long long)N1 * k2] = d;
             if constexpr (ZM) dbv[slot] = d;   // stage_last<256, 16, 16>: slot r <-> k2 = tL + 16 r
-        });
+        }, tw16);
     if constexpr (ZM) {
         static_assert(S == 32 && L == 256, "zoom: one half-wave per zoomed bin, k2 = tL + 16 r");
         if (tile >= ntiles) return;
@@ -836,7 +851,7 @@ static int launch_single(const FftPlan& p, const float2* in, long long stride, i
 template <int L, int S>
 static int launch_passA(const FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
     auto k = fft_passA_kernel<L, S>;
-    size_t lds = sizeof(float2) * (S * Lds<L>::LS + (L == 256 ? L : 0));   // + stage twiddles (256-point columns)
+    size_t lds = sizeof(float2) * (S * Lds<L>::LS + (L == 256 ? L + 256 : 0));   // + stage twiddles (256-point columns)
     SDRGPU_CHECK(set_lds(k, lds));
     const int g = (p.N2 / S) * frames;
     hipLaunchKernelGGL(k, dim3(g), dim3(S * L / 16), lds, s, in, stride, frames, p.win.as<float>(), p.nz, p.N2,
@@ -861,7 +876,7 @@ static int launch_passA2(const FftPlan& p, const float2* in, long long stride, i
 template <int L, int S, bool ZM = false>
 static int launch_passB(const FftPlan& p, int frames, float* out, hipStream_t s, float* zoom = nullptr) {
     auto k = fft_passB_kernel<L, S, ZM>;
-    size_t lds = sizeof(float2) * S * Lds<L>::LS;
+    size_t lds = sizeof(float2) * (S * Lds<L>::LS + (L >= 256 ? 256 : 0));   // + passB_tile's tw16
     SDRGPU_CHECK(set_lds(k, lds));
     const int g = (p.N1 / S) * frames;
     hipLaunchKernelGGL(k, dim3(g), dim3(S * L / 16), lds, s, p.cur, frames, p.N1, p.logN,
@@ -874,7 +889,8 @@ template <int LA, int SA, int LB, int SB, bool PAIRED, bool ZM = false>
 static int launch_merged(const FftPlan& p, const float2* scratchB, int framesB, float* outB, const float2* in,
                          long long stride, int framesA, float2* scratchA, hipStream_t s, float* zoomB = nullptr) {
     auto k = fft_merged_kernel<LA, SA, LB, SB, PAIRED, ZM>;
-    size_t lds = sizeof(float2) * std::max(SA * Lds<LA>::LS + ((PAIRED || LA == 256) ? LA : 0), SB * Lds<LB>::LS);
+    size_t lds = sizeof(float2) * std::max(SA * Lds<LA>::LS + ((PAIRED || LA == 256) ? LA : 0) + (LA == 256 && !PAIRED ? 256 : 0),
+                                           SB * Lds<LB>::LS + (LB >= 256 ? 256 : 0));
     SDRGPU_CHECK(set_lds(k, lds));
     const int nB = (LA / SB) * framesB, nA = (LB / SA) * framesA;
     hipLaunchKernelGGL(k, dim3(nB + nA), dim3(SB * LB / 16), lds, s, nB, scratchB, framesB, outB, zoomB, in, stride, framesA,
@@ -888,7 +904,7 @@ template <int S, int CP, int VAR>
 static int launch_passA_1m(FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
     if (p.N2 % S) { set_error("fft: N2 %d not a multiple of %d columns", p.N2, S); return SDRGPU_ESTATE; }
     auto k = fft_passA_1m_kernel<S, CP, VAR>;
-    size_t lds = sizeof(float2) * (S * Lds<1024>::LS + 1024);
+    size_t lds = sizeof(float2) * (S * Lds<1024>::LS + 1024 + 256);
     SDRGPU_CHECK(set_lds(k, lds));
     if (!p.gridA) {
         int per = 0, cus = 0;
@@ -906,7 +922,7 @@ static int launch_passA_1m(FftPlan& p, const float2* in, long long stride, int f
 template <int S, int CP, int VAR = 0>
 static int launch_passB_1m(FftPlan& p, int frames, float* out, hipStream_t s) {
     auto k = fft_passB_1m_kernel<S, CP, VAR>;
-    size_t lds = sizeof(float2) * (S * Lds<1024>::LS + 1024);
+    size_t lds = sizeof(float2) * (S * Lds<1024>::LS + 1024 + 256);
     SDRGPU_CHECK(set_lds(k, lds));
     if (!p.gridB) {
         int per = 0, cus = 0;

@@ -104,10 +104,22 @@ template <> __device__ __forceinline__ void dft<16>(float2* v) { dft16(v); }
 __device__ __forceinline__ int pad16(int i) { return i + (i >> 4); }
 template <int L> struct Lds { static constexpr int LS = L + L / 16 + 1; };   // sequence stride (odd)
 
+// tw16[16 r + jm] = tw[r jm (L / 256)] (r, jm < 16) for the T16 stages below; the caller's next
+// barrier orders the writes
+template <int L>
+__device__ __forceinline__ void stage16_twiddles(float2* tw16, const float2* __restrict__ tw, int tid, int nthreads) {
+    for (int i = tid; i < 256; i += nthreads) tw16[i] = tw[(i >> 4) * (i & 15) * (L / 256)];
+}
+
 // One Stockham radix-R stage, LDS -> LDS, for sequence s, thread t (T = L/16 threads per
 // sequence, each owning butterflies j = t + b*T, b < 16/R). Caller provides the barriers.
-template <int L, int R, int NS>
-__device__ __forceinline__ void stage_lds(float2* seq, const float2* __restrict__ tw, int t) {
+// stage16_twiddles fills it (256 entries, once per workgroup)
+// tw16 (optional, R = NS = 16): the stage's twiddles as tw16[16 r + jm] = tw[r jm (L / 256)], so
+// the 16 lanes of different jm read 16 consecutive words for each r. Read from tw directly the
+// stride r jm (L / 256) puts them in the same LDS banks for even r (16-way at r = 8 when tw is
+// in LDS: the 1M pass B spent more cycles in bank conflicts than in LDS issue, r3 SQ counters).
+template <int L, int R, int NS, bool T16 = false>
+__device__ __forceinline__ void stage_lds(float2* seq, const float2* __restrict__ tw, int t, const float2* tw16 = nullptr) {
     constexpr int T = L / 16;
     constexpr int BPT = 16 / R;
     float2 v[BPT][R];
@@ -117,8 +129,13 @@ __device__ __forceinline__ void stage_lds(float2* seq, const float2* __restrict_
 #pragma unroll
         for (int r = 0; r < R; r++) v[b][r] = seq[pad16(j + r * (L / R))];
         const int jm = j % NS;
+        if constexpr (T16 && R == 16 && NS == 16) {
 #pragma unroll
-        for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw[r * jm * (L / (NS * R))]);
+            for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw16[16 * r + jm]);
+        } else {
+#pragma unroll
+            for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw[r * jm * (L / (NS * R))]);
+        }
         dft<R>(v[b]);
     }
     __syncthreads();
@@ -133,8 +150,9 @@ __device__ __forceinline__ void stage_lds(float2* seq, const float2* __restrict_
 }
 
 // Last stage: LDS -> registers -> store functor (output index k, value).
-template <int L, int R, int NS, class Store>
-__device__ __forceinline__ void stage_last(const float2* seq, const float2* __restrict__ tw, int t, Store&& st) {
+template <int L, int R, int NS, bool T16 = false, class Store>
+__device__ __forceinline__ void stage_last(const float2* seq, const float2* __restrict__ tw, int t, Store&& st,
+                                           const float2* tw16 = nullptr) {
     constexpr int T = L / 16;
     constexpr int BPT = 16 / R;
     float2 v[BPT][R];
@@ -144,8 +162,13 @@ __device__ __forceinline__ void stage_last(const float2* seq, const float2* __re
 #pragma unroll
         for (int r = 0; r < R; r++) v[b][r] = seq[pad16(j + r * (L / R))];
         const int jm = j % NS;
+        if constexpr (T16 && R == 16 && NS == 16) {   // (stage_lds's conflict-free layout)
 #pragma unroll
-        for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw[r * jm * (L / (NS * R))]);
+            for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw16[16 * r + jm]);
+        } else {
+#pragma unroll
+            for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw[r * jm * (L / (NS * R))]);
+        }
         dft<R>(v[b]);
     }
 #pragma unroll
@@ -172,9 +195,11 @@ __device__ __forceinline__ void stage_first(float2* seq, float2 (&v)[16], int t)
 }
 
 // Stages after the first: LDS -> ... -> store functor. Expects stage_first's LDS writes
-// to be complete (caller's barrier); leaves the LDS free for reuse on return.
-template <int L, class Store>
-__device__ __forceinline__ void stages_rest(float2* lds, const float2* __restrict__ tw, int sL, int tL, Store&& st) {
+// to be complete (caller's barrier); leaves the LDS free for reuse on return. T16: the radix-16
+// stage with NS = 16 (L >= 256) reads its twiddles from tw16 (stage_lds), staged by the caller.
+template <int L, bool T16 = false, class Store>
+__device__ __forceinline__ void stages_rest(float2* lds, const float2* __restrict__ tw, int sL, int tL, Store&& st,
+                                            const float2* tw16 = nullptr) {
     constexpr int LS = Lds<L>::LS;
     const float2* seqL = lds + sL * LS;
     if constexpr (L == 64) {
@@ -182,9 +207,9 @@ __device__ __forceinline__ void stages_rest(float2* lds, const float2* __restric
     } else if constexpr (L == 128) {
         stage_last<L, 8, 16>(seqL, tw, tL, st);
     } else if constexpr (L == 256) {
-        stage_last<L, 16, 16>(seqL, tw, tL, st);
+        stage_last<L, 16, 16, T16>(seqL, tw, tL, st, tw16);
     } else {
-        stage_lds<L, 16, 16>(lds + sL * LS, tw, tL);   // middle stage (radix 16, NS = 16)
+        stage_lds<L, 16, 16, T16>(lds + sL * LS, tw, tL, tw16);   // middle stage (radix 16, NS = 16)
         if constexpr (L == 512) stage_last<L, 2, 256>(seqL, tw, tL, st);
         else if constexpr (L == 1024) stage_last<L, 4, 256>(seqL, tw, tL, st);
         else if constexpr (L == 2048) stage_last<L, 8, 256>(seqL, tw, tL, st);
