@@ -41,6 +41,8 @@ __global__ __launch_bounds__(L) void chan_kernel(const float2* __restrict__ hist
     const int r = threadIdx.x;
     float2* twl = lds + 16 * LS;                       // FFT twiddles staged once in LDS
     twl[r] = tw[r];                                    // (L threads, L twiddles; first barrier orders it)
+    float2* tw16 = twl + L;                            // middle stage's, bank-conflict-free (stage_lds)
+    stage16_twiddles<L>(tw16, tw, r, L);
     const int m0 = blockIdx.x * fpw;
     const int m1 = min(m0 + fpw, frames);
     auto fetch = [&](long long b) -> float2 {          // buf[b] of [hist (H) || in (count)], 0 outside
@@ -96,9 +98,9 @@ __global__ __launch_bounds__(L) void chan_kernel(const float2* __restrict__ hist
         __syncthreads();
         const int m = mb + sF;
         float2* o = out + (long long)m * L;
-        stages_rest<L>(lds, twl, sF, tF, [&](int k, float2 y) {
+        stages_rest<L, (L >= 256)>(lds, twl, sF, tF, [&](int k, float2 y) {
             if (m < m1) o[k] = y;
-        });
+        }, tw16);
         __syncthreads();
     }
 }
@@ -230,6 +232,8 @@ __global__ __launch_bounds__(L / 2) void chan2_kernel(const float2* __restrict__
     float2* twl = lds + 16 * LS;
     twl[threadIdx.x] = tw[threadIdx.x];
     twl[threadIdx.x + NT] = tw[threadIdx.x + NT];
+    float2* tw16 = twl + L;   // the middle FFT stage's twiddles, bank-conflict-free (stage_lds)
+    stage16_twiddles<L>(tw16, tw, threadIdx.x, NT);
     const int m0 = blockIdx.x * fpw;
     const int m1 = min(m0 + fpw, frames);
     auto fetch = [&](long long b) -> float2 {
@@ -297,9 +301,9 @@ __global__ __launch_bounds__(L / 2) void chan2_kernel(const float2* __restrict__
             __syncthreads();
             const int m = mb + sF;
             float2* o = out + (long long)m * L;
-            stages_rest<L>(lds, twl, sF, tF, [&](int k, float2 y) {
+            stages_rest<L, (L >= 256)>(lds, twl, sF, tF, [&](int k, float2 y) {
                 if (m < m1) o[k] = y;
-            });
+            }, tw16);
             __syncthreads();
         }
     }
@@ -369,7 +373,7 @@ struct ChannelizerBlock : Block {
         if constexpr (L == 1024) {
             if (dft == 1) k = chan2_kernel<L, true>;
         }
-        const size_t lds = sizeof(float2) * (16 * Lds<L>::LS + L);
+        const size_t lds = sizeof(float2) * (16 * Lds<L>::LS + L + 256);   // sequences, twiddles, tw16
         SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         const int grid = (frames + fpw - 1) / fpw;
         hipLaunchKernelGGL(k, dim3(grid), dim3(two || dft ? L / 2 : L), lds, s, hist[cur].as<float2>(), (const float2*)in, Hp, count,
