@@ -103,6 +103,11 @@ __global__ __launch_bounds__(S * L / 16) void fft_single_kernel(
         });
 }
 
+// raw buffer resource over `bytes` bytes from p: loads past the end return 0, stores past it are dropped
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
 // ---- pass A: S columns x N1 rows per tile ---------------------------------------
 // Column c of the frame viewed as N1 x N2: x[n1*N2 + c0 + c]. The column index is the
 // fastest-varying thread coordinate in both the load and the store, so each wave reads
@@ -115,7 +120,7 @@ template <int L, int S>
 __device__ __forceinline__ void passA_tile(
     float2* lds, int tile, const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win,
     int nz, int N2, int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull,
-    float2* __restrict__ scratch) {
+    float2* __restrict__ scratch, const float2* __restrict__ headp = nullptr, int nh = 0) {
     const int tid = threadIdx.x;
     const int c = tid % S, t = tid / S;
     constexpr int T = L / 16;
@@ -136,7 +141,8 @@ __device__ __forceinline__ void passA_tile(
         // (o0) shared by every access of the thread; the row step r * 16 * N2 rides in the
         // scalar soffset. (Plain global accesses kept a 64-bit address pair per row live and
         // spilled at the 4-waves/SIMD register budget.)
-        const float2* x = in + f * frameStride;
+        // split stream (fft_execute_split): frame 0 = [headp (nh) || in], frame f >= 1 at in + f stride - nh
+        const float2* x = in + f * frameStride - (f > 0 ? nh : 0);
         const unsigned o0 = (unsigned)(t * N2 + col);
         const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, 0x7fffffff, 0x00020000);
         const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)win, (short)0, 0x7fffffff, 0x00020000);
@@ -144,7 +150,23 @@ __device__ __forceinline__ void passA_tile(
         const int rowB = T * N2 * 8;   // bytes between the rows t + 16 r and t + 16 (r + 1)
         float2 xv[16], tt[16];
         float wv[16];
-        if (nz >= L * N2) {   // no zero padding (wave-uniform)
+        if (nh > 0 && f == 0) {   // the frame straddling two buffers (workgroup-uniform)
+            // sample n comes from headp[n] (n < nh) or in[n - nh]: two range-checked loads (resources
+            // of nh and nz - nh elements; the one out of range returns 0) summed, so no branch per
+            // sample. The row step is in the per-lane offset: the range check ignores soffset.
+            const __amdgpu_buffer_rsrc_t rh = brsrc(headp, (unsigned)nh * 8u);
+            const __amdgpu_buffer_rsrc_t rb = brsrc(in, (unsigned)(nz - nh) * 8u);
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const unsigned n = o0 + (unsigned)(r * T * N2);
+                const bool live = (int)n < nz;
+                const float2 a = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, n * 8, 0, 0));
+                const float2 b = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rb, (n - (unsigned)nh) * 8, 0, 0));
+                const float we = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, (live ? n : 0u) * 4, 0, 0));
+                xv[r] = make_float2(a.x + b.x, a.y + b.y);
+                wv[r] = live ? we : 0.0f;
+            }
+        } else if (nz >= L * N2) {   // no zero padding (wave-uniform)
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 xv[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, o0 * 8, r * rowB, 0));
@@ -221,9 +243,16 @@ template <int L, int S>
 __global__ __launch_bounds__(S * L / 16) __attribute__((amdgpu_waves_per_eu(4))) void fft_passA_kernel(
     const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
     int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull,
-    float2* __restrict__ scratch) {
+    float2* __restrict__ scratch, const float2* __restrict__ headp, int nh, SideCopy side) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    passA_tile<L, S>(lds, blockIdx.x, in, frameStride, frames, win, nz, N2, logN, tw, tfull, scratch);
+    const int ntiles = (N2 / S) * frames;
+    if ((int)blockIdx.x >= ntiles) {   // spare workgroups: the caller's side copies (fft_execute_split)
+        const int w = blockIdx.x - ntiles, nw = gridDim.x - ntiles;
+        for (int k = 0; k < side.count; k++)
+            for (int i = w * blockDim.x + threadIdx.x; i < side.n[k]; i += nw * blockDim.x) side.dst[k][i] = side.src[k][i];
+        return;
+    }
+    passA_tile<L, S>(lds, blockIdx.x, in, frameStride, frames, win, nz, N2, logN, tw, tfull, scratch, headp, nh);
 }
 
 // ---- pass A, paired columns: S columns x N1 rows per tile, two adjacent columns per lane --
@@ -399,10 +428,6 @@ __device__ __forceinline__ double2 zmul(double2 a, double2 b) {
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
-// raw buffer resource over `bytes` bytes from p: loads past the end return 0, stores past it are dropped
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, unsigned bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
 typedef unsigned bu2 __attribute__((ext_vector_type(2)));
 typedef unsigned bu4 __attribute__((ext_vector_type(4)));
 
@@ -849,13 +874,23 @@ static int launch_single(const FftPlan& p, const float2* in, long long stride, i
 }
 
 template <int L, int S>
-static int launch_passA(const FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
+static int launch_passA(const FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s,
+                        const float2* headp = nullptr, int nh = 0, const SideCopy* side = nullptr) {
     auto k = fft_passA_kernel<L, S>;
     size_t lds = sizeof(float2) * (S * Lds<L>::LS + (L == 256 ? L + 256 : 0));   // + stage twiddles (256-point columns)
     SDRGPU_CHECK(set_lds(k, lds));
-    const int g = (p.N2 / S) * frames;
+    SideCopy sc{};
+    int spare = 0;
+    if (side && side->count > 0) {
+        sc = *side;
+        int mx = 0;
+        for (int i = 0; i < sc.count; i++) mx = std::max(mx, sc.n[i]);
+        spare = std::min(64, (mx + S * L / 16 * 4 - 1) / (S * L / 16 * 4));   // ~4 elements per thread
+        spare = std::max(spare, 1);
+    }
+    const int g = (p.N2 / S) * frames + spare;
     hipLaunchKernelGGL(k, dim3(g), dim3(S * L / 16), lds, s, in, stride, frames, p.win.as<float>(), p.nz, p.N2,
-                       p.logN, p.tw1.as<float2>(), p.tfull.as<float2>(), p.cur);
+                       p.logN, p.tw1.as<float2>(), p.tfull.as<float2>(), p.cur, headp, nh, sc);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
@@ -1276,6 +1311,20 @@ extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long f
     SDRGPU_CHECK(p.order.follow(s));
     OrderScope od(p.order, s);
     return fft_execute(h, in, frameStride, frames, out, nullptr, s);
+}
+
+int sdrgpu::fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const float2* body, long long stride, int frames,
+                              float* out, const SideCopy& side, hipStream_t s) {
+    if (!h || !body || frames <= 0 || nh < 0 || (nh > 0 && !head)) return SDRGPU_ESTATE;
+    FftPlan& p = h->p;
+    // the 64k plan's default tiles (256 x 256, 32 columns / 32 rows, one-column pass A); one chunk
+    if (!(p.N1 == 256 && p.N2 == 256 && p.sa == 32 && p.sb == 32 && p.sa2 == 0) || frames > p.chunkFrames || nh >= p.nz)
+        return SDRGPU_ESTATE;
+    SDRGPU_CHECK(p.scratch.ensure((size_t)frames * p.N * sizeof(float2)));
+    p.cur = p.scratch.as<float2>();
+    SDRGPU_CHECK((launch_passA<256, 32>(p, body, stride, frames, s, head, nh, &side)));
+    SDRGPU_CHECK(dispatch_passB(p, frames, out, s));
+    return frames;
 }
 
 int sdrgpu::fft_execute_owned(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, hipStream_t s) {

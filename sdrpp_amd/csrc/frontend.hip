@@ -81,6 +81,7 @@ struct sdrgpu_frontend {
     hipStream_t cs = nullptr;
     PipeSlot pipe[2];
     long long nextTicket = 0;
+    int split = 1;   // fft_execute_split for pushes that complete frames (SDRGPU_FE_SPLIT=0, tuning: stitch copies)
 };
 
 static void destroy_parts(sdrgpu_frontend* f) {
@@ -131,6 +132,7 @@ extern "C" int sdrgpu_frontend_create(sdrgpu_frontend** out, int device, double 
     f->fftSize = fftSize;
     f->fftRate = fftRate;
     f->window = windowType;
+    if (const char* e = tuning_env("SDRGPU_FE_SPLIT")) f->split = atoi(e);
     int rc = hipStreamCreateWithFlags(&f->s, hipStreamNonBlocking) == hipSuccess ? SDRGPU_OK : SDRGPU_EHIP;
     if (rc < 0) set_error("frontend_create: hipStreamCreate failed");
     if (rc >= 0) rc = fe_build_preproc(f);
@@ -276,6 +278,38 @@ static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s)
     if (T + m >= f->nextFrame + f->nz) nf = (int)((T + m - f->nextFrame - f->nz) / st) + 1;
     SDRGPU_CHECK(f->spectra.ensure(sizeof(float) * (size_t)std::max(nf, 1) * f->fftSize));
     float* spec = f->spectra.as<float>();
+    if (nf > 0 && f->split) {
+        // One launch pair and no copy launch: pass A reads the frame straddling the previous push
+        // from the device tail and this block in place (fft_execute_split), and its spare
+        // workgroups copy the new tail (samples after the last frame: all in this block, since a
+        // frame completed) into the other tail buffer. 45 -> see DESIGN.md §3 per call.
+        const long long nextAfterS = f->nextFrame + (long long)nf * st, endS = T + m;
+        const int head = f->nextFrame < T ? (int)(T - f->nextFrame) : 0;
+        const float2* body = head > 0 ? x : x + (f->nextFrame - T);
+        SideCopy side{};
+        int newLenS = 0, nbS = f->curTail;
+        if (nextAfterS < endS) {
+            newLenS = (int)(endS - nextAfterS);
+            nbS = f->curTail ^ 1;
+            SDRGPU_CHECK(f->tail[0].ensure(sizeof(float2) * f->nz));
+            SDRGPU_CHECK(f->tail[1].ensure(sizeof(float2) * f->nz));
+            side.dst[0] = f->tail[nbS].as<float2>();
+            side.src[0] = x + (m - newLenS);
+            side.n[0] = newLenS;
+            side.count = 1;
+        }
+        const int rc = fft_execute_split(f->fft, head > 0 ? f->tail[f->curTail].as<float2>() : nullptr, head, body, st, nf,
+                                         spec, side, s);
+        if (rc >= 0) {
+            f->nSpec = nf;
+            f->nextFrame = nextAfterS;
+            f->curTail = nbS;
+            f->tailLen = newLenS;
+            f->total = endS;
+            return nf;
+        }
+        if (rc != SDRGPU_ESTATE) return rc;   // (ESTATE: this plan has no split path; stitch below)
+    }
     int done = 0;
     // the stitched straddling frame and the new tail are built by one copy launch (up to four
     // device segments) before the spectrum: both read only the old tail and this block

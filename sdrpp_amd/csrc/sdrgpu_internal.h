@@ -147,4 +147,17 @@ namespace sdrgpu {
 // entry points without the cross-stream ordering, for a handle owned by another handle
 int block_run_owned(sdrgpu_block* h, const void* in, int count, void* out, hipStream_t s);
 int fft_execute_owned(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, hipStream_t s);
+// Up to two device copies of complex samples done by spare workgroups of another launch.
+struct SideCopy {
+    float2* dst[2];
+    const float2* src[2];
+    int n[2];
+    int count;
+};
+// Frames f = 0 .. frames - 1 of a stream split over two buffers: frame 0 is [head[0, nh) ||
+// body[0, nz - nh)], frame f >= 1 starts at body + f * stride - nh. The pass-A launch reads frame 0
+// from both buffers (no stitch copy) and runs `side` with spare workgroups. Returns frames, or
+// SDRGPU_ESTATE when the plan has no such path (the caller then stitches and calls fft_execute_owned).
+int fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const float2* body, long long stride, int frames, float* out,
+                      const SideCopy& side, hipStream_t s);
 }  // namespace sdrgpu
