@@ -238,6 +238,61 @@ def test_rxvfo_c5(rng):
         assert_close_c(yg, yo, 5e-5, "rxvfo")
 
 
+_TAIL_CASES = [
+    ("rxvfo", (61.44e6, 240000, 200000, 2.5e6)),     # plan 256 (32, 4, 2) + 91-tap LPF: 3 tail stages
+    ("rxvfo", (61.44e6, 480000, 150000, -3.1e6)),    # plan 128 (16, 4, 2) + LPF
+    ("rxvfo", (3.84e6, 60000, 60000, 1.7e5)),        # plan 64 (8, 4, 2), no LPF: 2 tail stages
+    ("rxvfo", (61.44e6, 120000, 90000, 7e5)),        # plan 512 + LPF: 4 tail stages
+    ("decim", (64,)),                                # PowerDecimator(64): no xlator
+]
+_TAIL_SIZES = [307200, 1, 5000, 31, 33333, 307200, 7, 100000, 1200000, 4099]
+
+
+def _tail_block(kind, args):
+    return dsp.RxVFO(*args) if kind == "rxvfo" else dsp.PowerDecimator(*args)
+
+
+@pytest.mark.parametrize("kind,args", _TAIL_CASES)
+def test_fir_tail_bit_identical_to_stage_launches(kind, args, monkeypatch, rng):
+    """fir_tail_kernel (a chain's FIR stages 2.. in one launch for short calls, halos recomputed per
+    workgroup) gives the per-stage fir_kernel launches' stream bit for bit, across ragged calls
+    (single samples, calls with no output, calls past the tail's size limit that take the
+    per-stage path, so the carried histories and decimation phases cross between the two paths).
+    Stage-2 kernels default to the MFMA phase-split tiles for big calls; they are pinned to
+    fir_kernel here (SDRGPU_FIR_MFMA_PS=0) so both paths run the same fmaf chain."""
+    monkeypatch.setenv("SDRGPU_TUNING", "1")
+    monkeypatch.setenv("SDRGPU_FIR_MFMA_PS", "0")
+    a, b = _tail_block(kind, args), _tail_block(kind, args)
+    x = iq(rng, sum(_TAIL_SIZES)) * (1.0 + 0.5j)
+    pos, ya, yb = 0, [], []
+    for k, n in enumerate(_TAIL_SIZES):
+        blk = x[pos:pos + n]
+        pos += n
+        if k == 0:   # the tail switch is read at a chain's first call
+            monkeypatch.setenv("SDRGPU_VFO_TAIL", "0")
+            ya.append(a.process(blk))
+            monkeypatch.setenv("SDRGPU_VFO_TAIL", "1")
+            yb.append(b.process(blk))
+        else:
+            ya.append(a.process(blk))
+            yb.append(b.process(blk))
+        assert ya[-1].shape == yb[-1].shape, k
+        assert np.array_equal(ya[-1].view(np.uint32), yb[-1].view(np.uint32)), (k, n, np.abs(ya[-1] - yb[-1]).max())
+
+
+def test_fir_tail_rxvfo_vs_oracle(rng):
+    """The default RxVFO path at the reference block size (tail on, MFMA stage 2 on big calls)
+    against the oracle, ragged calls switching between the tail and the per-stage path."""
+    g = dsp.RxVFO(61.44e6, 120000, 90000, 7e5)
+    o = oracle.RxVFO(61.44e6, 120000, 90000, 7e5)
+    for n in [307200, 4099, 262144 * 2, 1, 307200]:
+        x = iq(rng, n)
+        yo, yg = o.process(x), g.process(x)
+        assert len(yg) == len(yo)
+        if len(yo):
+            assert_close_c(yg, yo, 5e-5, "rxvfo 512")
+
+
 def _quad_bound(y_ref, y_prev0, e_fir, inv_dev):
     """Per-sample bound on the quadrature output (quadrature.h:41-56) of an FIR output stream
     known to within e_fir (absolute) of y_ref: an error e in y_i turns arg(y_i) by at most
