@@ -47,6 +47,36 @@ template <typename T> __device__ __forceinline__ T zero_of();
 template <> __device__ __forceinline__ float zero_of<float>() { return 0.0f; }
 template <> __device__ __forceinline__ float2 zero_of<float2>() { return make_float2(0.f, 0.f); }
 
+// atan2 of the FM quadrature (demod/quadrature.h:41-56: arg(y * conj(y[-1]))), for every kernel that
+// forms it. OCML's atan2f (an IEEE divide and special-case branches) cost ~8% of the fused C3 kernel
+// (DDCFM 0.77 vs DDC 0.70 ms, tools/c3_quad_cost.py). This is the CPU baseline's minimax polynomial
+// (oracle/cpu_fast.c) with v_rcp_f32: |error| <= 1.4 ulp(pi) (3.3e-7 rad, a numpy emulation over 4e6
+// random (y, x) spanning 17 decades), inside the quadrature bars of tests/ (8 ulp(pi) / dev vs the
+// reference code; 8 eps pi / dev + the FIR-error term in the fused-DDC tests). Signed zeros follow
+// C's atan2: atan2(+-0, +0) = +-0, atan2(+-0, -0) = +-pi (signbit, not x < 0).
+__device__ __forceinline__ float quad_atan2f(float y, float x) {
+#ifdef SDRGPU_OCML_ATAN2   // (A/B builds only)
+    return atan2f(y, x);
+#endif
+    const float ax = fabsf(x), ay = fabsf(y);
+    const bool swp = ay > ax;
+    const float mn = swp ? ax : ay, mx = swp ? ay : ax;
+    const float a = mn * __builtin_amdgcn_rcpf(mx == 0.0f ? 1.0f : mx);
+    const float s = a * a;
+    float p = 0.0028662257f;
+    p = fmaf(p, s, -0.0161657367f);
+    p = fmaf(p, s, 0.0429096138f);
+    p = fmaf(p, s, -0.0752896400f);
+    p = fmaf(p, s, 0.1065626393f);
+    p = fmaf(p, s, -0.1420889944f);
+    p = fmaf(p, s, 0.1999355085f);
+    p = fmaf(p, s, -0.3333314528f);
+    float r = fmaf(a * s, p, a);
+    r = swp ? 1.57079632679489662f - r : r;
+    r = signbit(x) ? 3.14159265358979324f - r : r;
+    return copysignf(r, y);
+}
+
 // acc += x * h for the four (data, tap) type pairs of filter/fir.h:69-75
 __device__ __forceinline__ void mac(float& acc, float x, float h) { acc = fmaf(x, h, acc); }
 __device__ __forceinline__ void mac(float2& acc, float2 x, float h) { acc.x = fmaf(x.x, h, acc.x); acc.y = fmaf(x.y, h, acc.y); }
@@ -277,7 +307,7 @@ __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
                 const float br = prev.x, bi = -prev.y;
                 const float re = (y.x * br) - (y.y * bi);
                 const float im = (y.y * br) + (y.x * bi);
-                out[m] = atan2f(im, re) * a.invDev;
+                out[m] = quad_atan2f(im, re) * a.invDev;
                 if (m == a.M - 1) a.dinNext[0] = y;
             }
         }
@@ -400,7 +430,7 @@ __global__ __launch_bounds__(64 * NW) void fir_mfma_kernel(FirArgs a) {
                 const float br = prev.x, bi = -prev.y;
                 const float re = (y.x * br) - (y.y * bi);
                 const float im = (y.y * br) + (y.x * bi);
-                out[m] = atan2f(im, re) * a.invDev;
+                out[m] = quad_atan2f(im, re) * a.invDev;
                 if (m == a.M - 1) a.dinNext[0] = y;
             }
         }
@@ -502,7 +532,7 @@ __global__ __launch_bounds__(256) void fir_mfma_ps_kernel(FirArgs a) {
             const float br = prev.x, bi = -prev.y;
             const float re = (y.x * br) - (y.y * bi);
             const float im = (y.y * br) + (y.x * bi);
-            reinterpret_cast<float*>(a.out)[m] = atan2f(im, re) * a.invDev;
+            reinterpret_cast<float*>(a.out)[m] = quad_atan2f(im, re) * a.invDev;
             if (m == a.M - 1) a.dinNext[0] = y;
         }
     } else {
@@ -657,7 +687,7 @@ __global__ __launch_bounds__(256) void fir_rows_kernel(FirArgs a) {
                         const float br = prev.x, bi = -prev.y;
                         const float re = (y.x * br) - (y.y * bi);
                         const float im = (y.y * br) + (y.x * bi);
-                        outf[m] = atan2f(im, re) * a.invDev;
+                        outf[m] = quad_atan2f(im, re) * a.invDev;
                         if (m == a.M - 1) a.dinNext[0] = y;
                     }
                 } else {
@@ -752,7 +782,7 @@ __device__ __forceinline__ float quad_value(float2 y, float2 d, float invDev) {
     const float br = d.x, bi = -d.y;
     const float re = (y.x * br) - (y.y * bi);
     const float im = (y.y * br) + (y.x * bi);
-    return atan2f(im, re) * invDev;
+    return quad_atan2f(im, re) * invDev;
 }
 __global__ void quad_kernel(const float2* __restrict__ in, float* __restrict__ out, int n, const float2* __restrict__ din,
                             float2* __restrict__ dinNext, float invDev) {
