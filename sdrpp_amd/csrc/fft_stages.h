@@ -7,8 +7,23 @@
 
 namespace sdrgpu {
 
+typedef float pk2 __attribute__((ext_vector_type(2)));
+
+// a * b as two packed ops with the operand halves picked by op_sel, the same roundings as the
+// contracted scalar form (re = fma(a.x, b.x, -(a.y b.y)), im = fma(a.x, b.y, a.y b.x)):
+//   t = (a.y b.y, a.y b.x)                    v_pk_mul_f32, src0 (hi, hi), src1 (hi, lo)
+//   r = (a.x b.x - t.x, a.x b.y + t.y)        v_pk_fma_f32, src0 (lo, lo), src2 lo negated
+// Left to itself the compiler builds the broadcast / swapped operand pairs with v_mov_b32 (208
+// moves in the 1M pass A's 1,559 VALU instructions, r3).
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+#ifdef SDRGPU_CMUL_C   // (A/B builds only)
     return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+#endif
+    pk2 t, r;
+    const pk2 x = {a.x, a.y}, y = {b.x, b.y};
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(x), "v"(y));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[0,1,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(x), "v"(y), "v"(t));
+    return make_float2(r.x, r.y);
 }
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
@@ -18,7 +33,6 @@ __device__ __forceinline__ float2 mul_negi(float2 a) { return make_float2(a.y, -
 // each (src1 halves swapped by op_sel, one half negated). Left to itself the compiler forms both
 // cross sums in two packed adds and assembles the results with four moves (r3: 439 v_mov_b32 in
 // the 1M pass A's 1,900 VALU instructions).
-typedef float pk2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float2 add_negi(float2 a, float2 b) {
     pk2 r;
     const pk2 x = {a.x, a.y}, y = {b.x, b.y};
