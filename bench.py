@@ -101,7 +101,7 @@ class C2:
         self.spectra = torch.empty(self.frames * self.N, dtype=torch.float32, device="cuda")
         self.bytes_per_sample = 8 + 4 * self.N / self.NZ
         self.kernel_bytes = self.bytes_per_sample * self.B
-        self.kernel_name = ("spectrum N=2^20, nz=1e6: fft_passA_1m_kernel<16,0,128> (persistent, tile-major intermediate) + "
+        self.kernel_name = ("spectrum N=2^20, nz=1e6: fft_passA_1m_kernel<16,2,128> (persistent, tile-major intermediate, non-temporal input loads) + "
                             "fft_passB_1m_kernel<8,0,192> (persistent, XCD-grouped rows) per 16-frame chunk")
 
     def dominant(self, x, s):

@@ -979,6 +979,11 @@ static int dispatch_1m(FftPlan& p, const float2* xc, long long stride, int nf, f
         SDRGPU_CHECK((launch_passA_1m<16, 2, 0>(p, xc, stride, nf, s)));
         return launch_passB_1m<16, 2>(p, nf, o, s);
     }
+    if (p.pipe1m == 3 || p.pipe1m == 4) {   // (tuning) default layout with cached input loads (3), nt pass B loads (4)
+        if (p.pipe1m == 3) SDRGPU_CHECK((launch_passA_1m<16, 0, 128>(p, xc, stride, nf, s)));
+        else SDRGPU_CHECK((launch_passA_1m<16, 2, 128>(p, xc, stride, nf, s)));
+        return p.pipe1m == 4 ? launch_passB_1m<8, 2, 64 | 128>(p, nf, o, s) : launch_passB_1m<8, 0, 64 | 128>(p, nf, o, s);
+    }
     bool tm = false;
     if (p.sA1m == 8) {
         if (p.var1m == 73) SDRGPU_CHECK((launch_passA_1m<8, 0, 73>(p, xc, stride, nf, s)));
@@ -986,7 +991,10 @@ static int dispatch_1m(FftPlan& p, const float2* xc, long long stride, int nf, f
         else SDRGPU_CHECK((launch_passA_1m<8, 0, 0>(p, xc, stride, nf, s)));
     } else {
         switch (p.var1m) {
-        case 128: SDRGPU_CHECK((launch_passA_1m<16, 0, 128>(p, xc, stride, nf, s))); tm = true; break;
+        // default: the input rows are read once, non-temporal (slc), so they do not push the 4 MB
+        // window out of L2 (PMC fetch 18.15 -> 17.50 B/sample, C2 1.848 -> 1.798 ms, 3 interleaved
+        // runs; non-temporal pass-B loads of the intermediate measured 2.41 ms: it must stay cached)
+        case 128: SDRGPU_CHECK((launch_passA_1m<16, 2, 128>(p, xc, stride, nf, s))); tm = true; break;
         case 137: SDRGPU_CHECK((launch_passA_1m<16, 0, 137>(p, xc, stride, nf, s))); tm = true; break;
         case 144: SDRGPU_CHECK((launch_passA_1m<16, 0, 144>(p, xc, stride, nf, s))); tm = true; break;   // (measurement)
         case 160: SDRGPU_CHECK((launch_passA_1m<16, 0, 160>(p, xc, stride, nf, s))); tm = true; break;
