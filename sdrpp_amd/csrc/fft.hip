@@ -19,6 +19,10 @@
 #include "sdrgpu_internal.h"
 #include "fft_stages.h"
 
+// cache policy of pass A's input loads (A/B builds; 2 = streaming)
+#ifndef SDRGPU_PA_CP
+#define SDRGPU_PA_CP 2
+#endif
 namespace sdrgpu {
 
 // K3, volk_32fc_s32f_power_spectrum_32f(out, X, 1.0, N): 10*log10(re^2 + im^2).
@@ -169,7 +173,7 @@ __device__ __forceinline__ void passA_tile(
         } else if (nz >= L * N2) {   // no zero padding (wave-uniform)
 #pragma unroll
             for (int r = 0; r < 16; r++) {
-                xv[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, o0 * 8, r * rowB, 0));
+                xv[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, o0 * 8, r * rowB, SDRGPU_PA_CP));
                 wv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, o0 * 4, r * rowB / 2, 0));
             }
         } else {              // zero-padded tail: clamped (in-bounds) loads, then select
