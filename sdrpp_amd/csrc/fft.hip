@@ -19,6 +19,9 @@
 #include "sdrgpu_internal.h"
 #include "fft_stages.h"
 
+#ifndef SDRGPU_PB_NT
+#define SDRGPU_PB_NT 1   // 64k pass B: streaming dB row stores (A/B builds: 0)
+#endif
 // cache policy of pass A's input loads (A/B builds; 2 = streaming)
 #ifndef SDRGPU_PA_CP
 #define SDRGPU_PA_CP 2
@@ -751,7 +754,11 @@ __device__ __forceinline__ void passB_tile(
             const int b = tile % nb;
             const long long f = tile / nb;
             const float d = db_of(y);
-            out[(f << logN) + b * S + sL + (long long)N1 * k2] = d;
+            // dB rows are written once and never read back here: streaming stores (whole 128-B
+            // lines: S = 32 consecutive floats per row), so they do not evict the intermediate
+            float* o = &out[(f << logN) + b * S + sL + (long long)N1 * k2];
+            if constexpr (SDRGPU_PB_NT) __builtin_nontemporal_store(d, o);
+            else *o = d;
             if constexpr (ZM) dbv[slot] = d;   // stage_last<256, 16, 16>: slot r <-> k2 = tL + 16 r
         }, tw16);
     if constexpr (ZM) {
