@@ -26,6 +26,9 @@
 #include <vector>
 #include "sdrgpu_internal.h"
 #include "fft_stages.h"
+#ifndef SDRGPU_CHAN_NT
+#define SDRGPU_CHAN_NT 1   // FFT-form channelizer: streaming output row stores (A/B builds: 0)
+#endif
 
 namespace sdrgpu {
 
@@ -302,7 +305,14 @@ __global__ __launch_bounds__(L / 2) void chan2_kernel(const float2* __restrict__
             const int m = mb + sF;
             float2* o = out + (long long)m * L;
             stages_rest<L, (L >= 256)>(lds, twl, sF, tF, [&](int k, float2 y) {
-                if (m < m1) o[k] = y;
+                if (m < m1) {
+                    if constexpr (SDRGPU_CHAN_NT) {   // channel rows are written once: streaming stores
+                        typedef float f2v __attribute__((ext_vector_type(2)));
+                        __builtin_nontemporal_store(f2v{y.x, y.y}, reinterpret_cast<f2v*>(o + k));
+                    } else {
+                        o[k] = y;
+                    }
+                }
             }, tw16);
             __syncthreads();
         }

@@ -6,5 +6,5 @@ st() { echo "$1 rc=$2 $(date +%T)" >> $OUT/${TAG}_status.txt; case "$2" in 0) ;;
 echo "start $(date +%T)" > $OUT/${TAG}_status.txt
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/${TAG}_tests.log 2>&1
 st tests $?
-timeout -k 10 400 bash tools/ab_lib.sh ${TAG}_c5 c5; st ab_c5 $?
+timeout -k 10 400 bash tools/ab_lib.sh ${TAG}_${CFG:-c5} ${CFG:-c5}; st ab $?
 echo "all done $(date +%T)" >> $OUT/${TAG}_status.txt
