@@ -62,7 +62,22 @@ extern "C" int sdrgpu_stream_synchronize(void* stream) {
 // a registered buffer and stage through their own pinned buffers otherwise.
 namespace {
 std::mutex g_pinMtx;
-std::map<uintptr_t, size_t> g_pinned;   // start -> bytes
+struct PinnedRange {
+    size_t bytes;
+    bool allocated;   // hipHostMalloc'd (sdrgpu_host_alloc) vs registered (sdrgpu_host_register)
+};
+std::map<uintptr_t, PinnedRange> g_pinned;   // start -> range
+// removes ptr's entry if it was pinned the given way; SDRGPU_EARG (entry kept) otherwise
+int take_pinned(void* ptr, bool allocated, const char* what) {
+    std::lock_guard<std::mutex> lk(g_pinMtx);
+    auto it = g_pinned.find((uintptr_t)ptr);
+    if (it == g_pinned.end() || it->second.allocated != allocated) {
+        set_error("%s: %p was not %s by this library", what, ptr, allocated ? "allocated (sdrgpu_host_alloc)" : "registered (sdrgpu_host_register)");
+        return SDRGPU_EARG;
+    }
+    g_pinned.erase(it);
+    return SDRGPU_OK;
+}
 }  // namespace
 namespace sdrgpu {
 bool host_pinned(const void* p, size_t bytes) {
@@ -71,14 +86,14 @@ bool host_pinned(const void* p, size_t bytes) {
     auto it = g_pinned.upper_bound(a);
     if (it == g_pinned.begin()) return false;
     --it;
-    return a >= it->first && a + bytes <= it->first + it->second;
+    return a >= it->first && a + bytes <= it->first + it->second.bytes;
 }
 }  // namespace sdrgpu
 extern "C" int sdrgpu_host_register(void* ptr, size_t bytes) {
     if (!ptr || bytes == 0) { set_error("host_register: empty range"); return SDRGPU_EARG; }
     SDRGPU_HIP(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
     std::lock_guard<std::mutex> lk(g_pinMtx);
-    g_pinned[(uintptr_t)ptr] = bytes;
+    g_pinned[(uintptr_t)ptr] = {bytes, false};
     return SDRGPU_OK;
 }
 extern "C" int sdrgpu_host_alloc(void** ptr, size_t bytes) {
@@ -86,23 +101,17 @@ extern "C" int sdrgpu_host_alloc(void** ptr, size_t bytes) {
     *ptr = nullptr;
     SDRGPU_HIP(hipHostMalloc(ptr, bytes, hipHostMallocDefault));
     std::lock_guard<std::mutex> lk(g_pinMtx);
-    g_pinned[(uintptr_t)*ptr] = bytes;
+    g_pinned[(uintptr_t)*ptr] = {bytes, true};
     return SDRGPU_OK;
 }
 extern "C" int sdrgpu_host_free(void* ptr) {
     if (!ptr) return SDRGPU_OK;
-    {
-        std::lock_guard<std::mutex> lk(g_pinMtx);
-        g_pinned.erase((uintptr_t)ptr);
-    }
+    SDRGPU_CHECK(take_pinned(ptr, true, "host_free"));
     SDRGPU_HIP(hipHostFree(ptr));
     return SDRGPU_OK;
 }
 extern "C" int sdrgpu_host_unregister(void* ptr) {
-    {
-        std::lock_guard<std::mutex> lk(g_pinMtx);
-        g_pinned.erase((uintptr_t)ptr);
-    }
+    SDRGPU_CHECK(take_pinned(ptr, false, "host_unregister"));
     SDRGPU_HIP(hipHostUnregister(ptr));
     return SDRGPU_OK;
 }

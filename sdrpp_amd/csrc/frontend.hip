@@ -595,5 +595,6 @@ extern "C" int sdrgpu_frontend_release(sdrgpu_frontend* f, int ticket) {
     PipeSlot* ps = pipe_find(f, ticket);
     if (!ps) return SDRGPU_EARG;
     ps->collected = true;
+    ps->ticket = -1;   // a released ticket is gone: a late collect / release gets SDRGPU_EARG
     return SDRGPU_OK;
 }

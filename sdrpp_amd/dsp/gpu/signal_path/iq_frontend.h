@@ -230,6 +230,9 @@ public:
     sdrgpu_frontend* device_frontend() { return _fe; }
     // (not in the reference) input blocks dropped by the lossy ring since init
     long long droppedBlocks() { return _ring.droppedCount(); }
+    // (not in the reference; test hook, call with the worker stopped) every input-ring slot is
+    // exactly once free, queued or held by the worker's block in flight
+    bool ringSlotsConsistent() { return _ring.consistent(_worker.pendingSlot >= 0 ? 1 : 0); }
 
 protected:
     struct Vfo {
@@ -303,10 +306,28 @@ protected:
             std::lock_guard<std::mutex> lk(mtx);
             return queue.empty();
         }
-        void release(int idx) {
+        // false (and no change) when idx is out of range, already free or still queued
+        bool release(int idx) {
             std::lock_guard<std::mutex> lk(mtx);
+            if (idx < 0 || idx >= RING_SLOTS) return false;
+            if (std::find(freeList.begin(), freeList.end(), idx) != freeList.end()) return false;
+            if (std::find(queue.begin(), queue.end(), idx) != queue.end()) return false;
             freeList.push_back(idx);
             cv.notify_all();
+            return true;
+        }
+        // every slot index exactly once over free + queued + the n in flight (test hook)
+        bool consistent(int inFlight) {
+            std::lock_guard<std::mutex> lk(mtx);
+            std::vector<int> seen(RING_SLOTS, 0);
+            for (int i : freeList) seen[i]++;
+            for (int i : queue) seen[i]++;
+            int missing = 0;
+            for (int c : seen) {
+                if (c > 1) return false;
+                missing += c == 0;
+            }
+            return missing == inFlight;
         }
         void flush() {
             std::lock_guard<std::mutex> lk(mtx);
@@ -413,8 +434,11 @@ protected:
     int iteration(Worker& w) {
         // nothing queued: hand on the block in flight first (no extra latency when keeping up)
         if (w.pendingTicket >= 0 && _ring.empty()) {
-            if (!deliver(w, w.pendingTicket, w.pendingSlot)) return -1;
+            // deliver() releases the ticket and the slot whatever it returns: clear them first,
+            // or a stop landing in an output swap would drop them a second time (doStop)
+            const int t = w.pendingTicket, s = w.pendingSlot;
             w.pendingTicket = w.pendingSlot = -1;
+            if (!deliver(w, t, s)) return -1;
         }
         const int slot = _ring.pop(true);
         if (slot < 0) return -1;
@@ -424,13 +448,16 @@ protected:
             ticket = sdrgpu_frontend_submit(_fe, _ring.data(slot), _ring.count(slot), -1, w.bound.empty() ? 0 : SDRGPU_FE_IQ);
         }
         if (!dsp::gpu::ok(ticket, "frontend_submit")) {
-            _ring.release(slot);
+            releaseSlot(slot);
             return -1;
         }
-        if (w.pendingTicket >= 0 && !deliver(w, w.pendingTicket, w.pendingSlot)) {
+        if (w.pendingTicket >= 0) {
+            const int t = w.pendingTicket, s = w.pendingSlot;
             w.pendingTicket = w.pendingSlot = -1;
-            dropTicket(ticket, slot);
-            return -1;
+            if (!deliver(w, t, s)) {
+                dropTicket(ticket, slot);
+                return -1;
+            }
         }
         w.pendingTicket = ticket;
         w.pendingSlot = slot;
@@ -452,8 +479,13 @@ protected:
                 if (sdrgpu_frontend_collected_vfo(_fe, ticket, v.vfo->frontEndId(), &p, &n) >= 0) outs.push_back({v.vfo, {p, n}});
             }
         }
-        _ring.release(slot);   // the block's H2D is done
+        releaseSlot(slot);   // the block's H2D is done
         bool ok = dsp::gpu::ok(nf, "frontend_collect");
+        // a stream buffer holds STREAM_BUFFER_SIZE samples (stream.h): an interpolating VFO's
+        // output past that fails the delivery instead of writing past writeBuf
+        for (auto& [vfo, pn] : outs)
+            if (pn.second > STREAM_BUFFER_SIZE) ok = dsp::gpu::ok(SDRGPU_EARG, "VFO output exceeds STREAM_BUFFER_SIZE");
+        if (niq > STREAM_BUFFER_SIZE) ok = dsp::gpu::ok(SDRGPU_EARG, "IQ block exceeds STREAM_BUFFER_SIZE");
         for (int r = 0; ok && r < nf; r++) {   // IQFrontEnd::handler's acquire -> write -> release per row
             float* buf = _acquireFFTBuffer(_fftCtx);
             if (buf) std::memcpy(buf, rows + (size_t)r * _fftSize, sizeof(float) * _fftSize);
@@ -473,13 +505,16 @@ protected:
         return ok;
     }
 
+    void releaseSlot(int slot) {
+        if (!_ring.release(slot)) SDRGPU_FE_ERROR("input ring slot released twice");
+    }
     void dropTicket(int ticket, int slot) {
         {
             std::lock_guard<std::mutex> l(_mtx);
             sdrgpu_frontend_collect(_fe, ticket, nullptr, nullptr, nullptr);
             sdrgpu_frontend_release(_fe, ticket);
         }
-        _ring.release(slot);
+        releaseSlot(slot);
     }
     void dropPending(Worker& w) {
         if (w.pendingTicket < 0) return;

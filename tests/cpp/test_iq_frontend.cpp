@@ -217,6 +217,32 @@ int main() {
         std::printf("lossy run: %d source blocks in %.1f ms, %lld dropped, VFO %lld -> %lld samples, rows %d -> %d\n", nb2,
                     srcMs, dropped, atSet, gotEnd, rowsAtSet, rowsEnd);
     }
+    // ---- a setter parks the worker while it is blocked in a VFO out.swap with the ring empty
+    // (the delivered block's ticket and ring slot were dropped a second time)
+    {
+        RowSink s3;
+        s3.buf.resize(N);
+        dsp::stream<dsp::complex_t> in3;
+        IQFrontEnd fe3;
+        fe3.init(&in3, fs, false, 1, false, N, 15.0, dsp::window::BLACKMAN_HARRIS7, acquire, release, &s3);
+        dsp::channel::RxVFO* v3 = fe3.addVFO("stalled", 48000, 12500, 150e3);   // nobody reads v3->out
+        fe3.start();
+        for (int round = 0; round < 4; round++) {
+            for (int b = 0; b < 3; b++) {   // the second delivery blocks in out.swap: the reader never flushes
+                std::memcpy(in3.writeBuf, x.data() + (size_t)b * blk, sizeof(dsp::complex_t) * blk);
+                if (!in3.swap(blk)) break;
+            }
+            std::this_thread::sleep_for(std::chrono::milliseconds(50));   // worker now waits in swap, ring empty
+            v3->setBandwidth(round % 2 ? 25000 : 12500);   // pause: tempStop -> stopWriter(out) -> swap false
+            std::this_thread::sleep_for(std::chrono::milliseconds(20));
+            fe3.stop();   // and again from stop() itself
+            CHECK(fe3.ringSlotsConsistent(), "round %d: an input-ring slot is free / queued twice or lost", round);
+            fe3.start();
+        }
+        fe3.stop();
+        CHECK(fe3.ringSlotsConsistent(), "after the stalled-consumer rounds: ring slots inconsistent");
+        std::printf("stalled-consumer run: ring slots consistent after 4 parks in out.swap\n");
+    }
     std::printf(failures ? "FAILED (%d)\n" : "ALL OK\n", failures);
     return failures ? 1 : 0;
 }
