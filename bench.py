@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline leg (1-core, all-core)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-sub", action="store_true", help="time only --config (no C2/C3/C4 sub-objects)")
+    ap.add_argument("--no-ulp", action="store_true", help="skip the live spectrum ulp report (profiling runs: "
+                    "only the timed config's kernels run)")
     return ap.parse_args()
 
 
@@ -262,7 +264,7 @@ def spectrum_ulp_report(dev=0, seed=20261017):
 def traffic_per_sample(config):
     """HBM bytes per input sample of the dominant launch group, from the newest committed
     rocprofv3 PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/pmc_bytes_per_sample.py)."""
-    for rnd in ("r3", "r2", "r1"):
+    for rnd in ("r4", "r3", "r2", "r1"):
         path = os.path.join(ROOT, "profiles", rnd, f"{config}_pmc_traffic.json")
         try:
             d = json.load(open(path))
@@ -533,7 +535,8 @@ def main():
             out["roofline_flops"] = head["roofline_flops"]
         if "gather" in head:
             out["gather"] = head["gather"]
-        out["spectrum_ulp"] = spectrum_ulp_report(dev)
+        if not a.no_ulp:
+            out["spectrum_ulp"] = spectrum_ulp_report(dev)
         if world == 1 and not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline("c4" if a.config == "c4g" else a.config, a.cpu_seconds)
             out["speedup_vs_cpu_all_cores"] = round(out["value"] / out["cpu_baseline"]["value"], 1)

@@ -107,6 +107,13 @@ int sdrgpu_fft_execute_vfo_dev(sdrgpu_fft* h, const void* in, int frames, float*
  * (acquireFFTBuffer may return NULL; the spectrum is then computed but not written). */
 int sdrgpu_fft_logmag(sdrgpu_fft* h, const void* in, float* out);
 int sdrgpu_fft_size(sdrgpu_fft* h);
+/* spectrum arithmetic (not in the reference: the north_star's <= 1 ulp parity mode):
+ * 0 = fp32 kernels (default; FFTW-class accuracy), 1 = fp64 interior: the reference's fp32 window
+ * product (volk_32fc_32f_multiply_32fc), then fp64 butterflies, twiddles, |X|^2 and 10 log10,
+ * rounded once to fp32 -- the correctly rounded dB of the exact DFT up to ~1e-15. Waits for the
+ * device; the zoom rows of sdrgpu_fft_execute_zoom_dev are then computed unfused. */
+int sdrgpu_fft_set_precision(sdrgpu_fft* h, int mode);
+int sdrgpu_fft_get_precision(sdrgpu_fft* h);
 int sdrgpu_fft_destroy(sdrgpu_fft* h);
 
 /* ---------------------------------------------------- stream blocks ---- */

@@ -22,6 +22,7 @@ SOURCES = [
     ("host_design.cpp", ["-ffp-contract=off"]),
     ("capi.cpp", []),
     ("fft.hip", []),
+    ("fft64.hip", []),
     ("blocks.hip", []),
     ("channelizer.hip", []),
     ("loops.hip", ["-ffp-contract=off"]),   # bit-exact serial recurrences
@@ -44,22 +45,27 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_lib(force=False):
-    os.makedirs(LIBDIR, exist_ok=True)
-    os.makedirs(BUILD, exist_ok=True)
+def build_lib(force=False, variant=None, defines=()):
+    """variant: an A/B build of the same ABI with extra -D defines, into build/<variant>/ and
+    sdrpp_amd/lib_<variant>/libsdrgpu.so (loaded through SDRGPU_LIB_PATH; tools/session.sh)."""
+    libdir = LIBDIR if not variant else os.path.join(ROOT, "sdrpp_amd", "lib_" + variant)
+    build = BUILD if not variant else os.path.join(BUILD, variant)
+    os.makedirs(libdir, exist_ok=True)
+    os.makedirs(build, exist_ok=True)
     headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     headers.append(os.path.join(ROOT, "include", "sdrgpu.h"))
     objs = []
     for src, extra in SOURCES:
         path = os.path.join(CSRC, src)
-        obj = os.path.join(BUILD, src + ".o")
+        obj = os.path.join(build, src + ".o")
         objs.append(obj)
         if force or _stale(obj, [path] + headers):
             lang = ["-x", "hip"] if src.endswith(".hip") else []
             _run([HIPCC, "--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17",
                   "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
-                  "-I", os.path.join(ROOT, "include")] + extra + lang + ["-c", path, "-o", obj])
-    lib = os.path.join(LIBDIR, "libsdrgpu.so")
+                  "-I", os.path.join(ROOT, "include")] + ["-D" + d for d in defines] + extra + lang +
+                 ["-c", path, "-o", obj])
+    lib = os.path.join(libdir, "libsdrgpu.so")
     if force or _stale(lib, objs):
         _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs + ["-ldl"])
     return lib
@@ -77,5 +83,9 @@ def build_oracle():
 
 if __name__ == "__main__":
     force = "--force" in sys.argv
-    build_lib(force)
+    args = [a for a in sys.argv[1:] if a != "--force"]
+    if args and args[0] == "--variant":   # python sdrpp_amd/build.py --variant NAME DEF [DEF ...]
+        build_lib(True, args[1], args[2:])
+    else:
+        build_lib(force)
     build_oracle()

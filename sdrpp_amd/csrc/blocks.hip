@@ -47,17 +47,17 @@ template <typename T> __device__ __forceinline__ T zero_of();
 template <> __device__ __forceinline__ float zero_of<float>() { return 0.0f; }
 template <> __device__ __forceinline__ float2 zero_of<float2>() { return make_float2(0.f, 0.f); }
 
-// atan2 of the FM quadrature (demod/quadrature.h:41-56: arg(y * conj(y[-1]))), for every kernel that
-// forms it. OCML's atan2f (an IEEE divide and special-case branches) cost ~8% of the fused C3 kernel
-// (DDCFM 0.77 vs DDC 0.70 ms, tools/c3_quad_cost.py). This is the CPU baseline's minimax polynomial
-// (oracle/cpu_fast.c) with v_rcp_f32: |error| <= 1.4 ulp(pi) (3.3e-7 rad, a numpy emulation over 4e6
-// random (y, x) spanning 17 decades), inside the quadrature bars of tests/ (8 ulp(pi) / dev vs the
-// reference code; 8 eps pi / dev + the FIR-error term in the fused-DDC tests). Signed zeros follow
-// C's atan2: atan2(+-0, +0) = +-0, atan2(+-0, -0) = +-pi (signbit, not x < 0).
+// atan2 of the FM quadrature (demod/quadrature.h:41-56: arg(y * conj(y[-1])) = complex_t::phase(), i.e.
+// atan2f), for every kernel that forms it: OCML's atan2f, the device libm's correctly-signed,
+// ~1-ulp counterpart of the reference's glibc atan2f (tests/test_ref_pinned.py pins it against the
+// reference-code fixture). Round 3 measured a minimax polynomial with v_rcp_f32 instead (|error| <=
+// 1.4 ulp(pi) absolute, far more ulps than that on small phase steps): C3 0.862 -> 0.850 ms, -1.3%
+// (profiles/r3/c3_atan/). Not worth the parity concession: it stays an A/B build only
+// (-DSDRGPU_POLY_ATAN2).
 __device__ __forceinline__ float quad_atan2f(float y, float x) {
-#ifdef SDRGPU_OCML_ATAN2   // (A/B builds only)
+#ifndef SDRGPU_POLY_ATAN2
     return atan2f(y, x);
-#endif
+#else
     const float ax = fabsf(x), ay = fabsf(y);
     const bool swp = ay > ax;
     const float mn = swp ? ax : ay, mx = swp ? ay : ax;
@@ -75,6 +75,7 @@ __device__ __forceinline__ float quad_atan2f(float y, float x) {
     r = swp ? 1.57079632679489662f - r : r;
     r = signbit(x) ? 3.14159265358979324f - r : r;
     return copysignf(r, y);
+#endif
 }
 
 // acc += x * h for the four (data, tap) type pairs of filter/fir.h:69-75

@@ -851,6 +851,7 @@ struct FftPlan {
     hipStream_t s2 = nullptr;
     hipEvent_t evFork = nullptr, evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr};
     DevBuf scratch2;
+    Fft64Plan* f64 = nullptr;         // sdrgpu_fft_set_precision(h, 1): the fp64-interior kernels (fft64.hip)
 };
 
 // t[m] = exp(-2 pi i (m * step) / L) for m < count (fp64 -> float)
@@ -1242,6 +1243,23 @@ extern "C" int sdrgpu_fft_set_window_type(sdrgpu_fft* h, int windowType, int nz)
 
 extern "C" int sdrgpu_fft_size(sdrgpu_fft* h) { return h ? h->p.N : SDRGPU_EARG; }
 
+// Spectrum arithmetic: 0 = fp32 kernels (default), 1 = fp64 interior (fft64.hip: the fp32 window
+// product as the reference forms it, then fp64 butterflies, twiddles, |X|^2 and dB, rounded once)
+extern "C" int sdrgpu_fft_set_precision(sdrgpu_fft* h, int mode) {
+    if (!h || mode < 0 || mode > 1) { set_error("fft_set_precision: bad argument"); return SDRGPU_EARG; }
+    FftPlan& p = h->p;
+    SDRGPU_SET_DEVICE(p.device);
+    SDRGPU_HIP(hipDeviceSynchronize());   // no call of the plan in flight while its kernels change
+    if (mode == 0 && p.f64) {
+        fft64_destroy(p.f64);
+        p.f64 = nullptr;
+    } else if (mode == 1 && !p.f64) {
+        SDRGPU_CHECK(fft64_create(&p.f64, p.N));
+    }
+    return SDRGPU_OK;
+}
+extern "C" int sdrgpu_fft_get_precision(sdrgpu_fft* h) { return h ? (h->p.f64 ? 1 : 0) : SDRGPU_EARG; }
+
 static bool zoom_fusable(const FftPlan& p, int zoomSize) {
     return p.N1 == 256 && p.N2 == 256 && p.sa == 32 && p.sb == 32 && zoomSize * 32 == p.N;
 }
@@ -1251,6 +1269,7 @@ static int fft_execute(sdrgpu_fft* h, const void* in, long long frameStride, int
                        hipStream_t s) {
     FftPlan& p = h->p;
     const float2* x = (const float2*)in;
+    if (p.f64) return fft64_execute(p.f64, x, frameStride, frames, p.win.as<float>(), p.nz, out, s);   // (zoom: unfused)
     if (p.N1 == 0) {
         SDRGPU_CHECK(dispatch_single(p, x, frameStride, frames, out, s));
         return frames;
@@ -1337,7 +1356,7 @@ int sdrgpu::fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const f
     if (!h || !body || frames <= 0 || nh < 0 || (nh > 0 && !head)) return SDRGPU_ESTATE;
     FftPlan& p = h->p;
     // the 64k plan's default tiles (256 x 256, 32 columns / 32 rows, one-column pass A); one chunk
-    if (!(p.N1 == 256 && p.N2 == 256 && p.sa == 32 && p.sb == 32 && p.sa2 == 0) || frames > p.chunkFrames || nh >= p.nz)
+    if (p.f64 || !(p.N1 == 256 && p.N2 == 256 && p.sa == 32 && p.sb == 32 && p.sa2 == 0) || frames > p.chunkFrames || nh >= p.nz)
         return SDRGPU_ESTATE;
     SDRGPU_CHECK(p.scratch.ensure((size_t)frames * p.N * sizeof(float2)));
     p.cur = p.scratch.as<float2>();
@@ -1368,7 +1387,7 @@ extern "C" int sdrgpu_fft_execute_zoom_dev(sdrgpu_fft* h, const void* in, long l
     hipStream_t s = stream ? (hipStream_t)stream : p.own;
     SDRGPU_CHECK(p.order.follow(s));
     OrderScope od(p.order, s);
-    if (zoom_fusable(p, zoomSize)) return fft_execute(h, in, frameStride, frames, out, zoomOut, s);
+    if (zoom_fusable(p, zoomSize) && !p.f64) return fft_execute(h, in, frameStride, frames, out, zoomOut, s);
     SDRGPU_CHECK(fft_execute(h, in, frameStride, frames, out, nullptr, s));
     if (!p.zoom || p.zoomSize != zoomSize) {
         if (p.zoom) sdrgpu_zoom_destroy(p.zoom);
@@ -1436,6 +1455,7 @@ extern "C" int sdrgpu_fft_destroy(sdrgpu_fft* h) {
     (void)hipSetDevice(h->p.device);
     if (h->p.own) (void)hipStreamDestroy(h->p.own);
     if (h->p.zoom) sdrgpu_zoom_destroy(h->p.zoom);
+    if (h->p.f64) fft64_destroy(h->p.f64);
     if (h->p.s2) {
         (void)hipStreamSynchronize(h->p.s2);
         (void)hipStreamDestroy(h->p.s2);

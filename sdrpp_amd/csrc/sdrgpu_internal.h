@@ -160,4 +160,10 @@ struct SideCopy {
 // SDRGPU_ESTATE when the plan has no such path (the caller then stitches and calls fft_execute_owned).
 int fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const float2* body, long long stride, int frames, float* out,
                       const SideCopy& side, hipStream_t s);
+// fp64-interior spectrum (fft64.hip): the opt-in parity mode behind sdrgpu_fft_set_precision
+struct Fft64Plan;
+int fft64_create(Fft64Plan** out, int N);
+void fft64_destroy(Fft64Plan* p);
+int fft64_execute(Fft64Plan* p, const float2* in, long long stride, int frames, const float* win, int nz, float* out,
+                  hipStream_t s);
 }  // namespace sdrgpu

@@ -213,10 +213,20 @@ class BroadcastFM(Block):
 class FFTSpectrum:
     """IQFrontEnd's FFT path (signal_path/iq_frontend.cpp:230-249, 272-296)."""
 
-    def __init__(self, fft_size, nz=None, window=6, device=0):
+    def __init__(self, fft_size, nz=None, window=6, device=0, precision="f32"):
+        """precision "f64": the fp64-interior parity mode (sdrgpu_fft_set_precision(h, 1))."""
         self.N = int(fft_size)
         self.nz = int(nz if nz is not None else fft_size)
         self._h = _make(lib.sdrgpu_fft_create, device, self.N, self.nz, int(window))
+        if precision != "f32":
+            self.set_precision(precision)
+
+    def set_precision(self, precision):
+        check(lib.sdrgpu_fft_set_precision(self._h, {"f32": 0, "f64": 1}[precision]))
+
+    @property
+    def precision(self):
+        return ("f32", "f64")[check(lib.sdrgpu_fft_get_precision(self._h))]
 
     def set_window(self, w):
         w = np.ascontiguousarray(w, dtype=np.float32)

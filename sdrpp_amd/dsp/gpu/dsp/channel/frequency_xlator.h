@@ -4,6 +4,12 @@
 #pragma once
 #include "../processor.h"
 #include "../sdrgpu_handle.h"
+// the reference header's own includes (core/src/dsp/channel/frequency_xlator.h): callers such as
+// decoder_modules/radio/src/demodulators/*.h rely on them transitively. Headers that exist
+// only in the SDR++ tree are guarded, so the block-API mirror build skips them.
+#if __has_include("../math/hz_to_rads.h")
+#include "../math/hz_to_rads.h"
+#endif
 
 namespace dsp::channel {
 class FrequencyXlator : public Processor<complex_t, complex_t> {

@@ -5,6 +5,11 @@
 #include <mutex>
 #include "../processor.h"
 #include "../sdrgpu_handle.h"
+// the reference header's own includes (core/src/dsp/channel/rx_vfo.h): callers such as
+// decoder_modules/radio/src/demodulators/*.h rely on them transitively. Headers that exist
+// only in the SDR++ tree are guarded, so the block-API mirror build skips them.
+#include "frequency_xlator.h"
+#include "../multirate/rational_resampler.h"
 
 namespace dsp::channel {
 class RxVFO : public Processor<complex_t, complex_t> {

@@ -6,6 +6,18 @@
 #include <type_traits>
 #include "../processor.h"
 #include "../sdrgpu_handle.h"
+// the reference header's own includes (core/src/dsp/demod/am.h): callers such as
+// decoder_modules/radio/src/demodulators/*.h rely on them transitively. Headers that exist
+// only in the SDR++ tree are guarded, so the block-API mirror build skips them.
+#include "../loop/agc.h"
+#include "../correction/dc_blocker.h"
+#if __has_include("../convert/mono_to_stereo.h")
+#include "../convert/mono_to_stereo.h"
+#endif
+#include "../filter/fir.h"
+#if __has_include("../taps/low_pass.h")
+#include "../taps/low_pass.h"
+#endif
 
 namespace dsp::demod {
 template <class T>

@@ -9,6 +9,45 @@
 #pragma once
 #include "../processor.h"
 #include "../sdrgpu_handle.h"
+// the reference header's own includes (core/src/dsp/demod/broadcast_fm.h): callers such as
+// decoder_modules/radio/src/demodulators/*.h rely on them transitively. Headers that exist
+// only in the SDR++ tree are guarded, so the block-API mirror build skips them.
+#include "quadrature.h"
+#if __has_include("../taps/low_pass.h")
+#include "../taps/low_pass.h"
+#endif
+#if __has_include("../taps/band_pass.h")
+#include "../taps/band_pass.h"
+#endif
+#include "../filter/fir.h"
+#if __has_include("../loop/pll.h")
+#include "../loop/pll.h"
+#endif
+#if __has_include("../convert/l_r_to_stereo.h")
+#include "../convert/l_r_to_stereo.h"
+#endif
+#if __has_include("../convert/real_to_complex.h")
+#include "../convert/real_to_complex.h"
+#endif
+#if __has_include("../convert/complex_to_real.h")
+#include "../convert/complex_to_real.h"
+#endif
+#if __has_include("../math/conjugate.h")
+#include "../math/conjugate.h"
+#endif
+#if __has_include("../math/delay.h")
+#include "../math/delay.h"
+#endif
+#if __has_include("../math/multiply.h")
+#include "../math/multiply.h"
+#endif
+#if __has_include("../math/add.h")
+#include "../math/add.h"
+#endif
+#if __has_include("../math/subtract.h")
+#include "../math/subtract.h"
+#endif
+#include "../multirate/rational_resampler.h"
 
 namespace dsp::demod {
 class BroadcastFM : public Processor<complex_t, stereo_t> {

@@ -5,6 +5,23 @@
 #include <vector>
 #include "../processor.h"
 #include "../sdrgpu_handle.h"
+// the reference header's own includes (core/src/dsp/demod/fm.h): callers such as
+// decoder_modules/radio/src/demodulators/*.h rely on them transitively. Headers that exist
+// only in the SDR++ tree are guarded, so the block-API mirror build skips them.
+#include "quadrature.h"
+#include "../filter/fir.h"
+#if __has_include("../taps/low_pass.h")
+#include "../taps/low_pass.h"
+#endif
+#if __has_include("../taps/high_pass.h")
+#include "../taps/high_pass.h"
+#endif
+#if __has_include("../taps/band_pass.h")
+#include "../taps/band_pass.h"
+#endif
+#if __has_include("../convert/mono_to_stereo.h")
+#include "../convert/mono_to_stereo.h"
+#endif
 
 namespace dsp::demod {
 template <class T>

@@ -4,6 +4,18 @@
 #pragma once
 #include "../processor.h"
 #include "../sdrgpu_handle.h"
+// the reference header's own includes (core/src/dsp/demod/quadrature.h): callers such as
+// decoder_modules/radio/src/demodulators/*.h rely on them transitively. Headers that exist
+// only in the SDR++ tree are guarded, so the block-API mirror build skips them.
+#if __has_include("../math/fast_atan2.h")
+#include "../math/fast_atan2.h"
+#endif
+#if __has_include("../math/hz_to_rads.h")
+#include "../math/hz_to_rads.h"
+#endif
+#if __has_include("../math/normalize_phase.h")
+#include "../math/normalize_phase.h"
+#endif
 
 namespace dsp::demod {
 class Quadrature : public Processor<complex_t, float> {

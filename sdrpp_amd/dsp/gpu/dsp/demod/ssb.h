@@ -5,6 +5,17 @@
 #include <type_traits>
 #include "../processor.h"
 #include "../sdrgpu_handle.h"
+// the reference header's own includes (core/src/dsp/demod/ssb.h): callers such as
+// decoder_modules/radio/src/demodulators/*.h rely on them transitively. Headers that exist
+// only in the SDR++ tree are guarded, so the block-API mirror build skips them.
+#include "../channel/frequency_xlator.h"
+#if __has_include("../convert/complex_to_real.h")
+#include "../convert/complex_to_real.h"
+#endif
+#include "../loop/agc.h"
+#if __has_include("../convert/mono_to_stereo.h")
+#include "../convert/mono_to_stereo.h"
+#endif
 
 namespace dsp::demod {
 template <class T>

@@ -6,6 +6,12 @@
 #include "../processor.h"
 #include "../taps/tap.h"
 #include "../sdrgpu_handle.h"
+// the reference header's own includes (core/src/dsp/multirate/polyphase_resampler.h): callers such as
+// decoder_modules/radio/src/demodulators/*.h rely on them transitively. Headers that exist
+// only in the SDR++ tree are guarded, so the block-API mirror build skips them.
+#if __has_include("polyphase_bank.h")
+#include "polyphase_bank.h"
+#endif
 
 namespace dsp::multirate {
 template <class T>

@@ -4,6 +4,16 @@
 #include <type_traits>
 #include "../processor.h"
 #include "../sdrgpu_handle.h"
+// the reference header's own includes (core/src/dsp/multirate/power_decimator.h): callers such as
+// decoder_modules/radio/src/demodulators/*.h rely on them transitively. Headers that exist
+// only in the SDR++ tree are guarded, so the block-API mirror build skips them.
+#include "../filter/decimating_fir.h"
+#if __has_include("../taps/from_array.h")
+#include "../taps/from_array.h"
+#endif
+#if __has_include("decim/plans.h")
+#include "decim/plans.h"
+#endif
 
 namespace dsp::multirate {
 template <class T>

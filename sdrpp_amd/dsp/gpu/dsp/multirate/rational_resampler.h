@@ -5,6 +5,26 @@
 #include <type_traits>
 #include "../processor.h"
 #include "../sdrgpu_handle.h"
+// the reference header's own includes (core/src/dsp/multirate/rational_resampler.h): callers such as
+// decoder_modules/radio/src/demodulators/*.h rely on them transitively. Headers that exist
+// only in the SDR++ tree are guarded, so the block-API mirror build skips them.
+#include <vector>
+#include <numeric>
+#include "../filter/decimating_fir.h"
+#if __has_include("../taps/from_array.h")
+#include "../taps/from_array.h"
+#endif
+#include "polyphase_resampler.h"
+#include "power_decimator.h"
+#if __has_include("../taps/low_pass.h")
+#include "../taps/low_pass.h"
+#endif
+#if __has_include("../window/nuttall.h")
+#include "../window/nuttall.h"
+#endif
+#if __has_include("utils/flog.h")
+#include "utils/flog.h"
+#endif
 
 namespace dsp::multirate {
 template <class T>

@@ -44,6 +44,36 @@
 #include "../dsp/stream.h"
 #include "../dsp/window/window.h"
 #include "../dsp/channel/rx_vfo.h"
+// the reference header's own includes (core/src/signal_path/iq_frontend.h:2-12): callers rely on
+// them transitively (the radio module's WFM takes dsp::sink::Handler and dsp::buffer::Reshaper
+// through signal_path.h). Headers that exist only in the SDR++ tree are guarded.
+#if __has_include("../dsp/buffer/frame_buffer.h")
+#include "../dsp/buffer/frame_buffer.h"
+#endif
+#if __has_include("../dsp/buffer/reshaper.h")
+#include "../dsp/buffer/reshaper.h"
+#endif
+#if __has_include("../dsp/multirate/power_decimator.h")
+#include "../dsp/multirate/power_decimator.h"
+#endif
+#if __has_include("../dsp/correction/dc_blocker.h")
+#include "../dsp/correction/dc_blocker.h"
+#endif
+#if __has_include("../dsp/chain.h")
+#include "../dsp/chain.h"
+#endif
+#if __has_include("../dsp/routing/splitter.h")
+#include "../dsp/routing/splitter.h"
+#endif
+#if __has_include("../dsp/sink/handler_sink.h")
+#include "../dsp/sink/handler_sink.h"
+#endif
+#if __has_include("../dsp/math/conjugate.h")
+#include "../dsp/math/conjugate.h"
+#endif
+#if __has_include(<fftw3.h>)
+#include <fftw3.h>
+#endif
 #if __has_include("../core.h")
 #include "../core.h"
 #include "../gui/gui.h"
