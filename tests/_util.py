@@ -25,19 +25,19 @@ def assert_close_c(a, b, atol, what=""):
 
 
 def db_check(db_gpu, power_true, N, ref32_db=None, floor_db=60.0):
-    """Spectrum parity (DESIGN.md 'Parity bar'), on bins within `floor_db` of the frame peak:
-    1. the GPU's dB error vs the fp64 truth is in the accuracy class of a reference-class fp32
-       FFT (pocketfft single precision) on the same windowed input: rms <= 2x its rms (+ the
-       rms of 1 ulp of the fp32 dB values) and max <= 8x its max (+2 ulp of the fp32 dB value).
-       The max bar is a ratio of two single-bin maxima, a heavy-tailed statistic: over 504 random
-       frames (4k / 16k / 64k, all 7 windows; profiles/r3/fft_cmul/) it reached 5.72x for the
-       round-2 kernels and 6.63x with the packed-asm complex multiply (p99 3.2x / 3.6x), while the
-       rms ratio stayed at 0.97 / 0.98 (mean). A 3x bar failed 9 / 10 of those frames for the two
-       builds, so it was a coin toss at the 2% level; 8x sits above both tails, and the rms bar
-       carries the accuracy class;
-    2. normwise: || |X_gpu| - |X_true| ||_2 <= 4 * eps32 * log2(N) * ||X_true||_2 (all bins).
-    Without a reference-class FFT the bound is 2e-4 dB.
-    """
+    """Spectrum parity (DESIGN.md §4 'Parity bar'), on bins within `floor_db` of the frame peak.
+    With a reference-class fp32 FFT (pocketfft single precision) on the same windowed frame:
+    1. rms dB error <= 2x its rms (+ the rms of 1 ulp of the fp32 dB values);
+    2. per bin, in fp32 ulps of the correctly rounded dB of the exact DFT (db_ulp_errors), against
+       pocketfft's ulps on the SAME frame (round 4; replaces round 3's 8x ratio of two single-bin dB
+       maxima): within-1-ulp fraction >= pocketfft's - 1 point and p99.9 <= pocketfft's + 4 ulp
+       (frames with >= 1000 bins in range), worst bin <= 4x pocketfft's worst + 16 ulp. Measured over
+       the 510-frame corpus (corpus_ulp_rows, profiles/r4/spectrum_corpus_*.json): fraction -0.59
+       points at worst, p99.9 +3 ulp, worst bin 68 vs 17 ulp (4.0x) on one frame -- a heavy-tailed
+       statistic, which is why the corpus test (test_spectrum_ulp_corpus) bounds the worst bins over
+       all frames as well;
+    3. normwise: || |X_gpu| - |X_true| ||_2 <= 4 * eps32 * log2(N) * ||X_true||_2 (all bins).
+    Without a reference-class FFT the bound is 2e-4 dB."""
     db_true = 10.0 * np.log10(np.maximum(power_true, 1e-300))
     peak = db_true.max()
     sel = db_true >= peak - floor_db
@@ -51,7 +51,12 @@ def db_check(db_gpu, power_true, N, ref32_db=None, floor_db=60.0):
         # (log10f + the x10 rounding); the scipy row here is rounded once from fp64
         ulp_rms = np.sqrt(np.mean(ulp ** 2))
         assert rms_g <= 2.0 * rms_r + ulp_rms + 1e-12, f"rms dB err {rms_g:.3e} > 2 x fp32-ref {rms_r:.3e} + ulp {ulp_rms:.3e}"
-        assert np.all(err <= 8.0 * rerr.max() + 2.0 * ulp), f"max dB err {err.max():.3e} > 8 x fp32-ref {rerr.max():.3e}"
+        eg, er = db_ulp_errors(db_gpu, power_true, floor_db), db_ulp_errors(ref32_db, power_true, floor_db)
+        sg, sr = ulp_stats(eg), ulp_stats(er)
+        if eg.size >= 1000:
+            assert sg["frac_le_1ulp"] >= sr["frac_le_1ulp"] - 0.01, (sg, sr)
+            assert sg["p999"] <= sr["p999"] + 4.0, (sg, sr)
+        assert sg["max"] <= 4.0 * sr["max"] + 16.0, (sg, sr)
     else:
         assert np.all(err <= np.maximum(2e-4, 2.0 * ulp)), f"max dB err {err.max():.3e}"
     mag_gpu = np.sqrt(10.0 ** (db_gpu.astype(np.float64) / 10.0))
@@ -59,6 +64,66 @@ def db_check(db_gpu, power_true, N, ref32_db=None, floor_db=60.0):
     nerr = np.linalg.norm(mag_gpu - mag_true) / np.linalg.norm(mag_true)
     assert nerr <= 4 * EPS32 * np.log2(N), f"normwise magnitude error {nerr:.3e}"
     return err.max(), nerr
+
+
+def ulp_stats(e):
+    return {"frac_le_1ulp": float(np.mean(e <= 1.0)), "p999": float(np.percentile(e, 99.9)), "max": float(e.max())}
+
+
+def corpus_frame(N, nz, wt, k):
+    """Seed-fixed random frame k of the spectrum corpus (depends only on N, window, k)."""
+    rng = np.random.default_rng(1234 + wt + 100 * k + 7 * N)
+    return (rng.uniform(-1, 1, nz) + 1j * rng.uniform(-1, 1, nz)).astype(np.complex64)
+
+
+def corpus_ulp_rows(frames=24, f1m=6, sizes=(4096, 16384, 65536)):
+    """The spectrum accuracy corpus: sizes x the 7 window types x `frames` random frames, plus `f1m`
+    1M-point frames (nz = 1e6, BH7). Per frame: the GPU's (fp32 kernels and fp64-interior mode) and
+    pocketfft's ulp statistics against the fp64 truth (bins within 60 dB of the peak)."""
+    import oracle
+    from sdrpp_amd import dsp
+    cases = [(N, N, wt, k) for N in sizes for wt in range(7) for k in range(frames)]
+    cases += [(1 << 20, 1000000, 6, k) for k in range(f1m)]
+    plans, rows = {}, []
+    for N, nz, wt, k in cases:
+        if (N, nz, wt) not in plans:
+            plans[(N, nz, wt)] = (dsp.FFTSpectrum(N, nz, wt), dsp.FFTSpectrum(N, nz, wt, precision="f64"))
+        f32, f64 = plans[(N, nz, wt)]
+        x = corpus_frame(N, nz, wt, k)
+        w = oracle.create_window(wt, nz)
+        truth = oracle.fft_truth_power(x, nz, N, w)
+        e = db_ulp_errors(f32.logmag(x), truth)
+        er = db_ulp_errors(ref32_fft_db(x, nz, N, w), truth)
+        e64 = db_ulp_errors(f64.logmag(x), truth)
+        g, r = ulp_stats(e), ulp_stats(er)
+        rows.append({"N": N, "nz": nz, "w": wt, "k": k, "bins": int(e.size), "gpu": g, "pocketfft": r,
+                     "max_ratio": g["max"] / max(r["max"], 1.0), "f64_max": float(e64.max()),
+                     "f64_frac_exact": float(np.mean(e64 == 0))})
+    return rows
+
+
+def corpus_aggregate(rows):
+    agg = {}
+    for N in sorted({r["N"] for r in rows}):
+        rs = [r for r in rows if r["N"] == N]
+        agg[str(N)] = {
+            "frames": len(rs),
+            "gpu_min_frac_le_1ulp": min(r["gpu"]["frac_le_1ulp"] for r in rs),
+            "pocketfft_min_frac_le_1ulp": min(r["pocketfft"]["frac_le_1ulp"] for r in rs),
+            "min_frac_diff": min(r["gpu"]["frac_le_1ulp"] - r["pocketfft"]["frac_le_1ulp"] for r in rs),
+            "gpu_max_p999": max(r["gpu"]["p999"] for r in rs),
+            "pocketfft_max_p999": max(r["pocketfft"]["p999"] for r in rs),
+            "max_p999_diff": max(r["gpu"]["p999"] - r["pocketfft"]["p999"] for r in rs),
+            "gpu_max": max(r["gpu"]["max"] for r in rs),
+            "pocketfft_max": max(r["pocketfft"]["max"] for r in rs),
+            "gpu_mean_frame_max": float(np.mean([r["gpu"]["max"] for r in rs])),
+            "pocketfft_mean_frame_max": float(np.mean([r["pocketfft"]["max"] for r in rs])),
+            "frames_max_ratio_gt_1.25": sum(r["max_ratio"] > 1.25 for r in rs),
+            "worst_max_ratio": max(r["max_ratio"] for r in rs),
+            "f64_max": max(r["f64_max"] for r in rs),
+            "f64_min_frac_exact": min(r["f64_frac_exact"] for r in rs),
+        }
+    return agg
 
 
 def db_ulp_errors(db, power_true, floor_db=60.0):
