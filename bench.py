@@ -71,24 +71,48 @@ class C5:
         # doZoom), fused into the transform's last pass; double-buffered for the rank-0 gather
         self.zoom = [torch.empty(self.frames * self.ZW, dtype=torch.float32, device="cuda") for _ in range(2)]
         self.with_zoom = os.environ.get("BENCH_C5_ZOOM", "1") != "0"
+        # one launch group for the spectrum, the zoom rows and the VFO's first stage, which reads the
+        # IQ batch the spectrum reads (sdrgpu_fft_execute_zoom_vfo_dev); BENCH_C5_FUSE=0 (A/B only):
+        # the spectrum group and the VFO as separate launch groups, as in round 3
+        self.fuse = os.environ.get("BENCH_C5_FUSE", "1") != "0"
         self.zoom_count = self.frames * self.ZW
         self.bytes_per_sample = 8 + 4 + 4 / 32 + 8 / 256 + 8 / 256   # SURVEY 8(d) C5 (~12.06 B) + the zoom rows
-        self.kernel_bytes = (12.0 + 4 / 32) * self.B            # spectrum: 8 B in, 4 B dB + 4/32 B zoom out
-        self.kernel_name = ("spectrum N=65536 + zoom to 2048: fft_passA_kernel<256,32> (chunk 0) + "
-                            "fft_merged_kernel<256,32,256,32,false,zoom> (pass B chunk c + pass A chunk c+1) x15 + "
-                            "fft_passB_kernel<256,32,zoom> (last chunk)")
+        if self.fuse:
+            # the group: 8 B in (read once), 4 B dB + 4/32 B zoom rows out, 8/32 B VFO stage-1 out
+            self.kernel_bytes = (12.0 + 4 / 32 + 8 / 32) * self.B
+            self.kernel_name = ("spectrum N=65536 + zoom to 2048 + RxVFO stage 1 (D=32, 143 taps, xlator): "
+                                "fft_vfo_kernel<zoom,0> x17 (pass-A tiles of each frame dispatched beside the "
+                                "workgroup computing that frame's stage-1 outputs; pass B of the previous chunk)")
+            self.fft.set_timing(True)   # the group's own HIP events (the VFO's later stages are outside it)
+        else:
+            self.kernel_bytes = (12.0 + 4 / 32) * self.B            # spectrum: 8 B in, 4 B dB + 4/32 B zoom out
+            self.kernel_name = ("spectrum N=65536 + zoom to 2048: fft_passA_kernel<256,32> (chunk 0) + "
+                                "fft_merged_kernel<256,32,256,32,false,zoom> (pass B chunk c + pass A chunk c+1) x15 + "
+                                "fft_passB_kernel<256,32,zoom> (last chunk)")
 
     def run(self, x, s, timed_call, buf=0):
         # the front end's splitter hands the same block to the spectrum and the VFO
         # (iq_frontend.cpp:15-52); the VFO output then feeds the WFM demodulator
-        if self.with_zoom:
-            timed_call(lambda: self.fft.execute_zoom_dev(x.data_ptr(), self.N, self.frames, self.spectra.data_ptr(),
-                                                         self.zoom[buf].data_ptr(), self.ZW, s))
-        else:   # (A/B only: BENCH_C5_ZOOM=0 drops the waterfall rows)
-            timed_call(lambda: self.fft.execute_dev(x.data_ptr(), self.N, self.frames, self.spectra.data_ptr(), s))
-        m = self.vfo.process_dev(x.data_ptr(), self.B, self.ifbuf.data_ptr(), s)
+        if self.fuse:
+            z = self.zoom[buf].data_ptr() if self.with_zoom else 0
+            m = self.fft.execute_zoom_vfo_dev(x.data_ptr(), self.frames, self.spectra.data_ptr(), z, self.ZW, self.vfo,
+                                              self.ifbuf.data_ptr(), s)
+        else:
+            if self.with_zoom:
+                timed_call(lambda: self.fft.execute_zoom_dev(x.data_ptr(), self.N, self.frames, self.spectra.data_ptr(),
+                                                             self.zoom[buf].data_ptr(), self.ZW, s))
+            else:   # (A/B only: BENCH_C5_ZOOM=0 drops the waterfall rows)
+                timed_call(lambda: self.fft.execute_dev(x.data_ptr(), self.N, self.frames, self.spectra.data_ptr(), s))
+            m = self.vfo.process_dev(x.data_ptr(), self.B, self.ifbuf.data_ptr(), s)
         self.wfm.process_dev(self.ifbuf.data_ptr(), m, self.audio.data_ptr(), s)
 
+    def group_ms(self, steps):
+        """The dominant group's mean time over the timed steps from the library's own HIP events
+        (sdrgpu_fft_group_times), or None when the group is timed by the bench's events."""
+        if not self.fuse:
+            return None
+        t = self.fft.group_times(steps)
+        return float(np.mean(t)) if len(t) == steps else None
 
 
 class C2:
@@ -348,6 +372,8 @@ def run_config(config, a, shard, dev, stream):
     shard.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(sum(e0.elapsed_time(e1) for e0, e1 in evs) for evs in ev) / max(len(ev), 1)
+    if hasattr(wl, "group_ms") and wl.group_ms(a.steps) is not None:
+        kern_ms = wl.group_ms(a.steps)
     elapsed, kern_ms = shard.max_over_ranks([elapsed, kern_ms], device="cuda")
     if pipe is not None:
         # the first multi-GPU run proves the gather: rank 0's received rows of the last step carry

@@ -100,9 +100,20 @@ int sdrgpu_fft_execute_zoom_dev(sdrgpu_fft* h, const void* in, long long frameSt
                                 float* zoomOut, int zoomSize, void* stream);
 /* spectrum + one RxVFO over the same device batch of `frames` back-to-back frames (frame stride
  * N, nz = N: fftRate = fs / N), the VFO reading the batch in place as the front end's splitter
- * feeds both (iq_frontend.cpp:15-52), on one stream. Returns the VFO's output count (vfoOut). */
+ * feeds both (iq_frontend.cpp:15-52, splitter.h:46-60), on one stream. Returns the VFO's output
+ * count (vfoOut). On the 64k plan with an RxVFO whose first stage is the D = 32 row decimator
+ * (61.44 MS/s -> 240 kHz) that stage runs inside the spectrum launches, so the batch is read from
+ * HBM once; otherwise the spectrum and the VFO run as two launch groups. */
 int sdrgpu_fft_execute_vfo_dev(sdrgpu_fft* h, const void* in, int frames, float* out, sdrgpu_block* vfo,
                                void* vfoOut, void* stream);
+/* the same + the waterfall's full-span zoom rows (as sdrgpu_fft_execute_zoom_dev; zoomOut may be NULL) */
+int sdrgpu_fft_execute_zoom_vfo_dev(sdrgpu_fft* h, const void* in, int frames, float* out, float* zoomOut,
+                                    int zoomSize, sdrgpu_block* vfo, void* vfoOut, void* stream);
+/* (measurement, not in the reference) HIP events around each call's spectrum launch group -- the
+ * fused VFO stage included, the VFO's later stages not; group_times returns the last
+ * min(n, calls, 256) group times in ms, oldest first, waiting for them */
+int sdrgpu_fft_set_timing(sdrgpu_fft* h, int on);
+int sdrgpu_fft_group_times(sdrgpu_fft* h, float* ms, int n);
 /* drop-in for IQFrontEnd::handler: in = host complex_t[nz]; out = host float[N] or NULL
  * (acquireFFTBuffer may return NULL; the spectrum is then computed but not written). */
 int sdrgpu_fft_logmag(sdrgpu_fft* h, const void* in, float* out);

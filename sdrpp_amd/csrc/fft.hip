@@ -18,6 +18,7 @@
 #include <algorithm>
 #include "sdrgpu_internal.h"
 #include "fft_stages.h"
+#include "fir_rows.h"
 
 #ifndef SDRGPU_PB_NT
 #define SDRGPU_PB_NT 1   // 64k pass B: streaming dB row stores (A/B builds: 0)
@@ -123,7 +124,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, unsigned 
 // from the N-entry Tfull[k1][n2] table (contiguous per 16 lanes, L2-resident). A product of
 // two table values (W_N^(S b k1) x W_N^(c k1)) saved a little table space but added an
 // fp32 rounding: the 64k spectrum's rms dB error on a tonal signal was 2.1x pocketfft's.
-template <int L, int S>
+template <int L, int S, int CP = SDRGPU_PA_CP>   // CP: cache policy of the 256-point input loads
 __device__ __forceinline__ void passA_tile(
     float2* lds, int tile, const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win,
     int nz, int N2, int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull,
@@ -176,7 +177,7 @@ __device__ __forceinline__ void passA_tile(
         } else if (nz >= L * N2) {   // no zero padding (wave-uniform)
 #pragma unroll
             for (int r = 0; r < 16; r++) {
-                xv[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, o0 * 8, r * rowB, SDRGPU_PA_CP));
+                xv[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, o0 * 8, r * rowB, CP));
                 wv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, o0 * 4, r * rowB / 2, 0));
             }
         } else {              // zero-padded tail: clamped (in-bounds) loads, then select
@@ -811,6 +812,50 @@ __global__ __launch_bounds__((PAIRED ? SA / 2 : SA) * LA / 16) __attribute__((am
     }
 }
 
+// ---- spectrum launches that also run a VFO's first stage over the same batch ---------------
+// (sdrgpu_fft_execute_vfo_dev / _zoom_vfo_dev on the 64k plan: 256 x 256, 32-column / 32-row
+// tiles, 512 threads.) The IQ batch is read from HBM once: each pass-A frame's 8 column tiles are
+// dispatched next to one workgroup that computes the VFO stage-1 outputs of the same 65,536
+// samples (2,048 outputs of the D = 32, 143-tap decimator = 16 row-kernel segments of 128, one per
+// D-lane group of its 8 waves), so the second reader of every line finds it in the Infinity Cache
+// (or L2) instead of HBM (splitter.h:46-60 fans the block out with one memcpy per consumer; here no
+// consumer copies it). Pass A's input loads keep the default cache policy (CP) for that reason.
+// The stage's outputs are bit-identical to fir_rows_kernel's (the same fir_rows_segment; only the
+// row batch is smaller, to fit the spectrum's 128-VGPR budget, which leaves the summation order
+// unchanged). The launch that carries the last pass B also has the stage's history workgroup.
+struct VfoWork {
+    FirArgs a;       // stage 1 (vfo_stage1_prepare)
+    int frame0;      // global frame index of this launch's first pass-A frame
+    int hist;        // this launch's last workgroup writes the stage's next-call history
+};
+constexpr int kVfoRowBatch = 32;   // rows per load batch of the stage-1 segments in these launches
+
+__device__ __forceinline__ void vfo_frame_block(const VfoWork& v, int g) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;   // 8 waves x 2 groups = 16 segments
+    const long long seg = ((long long)(v.frame0 + g) * 8 + wave) * 2 + (lane >> 5);
+    fir_rows_segment<32, 5, true, false, 128, kVfoRowBatch, true>(v.a, seg, lane);
+}
+
+template <bool ZM, int CP>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fft_vfo_kernel(
+    int nB, const float2* __restrict__ scratchB, int framesB, float* __restrict__ outB, float* __restrict__ zoomB,
+    const float2* __restrict__ in, long long frameStride, int framesA, const float* __restrict__ win, int nz,
+    int logN, const float2* __restrict__ tw1, const float2* __restrict__ tw2, const float2* __restrict__ tfull,
+    float2* __restrict__ scratchA, VfoWork v) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    if (v.hist && blockIdx.x == gridDim.x - 1) {   // the stage's history carry (fir.h:80)
+        (void)fir_hist_block<float2, true, false>(v.a);
+        return;
+    }
+    if ((int)blockIdx.x < nB) {
+        passB_tile<256, 32, ZM>(lds, blockIdx.x, scratchB, framesB, 256, logN, tw2, outB, zoomB);
+        return;
+    }
+    const int i = blockIdx.x - nB, g = i / 9, r = i % 9;   // frame g: 8 column tiles, then its VFO block
+    if (r == 8) vfo_frame_block(v, g);
+    else passA_tile<256, 32, CP>(lds, g * 8 + r, in, frameStride, framesA, win, nz, 256, logN, tw1, tfull, scratchA);
+}
+
 // ---------------------------------------------------------------- host side
 struct FftPlan {
     int device = 0, N = 0, logN = 0, nz = 0;
@@ -852,7 +897,21 @@ struct FftPlan {
     hipEvent_t evFork = nullptr, evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr};
     DevBuf scratch2;
     Fft64Plan* f64 = nullptr;         // sdrgpu_fft_set_precision(h, 1): the fp64-interior kernels (fft64.hip)
+    // sdrgpu_fft_set_timing: HIP events around each call's spectrum launch group (the fused VFO
+    // stage included, the VFO's later stages not), a ring of kTimed calls read by sdrgpu_fft_group_times
+    static constexpr int kTimed = 256;
+    bool timing = false;
+    hipEvent_t tev[kTimed][2] = {};
+    long long tcalls = 0;
+    int vfoCP = 0;                    // fused VFO launches: pass-A input cache policy (SDRGPU_FFT_VFO_CP, tuning)
+    int vfoFuse = 1;                  // SDRGPU_FFT_VFO_FUSE=0 (tuning): spectrum and VFO as separate launch groups
 };
+static int time_mark(FftPlan& p, int which, hipStream_t s) {
+    if (!p.timing) return SDRGPU_OK;
+    SDRGPU_HIP(hipEventRecord(p.tev[p.tcalls % FftPlan::kTimed][which], s));
+    if (which == 1) p.tcalls++;
+    return SDRGPU_OK;
+}
 
 // t[m] = exp(-2 pi i (m * step) / L) for m < count (fp64 -> float)
 static int make_twiddles(DevBuf& b, int L, int count = -1, int step = 1) {
@@ -1189,6 +1248,8 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         if (const char* e = tuning_env("SDRGPU_FFT_1M_VARB")) p.var1mB = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_1M_SA")) p.sA1m = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_1M_SB")) p.sB1m = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_VFO_CP")) p.vfoCP = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_VFO_FUSE")) p.vfoFuse = atoi(e);
         if (rc >= 0 && p.N1 == 1024 && p.N2 == 1024) {   // fp64 W_N^(256 j), W_N^j for the 1M pass A
             std::vector<double2> t(512);
             for (int j = 0; j < 256; j++) {
@@ -1265,8 +1326,18 @@ static bool zoom_fusable(const FftPlan& p, int zoomSize) {
 }
 
 // frames -> dB rows (and, with zoom != nullptr on a zoom_fusable plan, the full-span zoom rows)
+static int fft_execute_body(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, float* zoom,
+                            hipStream_t s);
 static int fft_execute(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, float* zoom,
                        hipStream_t s) {
+    SDRGPU_CHECK(time_mark(h->p, 0, s));
+    const int rc = fft_execute_body(h, in, frameStride, frames, out, zoom, s);
+    if (rc < 0) return rc;
+    SDRGPU_CHECK(time_mark(h->p, 1, s));
+    return rc;
+}
+static int fft_execute_body(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, float* zoom,
+                            hipStream_t s) {
     FftPlan& p = h->p;
     const float2* x = (const float2*)in;
     if (p.f64) return fft64_execute(p.f64, x, frameStride, frames, p.win.as<float>(), p.nz, out, s);   // (zoom: unfused)
@@ -1399,25 +1470,140 @@ extern "C" int sdrgpu_fft_execute_zoom_dev(sdrgpu_fft* h, const void* in, long l
     return frames;
 }
 
-// Spectrum + one VFO over the same device batch of back-to-back frames (fftRate = fs / N: the
-// IQFrontEnd's reshaper keeps every sample, iq_frontend.h:56-60), the VFO reading the batch in
-// place like every consumer of the front end's splitter (iq_frontend.cpp:15-52): one call, two
-// launch groups on the caller's stream. (Computing the VFO's first stage inside the 64k pass A,
-// so that the batch is read once, was built and measured slower: DESIGN.md §3.)
-extern "C" int sdrgpu_fft_execute_vfo_dev(sdrgpu_fft* h, const void* in, int frames, float* out, sdrgpu_block* vfo,
-                                          void* vfoOut, void* stream) {
-    if (!h || !in || !out || !vfo || !vfoOut || frames < 0) { set_error("fft_execute_vfo: bad argument"); return SDRGPU_EARG; }
-    const long long count = (long long)frames * h->p.N;
-    if (count > 0x7fffffffLL) { set_error("fft_execute_vfo: %lld samples per call (max 2^31 - 1)", count); return SDRGPU_EARG; }
-    // back-to-back frames: the spectrum must cover every sample the VFO consumes, on one device
-    if (h->p.nz != h->p.N) { set_error("fft_execute_vfo: plan nz %d != N %d (frames must be back to back)", h->p.nz, h->p.N); return SDRGPU_EARG; }
-    if (vfo->impl && vfo->impl->device != h->p.device) {
-        set_error("fft_execute_vfo: VFO on device %d, spectrum plan on device %d", vfo->impl->device, h->p.device);
+// The fused launch group (fft_vfo_kernel): A(0)+V(0); [B(c-1) + A(c)+V(c)] for c = 1..; B(last) +
+// the stage's history workgroup. Scratch alternates between two buffers as in fft_execute.
+template <bool ZM, int CP>
+static int launch_vfo(FftPlan& p, const float2* scratchB, int framesB, float* outB, float* zoomB, const float2* in,
+                      int framesA, float2* scratchA, VfoWork v, hipStream_t s) {
+    auto k = fft_vfo_kernel<ZM, CP>;
+    const size_t lds = sizeof(float2) * (32 * Lds<256>::LS + 256 + 256);
+    SDRGPU_CHECK(set_lds(k, lds));
+    const int nB = 8 * framesB;
+    const int g = nB + 9 * framesA + (v.hist ? 1 : 0);
+    hipLaunchKernelGGL(k, dim3(g), dim3(512), lds, s, nB, scratchB, framesB, outB, zoomB, in, (long long)p.N, framesA,
+                       p.win.as<float>(), p.nz, p.logN, p.tw1.as<float2>(), p.tw2.as<float2>(), p.tfull.as<float2>(),
+                       scratchA, v);
+    SDRGPU_HIP(hipGetLastError());
+    return SDRGPU_OK;
+}
+static int dispatch_vfo(FftPlan& p, bool zm, const float2* scratchB, int framesB, float* outB, float* zoomB,
+                        const float2* in, int framesA, float2* scratchA, const VfoWork& v, hipStream_t s) {
+    if (zm) return p.vfoCP == 2 ? launch_vfo<true, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
+                                : launch_vfo<true, 0>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
+    return p.vfoCP == 2 ? launch_vfo<false, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
+                        : launch_vfo<false, 0>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
+}
+static bool vfo_fusable(const FftPlan& p, float* zoom, int zoomSize) {
+    return p.vfoFuse && !p.f64 && p.N1 == 256 && p.N2 == 256 && p.sa == 32 && p.sb == 32 && p.sa2 == 0 && p.nz == p.N &&
+           (zoom == nullptr || zoom_fusable(p, zoomSize));
+}
+static int fft_execute_vfo(FftPlan& p, const float2* x, int frames, float* out, float* zoom, const VfoStage1& st,
+                           hipStream_t s) {
+    const int cf = p.chunkFrames;
+    const int nchunks = (frames + cf - 1) / cf;
+    SDRGPU_CHECK(p.scratch.ensure((size_t)std::min(cf, frames) * p.N * sizeof(float2)));
+    SDRGPU_CHECK(p.scratch2.ensure(p.scratch.bytes));
+    float2* sc[2] = {p.scratch.as<float2>(), p.scratch2.as<float2>()};
+    const long long zw = p.N / 32;
+    auto zoomAt = [&](long long f0) { return zoom ? zoom + f0 * zw : nullptr; };
+    VfoWork v{st.a, 0, 0};
+    SDRGPU_CHECK(time_mark(p, 0, s));
+    SDRGPU_CHECK(dispatch_vfo(p, zoom != nullptr, nullptr, 0, nullptr, nullptr, x, std::min(cf, frames), sc[0], v, s));
+    for (int c = 1; c < nchunks; c++) {
+        const int fB = (c - 1) * cf, fA = c * cf, nfA = std::min(cf, frames - fA);
+        v.frame0 = fA;
+        SDRGPU_CHECK(dispatch_vfo(p, zoom != nullptr, sc[(c - 1) & 1], cf, out + (long long)fB * p.N, zoomAt(fB),
+                                  x + (long long)fA * p.N, nfA, sc[c & 1], v, s));
+    }
+    const int fL = (nchunks - 1) * cf;
+    v.hist = 1;
+    SDRGPU_CHECK(dispatch_vfo(p, zoom != nullptr, sc[(nchunks - 1) & 1], frames - fL, out + (long long)fL * p.N, zoomAt(fL),
+                              nullptr, 0, nullptr, v, s));
+    return time_mark(p, 1, s);
+}
+
+// Spectrum (+ the waterfall's zoom rows) + one RxVFO over the same device batch of back-to-back
+// frames (fftRate = fs / N: the IQFrontEnd's reshaper keeps every sample, iq_frontend.h:56-60), the
+// VFO reading the batch in place like every consumer of the front end's splitter
+// (iq_frontend.cpp:15-52). On the 64k plan with the VFO's D = 32 first stage (the RxVFO's plan_256
+// at 61.44 MS/s) the batch is read from HBM once: the stage runs inside the spectrum launches
+// (fft_vfo_kernel) and only the VFO's later stages run after them. Otherwise: the spectrum launch
+// group, then the VFO. Returns the VFO's output count (vfoOut).
+extern "C" int sdrgpu_fft_execute_zoom_vfo_dev(sdrgpu_fft* h, const void* in, int frames, float* out, float* zoomOut,
+                                               int zoomSize, sdrgpu_block* vfo, void* vfoOut, void* stream) {
+    if (!h || !in || !out || !vfo || !vfoOut || frames < 0 || (zoomOut && (zoomSize <= 0 || zoomSize > h->p.N))) {
+        set_error("fft_execute_vfo: bad argument");
         return SDRGPU_EARG;
     }
-    hipStream_t s = stream ? (hipStream_t)stream : h->p.own;
-    SDRGPU_CHECK(sdrgpu_fft_execute_dev(h, in, h->p.N, frames, out, s));
-    return sdrgpu_block_process_dev(vfo, in, (int)count, vfoOut, s);
+    FftPlan& p = h->p;
+    const long long count = (long long)frames * p.N;
+    if (count > 0x7fffffffLL) { set_error("fft_execute_vfo: %lld samples per call (max 2^31 - 1)", count); return SDRGPU_EARG; }
+    // back-to-back frames: the spectrum must cover every sample the VFO consumes, on one device
+    if (p.nz != p.N) { set_error("fft_execute_vfo: plan nz %d != N %d (frames must be back to back)", p.nz, p.N); return SDRGPU_EARG; }
+    if (vfo->impl && vfo->impl->device != p.device) {
+        set_error("fft_execute_vfo: VFO on device %d, spectrum plan on device %d", vfo->impl->device, p.device);
+        return SDRGPU_EARG;
+    }
+    if (frames == 0) return 0;
+    SDRGPU_SET_DEVICE(p.device);
+    hipStream_t s = stream ? (hipStream_t)stream : p.own;
+    SDRGPU_CHECK(p.order.follow(s));
+    OrderScope od(p.order, s);
+    SDRGPU_CHECK(vfo->impl->order.follow(s));
+    OrderScope ov(vfo->impl->order, s);
+    VfoStage1 st;
+    const int fuse = vfo_fusable(p, zoomOut, zoomSize) ? vfo_stage1_prepare(vfo, in, (int)count, &st) : 0;
+    if (fuse < 0) return fuse;
+    if (fuse) {
+        SDRGPU_CHECK(fft_execute_vfo(p, (const float2*)in, frames, out, zoomOut, st, s));
+        return vfo_stage1_finish(vfo, st, vfoOut, s);
+    }
+    if (zoomOut && !(zoom_fusable(p, zoomSize) && !p.f64)) {
+        SDRGPU_CHECK(fft_execute(h, in, p.N, frames, out, nullptr, s));
+        if (!p.zoom || p.zoomSize != zoomSize) {
+            if (p.zoom) sdrgpu_zoom_destroy(p.zoom);
+            p.zoom = nullptr;
+            SDRGPU_CHECK(sdrgpu_zoom_create(&p.zoom, p.device, 0.0, 1.0, 1.0, p.N, zoomSize));
+            p.zoomSize = zoomSize;
+        }
+        SDRGPU_CHECK(sdrgpu_zoom_execute_dev(p.zoom, out, frames, zoomOut, s));
+    } else {
+        SDRGPU_CHECK(fft_execute(h, in, p.N, frames, out, zoomOut, s));
+    }
+    return block_run_owned(vfo, in, (int)count, vfoOut, s);
+}
+
+extern "C" int sdrgpu_fft_execute_vfo_dev(sdrgpu_fft* h, const void* in, int frames, float* out, sdrgpu_block* vfo,
+                                          void* vfoOut, void* stream) {
+    return sdrgpu_fft_execute_zoom_vfo_dev(h, in, frames, out, nullptr, 0, vfo, vfoOut, stream);
+}
+
+// Timing of the spectrum launch group (HIP events on the call's stream; off by default)
+extern "C" int sdrgpu_fft_set_timing(sdrgpu_fft* h, int on) {
+    if (!h) { set_error("fft_set_timing: null handle"); return SDRGPU_EARG; }
+    FftPlan& p = h->p;
+    SDRGPU_SET_DEVICE(p.device);
+    if (on && !p.tev[0][0])
+        for (auto& e : p.tev) {
+            SDRGPU_HIP(hipEventCreate(&e[0]));
+            SDRGPU_HIP(hipEventCreate(&e[1]));
+        }
+    p.timing = on != 0;
+    p.tcalls = 0;
+    return SDRGPU_OK;
+}
+// the group times (ms) of the last min(n, calls, 256) timed calls, oldest first; waits for them
+extern "C" int sdrgpu_fft_group_times(sdrgpu_fft* h, float* ms, int n) {
+    if (!h || !ms || n < 0) { set_error("fft_group_times: bad argument"); return SDRGPU_EARG; }
+    FftPlan& p = h->p;
+    SDRGPU_SET_DEVICE(p.device);
+    const long long k = std::min<long long>({(long long)n, p.tcalls, (long long)FftPlan::kTimed});
+    for (long long i = 0; i < k; i++) {
+        auto& e = p.tev[(p.tcalls - k + i) % FftPlan::kTimed];
+        SDRGPU_HIP(hipEventSynchronize(e[1]));
+        SDRGPU_HIP(hipEventElapsedTime(&ms[i], e[0], e[1]));
+    }
+    return (int)k;
 }
 
 extern "C" int sdrgpu_fft_logmag(sdrgpu_fft* h, const void* in, float* out) {
@@ -1456,6 +1642,9 @@ extern "C" int sdrgpu_fft_destroy(sdrgpu_fft* h) {
     if (h->p.own) (void)hipStreamDestroy(h->p.own);
     if (h->p.zoom) sdrgpu_zoom_destroy(h->p.zoom);
     if (h->p.f64) fft64_destroy(h->p.f64);
+    for (auto& e : h->p.tev)
+        for (auto& ev : e)
+            if (ev) (void)hipEventDestroy(ev);
     if (h->p.s2) {
         (void)hipStreamSynchronize(h->p.s2);
         (void)hipStreamDestroy(h->p.s2);

@@ -256,6 +256,21 @@ class FFTSpectrum:
         return check(lib.sdrgpu_fft_execute_vfo_dev(self._h, _vp(in_ptr), int(frames), _vp(out_ptr), vfo._h,
                                                     _vp(vfo_out_ptr), _vp(stream or 0)))
 
+    def execute_zoom_vfo_dev(self, in_ptr, frames, out_ptr, zoom_ptr, zoom_size, vfo, vfo_out_ptr, stream=None):
+        """Spectra (+ zoom rows when zoom_ptr) + one RxVFO over `frames` back-to-back frames; the VFO's
+        first stage runs inside the spectrum launches where the plan allows. Returns the VFO's output count."""
+        return check(lib.sdrgpu_fft_execute_zoom_vfo_dev(self._h, _vp(in_ptr), int(frames), _vp(out_ptr), _vp(zoom_ptr or 0),
+                                                         int(zoom_size), vfo._h, _vp(vfo_out_ptr), _vp(stream or 0)))
+
+    def set_timing(self, on=True):
+        check(lib.sdrgpu_fft_set_timing(self._h, int(bool(on))))
+
+    def group_times(self, n=256):
+        """ms of the spectrum launch group of the last n timed calls (waits for them)."""
+        ms = np.zeros(n, dtype=np.float32)
+        k = check(lib.sdrgpu_fft_group_times(self._h, _fptr(ms), int(n)))
+        return ms[:k]
+
     def close(self):
         if self._h:
             lib.sdrgpu_fft_destroy(self._h)

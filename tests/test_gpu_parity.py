@@ -809,12 +809,16 @@ def test_spectrum_f64_zoom_rows(rng):
 
 
 # ------------------------------------------------- spectrum + VFO fused read
-def _fused_vs_separate(frames_list, pre, rng):
-    """sdrgpu_fft_execute_vfo_dev against the same batches through sdrgpu_fft_execute_dev +
-    RxVFO.process_dev, and the VFO stream (ragged plain calls mixed with batch calls: non-zero
-    decimation phase and history at a batch call) against the oracle."""
+def _fused_vs_separate(frames_list, pre, rng, zoom=False):
+    """sdrgpu_fft_execute_vfo_dev / _zoom_vfo_dev (the VFO's first stage inside the spectrum launches)
+    against the same batches through sdrgpu_fft_execute_dev / _zoom_dev + RxVFO.process_dev, and the
+    VFO stream (ragged plain calls mixed with batch calls: non-zero decimation phase and history at a
+    batch call) against the oracle. The fused launches run the same tile and segment code as the
+    separate ones (only the cache policy of pass A's input loads and the stage's row batch differ,
+    neither of which touches an output's arithmetic), so rows, zoom rows and VFO output are
+    bit-identical to the separate launches."""
     import torch
-    N = 65536
+    N, zw = 65536, 2048
     fs, off = 61.44e6, 2.5e6
     fused_vfo, sep_vfo = dsp.RxVFO(fs, 240000, 200000, off), dsp.RxVFO(fs, 240000, 200000, off)
     ovfo = oracle.RxVFO(fs, 240000, 200000, off)
@@ -828,21 +832,23 @@ def _fused_vs_separate(frames_list, pre, rng):
         d_x = torch.from_numpy(x.view(np.float32)).cuda()
         ra = torch.empty(frames * N, device="cuda")
         rb = torch.empty(frames * N, device="cuda")
+        za = torch.empty(frames * zw, device="cuda")
+        zb = torch.empty(frames * zw, device="cuda")
         cap = frames * N // 256 + 64
         va = torch.empty(2 * cap, device="cuda")
         vb = torch.empty(2 * cap, device="cuda")
-        ma = fa.execute_vfo_dev(d_x.data_ptr(), frames, ra.data_ptr(), fused_vfo, va.data_ptr())
-        fb.execute_dev(d_x.data_ptr(), N, frames, rb.data_ptr())
+        if zoom:
+            ma = fa.execute_zoom_vfo_dev(d_x.data_ptr(), frames, ra.data_ptr(), za.data_ptr(), zw, fused_vfo, va.data_ptr())
+            fb.execute_zoom_dev(d_x.data_ptr(), N, frames, rb.data_ptr(), zb.data_ptr(), zw)
+        else:
+            ma = fa.execute_vfo_dev(d_x.data_ptr(), frames, ra.data_ptr(), fused_vfo, va.data_ptr())
+            fb.execute_dev(d_x.data_ptr(), N, frames, rb.data_ptr())
         mb = sep_vfo.process_dev(d_x.data_ptr(), frames * N, vb.data_ptr())
         torch.cuda.synchronize()
         assert ma == mb
-        # the fused pass A is another instantiation of the same transform (FMA contraction may differ
-        # in the last bits): rows agree to 1e-3 dB within 60 dB of each row's peak (0.05 dB on the
-        # deep bins, where a last-bit change of a tiny |X| moves the dB value most), and the first /
-        # last rows meet the parity bar against the fp64 truth
-        d = (ra - rb).abs().view(frames, N)
-        near = rb.view(frames, N) >= rb.view(frames, N).max(dim=1, keepdim=True).values - 60.0
-        assert float(d[near].max()) <= 1e-3 and float(d.max()) <= 0.05, (float(d[near].max()), float(d.max()))
+        assert torch.equal(ra, rb), float((ra - rb).abs().max())
+        if zoom:
+            assert torch.equal(za, zb)
         w = oracle.create_window(6, N)
         rows = ra.cpu().numpy().reshape(frames, N)
         for j in {0, frames - 1}:
@@ -853,14 +859,24 @@ def _fused_vs_separate(frames_list, pre, rng):
         yo.append(ovfo.process(x))
     ya, yb, yo = (np.concatenate(v) for v in (ya, yb, yo))
     assert len(ya) == len(yb) == len(yo)
-    scale = np.abs(yo).max()
-    assert np.abs(ya - yb).max() <= 1e-5 * scale, np.abs(ya - yb).max()
+    np.testing.assert_array_equal(ya.view(np.uint64), yb.view(np.uint64))
     assert_close_c(ya, yo, 5e-5, "fused VFO vs oracle")
 
 
 @pytest.mark.parametrize("frames_list,pre", [([8], 0), ([3, 5], 1000), ([1, 2], 307200), ([257], 77)])
 def test_spectrum_vfo_fused(frames_list, pre, rng):
     _fused_vs_separate(frames_list, pre, rng)
+
+
+@pytest.mark.parametrize("frames_list,pre,chunk_mb", [([8], 0, None), ([9, 4], 1001, 1), ([1, 3], 31, 1), ([3], 0, 2)])
+def test_spectrum_zoom_vfo_fused(frames_list, pre, chunk_mb, rng, monkeypatch):
+    """The C5 launch group (rows + zoom rows + the VFO's first stage in one set of launches): 1 MB
+    chunks (2 frames per chunk: first pass-A launch, merged launches, last pass-B launch with the
+    history workgroup) and single-chunk calls."""
+    if chunk_mb:
+        monkeypatch.setenv("SDRGPU_TUNING", "1")
+        monkeypatch.setenv("SDRGPU_FFT_CHUNK_MB", str(chunk_mb))
+    _fused_vs_separate(frames_list, pre, rng, zoom=True)
 
 
 # ------------------------------------------------- waterfall zoom fused into the spectrum
