@@ -219,7 +219,7 @@ def _run_generic(wl, x, s, timed_call):
     wl.rest(x, s)
 
 
-def cpu_baseline(config, seconds):
+def cpu_baseline(config, seconds, bytes_per_sample=None):
     """The reference CPU path for the config on the host cores, measured by
     oracle/cpu_baseline.py (test infrastructure, run only here): the oracle's C restatement built
     on this host with -O3 -march=native (vectorised VOLK-class dots) and, for the spectrum legs,
@@ -242,6 +242,17 @@ def cpu_baseline(config, seconds):
     # the whole machine, extrapolated linearly from one core over every affinity CPU (SMT siblings
     # counted as cores: an upper bound for the CPU side)
     out["value_all_affinity_cpus_linear"] = round(r["value_1core"] * h["affinity"], 1)
+    # ... and bounded by the host's DRAM: no CPU chain moves fewer bytes per sample than the
+    # algorithmic ones (IQ in, results out), so a whole host delivers at most DRAM peak / bytes per
+    # sample. The lease's own measured memcpy rate is reported beside it.
+    out["host"]["sockets"] = h.get("sockets")
+    out["host"]["dram_peak_GBs"] = h.get("dram_peak_GBs")
+    out["host"]["lease_memcpy_GBs"] = h.get("lease_memcpy_GBs")
+    if bytes_per_sample and h.get("dram_peak_GBs"):
+        dram = h["dram_peak_GBs"] * 1e3 / bytes_per_sample   # MS/s
+        out["value_whole_host_dram_bound"] = round(min(out["value_all_affinity_cpus_linear"], dram), 1)
+        out["whole_host_bound_note"] = (f"min(1-core x {h['affinity']} CPUs, {h['dram_peak_GBs']:.0f} GB/s DRAM peak of "
+                                        f"{h.get('sockets')} sockets / {bytes_per_sample:.2f} B per sample)")
     for k in ("gflops_1core", "fma_peak_frac_1core"):
         if k in r:
             out[k] = r[k]
@@ -307,24 +318,51 @@ WORKLOADS = {"c5": "C5 per-GPU slice: 64k BH7 FFT+log-mag (back-to-back) + 2048-
                     "32x32 f32 MFMA products, 2^28 samples/step"}
 
 
-def run_config(config, a, shard, dev, stream):
+WORKLOAD_CLASSES = {"c5": C5, "c2": C2, "c3": C3, "c4": C4, "c4g": C4G}
+
+
+class CudaRuntime:
+    """The device side of run_config on a GPU: torch.cuda streams / events and libsdrgpu's RCCL
+    gather. tests/test_bench_multirank.py substitutes a CPU runtime (gloo, LazyGlooGather) to run
+    the same control flow at world size 2 on the CPU."""
+    reduce_device = "cuda"
+
+    def rand(self, n, seed):
+        g = torch.Generator(device="cuda")
+        g.manual_seed(seed)
+        return (torch.rand(n, device="cuda", generator=g) * 2 - 1).contiguous()
+
+    def event(self):
+        return torch.cuda.Event(enable_timing=True)
+
+    def handle(self, stream):
+        return stream.cuda_stream
+
+    def synchronize(self):
+        torch.cuda.synchronize()
+
+    def gather_backend(self, shard, dev):
+        return CudaGather(shard, dev)
+
+
+def run_config(config, a, shard, dev, stream, rt=None, workloads=None):
     """Time `a.steps` steps of one config on this rank; returns (B, elapsed_s, kernel_ms, wl)."""
+    rt = rt or CudaRuntime()
     world, rank = shard.world, shard.rank
     B = 1 << a.log2_batch
     if config == "c2":
         B = 256 * 1000000
-    wl = {"c5": C5, "c2": C2, "c3": C3, "c4": C4, "c4g": C4G}[config](B, shard, dev)
+    wl = (workloads or WORKLOAD_CLASSES)[config](B, shard, dev)
     B = wl.B
-    g = torch.Generator(device="cuda")
-    g.manual_seed(shard.seed())
-    x = (torch.rand(2 * B, device="cuda", generator=g) * 2 - 1).contiguous()   # complex_t interleaved
+    x = rt.rand(2 * B, shard.seed())   # complex_t interleaved
     # N > 1: every step's waterfall rows go to rank 0 over RCCL (libsdrgpu's C-ABI gather) on a
     # stream of their own, overlapping the next step; the zoom rows are double-buffered and a step
     # waits only for the gather that last used its buffer (multistream.GatherPipeline; the same
-    # protocol runs on the CPU over gloo in tests/test_multistream_gloo.py)
+    # protocol runs on the CPU over gloo in tests/test_multistream_gloo.py, and this whole function
+    # at world size 2 in tests/test_bench_multirank.py)
     pipe = None
     if world > 1 and hasattr(wl, "zoom"):
-        pipe = GatherPipeline(shard, wl.zoom_count, CudaGather(shard, dev))
+        pipe = GatherPipeline(shard, wl.zoom_count, rt.gather_backend(shard, dev))
         wl.zoom = pipe.bufs
 
     ev = []
@@ -339,7 +377,7 @@ def run_config(config, a, shard, dev, stream):
 
         def timed_call(fn):   # HIP events around the dominant kernel's launches, on their stream
             if timed:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0, e1 = rt.event(), rt.event()
                 e0.record(stream)
             fn()
             if timed:
@@ -347,9 +385,9 @@ def run_config(config, a, shard, dev, stream):
                 evs.append((e0, e1))
         buf = pipe.acquire(stream) if pipe is not None else 0
         if hasattr(wl, "run"):
-            wl.run(x, stream.cuda_stream, timed_call, buf)
+            wl.run(x, rt.handle(stream), timed_call, buf)
         else:
-            _run_generic(wl, x, stream.cuda_stream, timed_call)
+            _run_generic(wl, x, rt.handle(stream), timed_call)
         if timed:
             ev.append(evs)
         if pipe is not None:
@@ -362,24 +400,24 @@ def run_config(config, a, shard, dev, stream):
     for _ in range(a.warmup):
         step(False)
     drain()
-    torch.cuda.synchronize()
+    rt.synchronize()
     shard.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step(True)
     drain()   # the last step's gather is inside the timed region
-    torch.cuda.synchronize()
+    rt.synchronize()
     shard.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(sum(e0.elapsed_time(e1) for e0, e1 in evs) for evs in ev) / max(len(ev), 1)
     if hasattr(wl, "group_ms") and wl.group_ms(a.steps) is not None:
         kern_ms = wl.group_ms(a.steps)
-    elapsed, kern_ms = shard.max_over_ranks([elapsed, kern_ms], device="cuda")
+    elapsed, kern_ms = shard.max_over_ranks([elapsed, kern_ms], device=rt.reduce_device)
     if pipe is not None:
         # the first multi-GPU run proves the gather: rank 0's received rows of the last step carry
         # each sender's own checksum; the gather's own time is reported next to the step time
         ok, det = pipe.verify()
-        gms = shard.max_over_ranks([pipe.gather_ms() or 0.0], device="cuda")[0]
+        gms = shard.max_over_ranks([pipe.gather_ms() or 0.0], device=rt.reduce_device)[0]
         wl.gather_report = {"verified": bool(ok), "ms_per_gather_max_rank": round(gms, 4),
                             "bytes_per_rank_per_step": 4 * wl.zoom_count, **(det or {})}
         pipe.close()
@@ -564,17 +602,24 @@ def main():
         if not a.no_ulp:
             out["spectrum_ulp"] = spectrum_ulp_report(dev)
         if world == 1 and not a.no_cpu:
-            out["cpu_baseline"] = cpu_baseline("c4" if a.config == "c4g" else a.config, a.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline("c4" if a.config == "c4g" else a.config, a.cpu_seconds, head["bytes_per_sample"])
             out["speedup_vs_cpu_all_cores"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
             out["speedup_vs_cpu_all_affinity_linear"] = round(out["value"] / out["cpu_baseline"]["value_all_affinity_cpus_linear"], 2)
+            if out["cpu_baseline"].get("value_whole_host_dram_bound"):
+                out["speedup_vs_whole_host_bound"] = round(out["value"] / out["cpu_baseline"]["value_whole_host_dram_bound"], 2)
+            out["speedup_basis"] = ("speedup_vs_cpu_all_cores (the north_star's >= 10x) is against the CPUs the box grants "
+                                    "this job (cpu_baseline.cores, cgroup quota); speedup_vs_whole_host_bound against a whole "
+                                    "host, every CPU at the 1-core rate but never past its DRAM peak / bytes per sample")
             cpu_cache = {}
             for c, r in subs.items():
                 ck = "c4" if c == "c4g" else c   # both C4 forms against the same CPU channelizer
                 if ck not in cpu_cache:
-                    cpu_cache[ck] = cpu_baseline(ck, a.cpu_seconds)
+                    cpu_cache[ck] = cpu_baseline(ck, a.cpu_seconds, r["bytes_per_sample"])
                 r["cpu_baseline"] = cpu_cache[ck]
                 r["speedup_vs_cpu_all_cores"] = round(r["value"] / r["cpu_baseline"]["value"], 1)
                 r["speedup_vs_cpu_all_affinity_linear"] = round(r["value"] / r["cpu_baseline"]["value_all_affinity_cpus_linear"], 2)
+                if r["cpu_baseline"].get("value_whole_host_dram_bound"):
+                    r["speedup_vs_whole_host_bound"] = round(r["value"] / r["cpu_baseline"]["value_whole_host_dram_bound"], 2)
         if subs:
             out["configs"] = subs
         if world == 1 and a.config == "c5" and not a.no_sub:

@@ -102,6 +102,54 @@ def host_info():
             "core_max_mhz": mhz, "core_fp32_peak_gflops": peak}
 
 
+# DDR channels x MT/s per socket of the host CPUs the GPU boxes carry (vendor specifications): the
+# DRAM ceiling of a whole host is sockets x channels x MT/s x 8 B
+DRAM_PER_SOCKET = {"AMD EPYC 9575F": (12, 6400)}
+
+
+def host_sockets():
+    try:
+        ids = set()
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    ids.add(line.split(":", 1)[1].strip())
+        return max(1, len(ids))
+    except OSError:
+        return None
+
+
+def host_dram_peak_gbs(model, sockets):
+    for k, (ch, mts) in DRAM_PER_SOCKET.items():
+        if model and k in model and sockets:
+            return sockets * ch * mts * 8 / 1000.0
+    return None
+
+
+def _stream_worker(seconds):
+    """memcpy bandwidth of one process over 256 MB buffers (read + write bytes), GB/s"""
+    import numpy as np
+    a = np.ones(64 << 20, dtype=np.float32)
+    b = np.empty_like(a)
+    np.copyto(b, a)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        np.copyto(b, a)
+        n += 1
+    return 2 * a.nbytes * n / (time.perf_counter() - t0) / 1e9
+
+
+def stream_bw(ncores, cores, seconds=2.0):
+    """Aggregate memcpy bandwidth of `ncores` concurrent single-threaded processes (one per core of
+    the lease): what the lease's CPUs move to and from DRAM."""
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--stream", str(seconds), "--cpu", str(cores[k])],
+                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True) for k in range(ncores)]
+    tot = 0.0
+    for p in procs:
+        tot += float(p.communicate()[0].strip().splitlines()[-1])
+    return tot
+
+
 def _iq(rng, n):
     import numpy as np
     return (rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)).astype(np.complex64)
@@ -206,6 +254,9 @@ FLOP_PER_SAMPLE = {
 }
 
 
+_BW = None   # the lease's memcpy bandwidth, measured once per process
+
+
 def measure(config, seconds=8.0, max_cores=None):
     """1-core figure of every variant (in turn), then the fastest variant on all cores this process
     may use: the cgroup CPU quota (16 on the GPU box), capped by the affinity mask."""
@@ -228,6 +279,12 @@ def measure(config, seconds=8.0, max_cores=None):
     for p in procs:
         r = json.loads(p.communicate()[0].strip().splitlines()[-1])[best]
         rates.append(r["samples"] / r["seconds"] / 1e6)
+    global _BW
+    if _BW is None:
+        _BW = stream_bw(ncores, cores_avail)
+    info["sockets"] = host_sockets()
+    info["dram_peak_GBs"] = host_dram_peak_gbs(info["model"], info["sockets"])
+    info["lease_memcpy_GBs"] = round(_BW, 1)
     r = {"value_1core": one[best], "variant": best, "variants_1core": one, "value_all_cores": sum(rates),
          "cores_all": ncores, "cores_source": "cgroup cpu.max quota" if quota is not None else "affinity mask",
          "per_stream_min": min(rates), "host": info,
@@ -248,13 +305,19 @@ def workloads_names(config):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", required=True)
+    ap.add_argument("--config", default=None)
     ap.add_argument("--seconds", type=float, default=8.0)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--variant", default=None)
     ap.add_argument("--cpu", type=int, default=None)
     ap.add_argument("--measure", action="store_true", help="run the 1-core + all-core measurement")
+    ap.add_argument("--stream", type=float, default=None, help="memcpy bandwidth worker (seconds)")
     a = ap.parse_args()
+    if a.stream is not None:
+        if a.cpu is not None and hasattr(os, "sched_setaffinity"):
+            os.sched_setaffinity(0, {a.cpu})
+        print(_stream_worker(a.stream))
+        sys.exit(0)
     if a.measure:
         print(json.dumps(measure(a.config, a.seconds)))
         sys.exit(0)
