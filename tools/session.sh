@@ -14,7 +14,9 @@
 #   pct     per-call kernel trace (tools/per_call.py)
 #   ab      interleaved A/B of AB_VAR over AB_VALUES (env knob, SDRGPU_TUNING=1), AB_RUNS rounds,
 #           config AB_CFG                                              -> TAG_ab_<value>_<k>.json
-#   sq      SQ counter sets for SQ_CFG (tools/pmc_sets.sh)
+#   ablib   interleaved A/B of the in-tree build against sdrpp_amd/lib_<v> builds (AB_LIBS; built with
+#           python sdrpp_amd/build.py --variant <v> DEFINE ...)
+#   sq      SQ counter sets for SQ_CFG / SQ_RX (tools/pmc_sets.sh)
 # Every GPU step runs under its own timeout; the session stops at the first failure.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R" || exit 1
 OUT=$R/gpurun_out; TAG=${1:-s}; shift; mkdir -p "$OUT"
@@ -79,6 +81,16 @@ for step in $STEPS_LIST; do
         env SDRGPU_TUNING=1 $AB_VAR=$v timeout -k 10 300 python bench.py --config ${AB_CFG:-c5} --no-sub --no-cpu --no-ulp \
           --steps ${AB_STEPS:-20} --warmup 3 > "$OUT/${TAG}_ab_${v}_$k.json" 2> "$OUT/${TAG}_ab_${v}_$k.err"
         st ab_${v}_$k $?
+      done
+    done
+    python tools/ab_summary.py "$OUT" "$TAG" > "$OUT/${TAG}_ab_summary.txt" 2>&1 ;;
+  ablib)    # interleaved A/B of library builds: the in-tree one vs sdrpp_amd/lib_<v> for v in AB_LIBS
+    for k in $(seq 1 ${AB_RUNS:-3}); do
+      for v in tree $AB_LIBS; do
+        L=$R/sdrpp_amd/lib/libsdrgpu.so; [ "$v" = tree ] || L=$R/sdrpp_amd/lib_$v/libsdrgpu.so
+        SDRGPU_LIB_PATH=$L timeout -k 10 300 python bench.py --config ${AB_CFG:-c5} --no-sub --no-cpu --no-ulp \
+          --steps ${AB_STEPS:-20} --warmup 3 > "$OUT/${TAG}_ab_${v}_$k.json" 2> "$OUT/${TAG}_ab_${v}_$k.err"
+        st ablib_${v}_$k $?
       done
     done
     python tools/ab_summary.py "$OUT" "$TAG" > "$OUT/${TAG}_ab_summary.txt" 2>&1 ;;
