@@ -1408,7 +1408,9 @@ struct ChainBlock : Block {
     static constexpr int kTailMaxIn = 1 << 15;   // first kid's outputs (a reference block: 9,600)
     int tailMode = -1;                           // SDRGPU_VFO_TAIL (tuning): 0 off
     int tailVar = 0;                             // SDRGPU_TAIL_VAR (tuning, timing only): 1 no stage loops, 2 no image loads
-    int run_tail(const void* in, int count, void* out, hipStream_t s, int* nout) {
+    // The tail launch's arguments for kids[1..] on n0 samples of kid 0's output: 1 (t, f, lds
+    // filled), 0 (not applicable: the per-kid path runs).
+    int tail_plan(int n0, TailArgs& t, FirBlock** f, size_t& lds) {
         if (tailMode < 0) {
             const char* e = tuning_env("SDRGPU_VFO_TAIL");
             tailMode = e ? atoi(e) : 1;
@@ -1416,9 +1418,7 @@ struct ChainBlock : Block {
         }
         const int S = (int)kids.size() - 1;
         if (!tailMode || S < 2 || S > TAIL_MAXS) return 0;
-        const int n0 = kids[0]->out_count(count);
         if (n0 > kTailMaxIn) return 0;
-        FirBlock* f[TAIL_MAXS];
         for (int i = 0; i < S; i++) {
             f[i] = dynamic_cast<FirBlock*>(kids[i + 1].get());
             if (!f[i] || f[i]->in_dtype != SDRGPU_C64 || f[i]->ttype != SDRGPU_F32 || f[i]->xl || f[i]->quad ||
@@ -1426,7 +1426,7 @@ struct ChainBlock : Block {
                 f[i]->D > TAIL_NT / TAIL_K)
                 return 0;
         }
-        TailArgs t{};
+        t = TailArgs{};
         t.S = S;
         int n = n0;
         for (int i = 0; i < S; i++) {
@@ -1466,23 +1466,49 @@ struct ChainBlock : Block {
         }
         t.tapTotal = tapF;
         if (tapF > 2 * TAIL_NT) return 0;                 // two tap loads per thread
-        const size_t lds = sizeof(float2) * (size_t)maxEl + sizeof(float) * (size_t)tapF;
+        lds = sizeof(float2) * (size_t)maxEl + sizeof(float) * (size_t)tapF;
         if (lds > 64 * 1024) return 0;
+        t.var = tailVar;
+        return 1;
+    }
+    // the tail launch over kid 0's output s1 (n0 samples) into out, and the kids' state update
+    int launch_tail(TailArgs& t, FirBlock** f, size_t lds, const void* s1, void* out, hipStream_t s) {
+        t.in = reinterpret_cast<const float2*>(s1);
+        t.out = reinterpret_cast<float2*>(out);
+        hipLaunchKernelGGL(fir_tail_kernel, dim3(t.G), dim3(TAIL_NT), lds, s, t);
+        SDRGPU_HIP(hipGetLastError());
+        for (int i = 0; i < t.S; i++) {   // FirBlock::run's state update
+            f[i]->cur ^= 1;
+            f[i]->offset = f[i]->offset + t.st[i].M * f[i]->D - t.st[i].n;
+        }
+        return t.st[t.S - 1].M;
+    }
+    int run_tail(const void* in, int count, void* out, hipStream_t s, int* nout) {
+        TailArgs t;
+        FirBlock* f[TAIL_MAXS];
+        size_t lds = 0;
+        const int n0 = kids.empty() ? 0 : kids[0]->out_count(count);
+        const int ok = tail_plan(n0, t, f, lds);
+        if (ok <= 0) return ok;
         SDRGPU_CHECK(scratch[0].ensure(sizeof(float2) * (size_t)std::max(n0, 1)));
         const int m0 = kids[0]->run(in, count, scratch[0].p, s);
         if (m0 < 0) return m0;
         if (m0 != n0) { set_error("chain: first stage produced %d samples, expected %d", m0, n0); return SDRGPU_ESTATE; }
-        t.in = scratch[0].as<float2>();
-        t.out = reinterpret_cast<float2*>(out);
-        t.var = tailVar;
-        hipLaunchKernelGGL(fir_tail_kernel, dim3(t.G), dim3(TAIL_NT), lds, s, t);
-        SDRGPU_HIP(hipGetLastError());
-        for (int i = 0; i < S; i++) {   // FirBlock::run's state update
-            f[i]->cur ^= 1;
-            f[i]->offset = f[i]->offset + t.st[i].M * f[i]->D - t.st[i].n;
-        }
+        const int n = launch_tail(t, f, lds, scratch[0].p, out, s);
+        if (n < 0) return n;
         *nout = n;
         return 1;
+    }
+    // kids[1..] on kid 0's output that another launch produced (vfo_stage1_finish): the tail launch
+    // where it applies, else kid by kid
+    int run_rest(const void* s1, int n0, void* out, hipStream_t s) {
+        TailArgs t;
+        FirBlock* f[TAIL_MAXS];
+        size_t lds = 0;
+        const int ok = tail_plan(n0, t, f, lds);
+        if (ok < 0) return ok;
+        if (ok) return launch_tail(t, f, lds, s1, out, s);
+        return run_from(1, s1, n0, out, s);
     }
 };
 
@@ -1664,7 +1690,7 @@ int vfo_stage1_finish(sdrgpu_block* vfo, const VfoStage1& st, void* out, hipStre
     auto* c = dynamic_cast<ChainBlock*>(vfo->impl);
     auto* f = dynamic_cast<FirBlock*>(c->kids[0].get());
     f->rows_commit(st.count, st.M);
-    return c->run_from(1, st.out, st.M, out, s);
+    return c->run_rest(st.out, st.M, out, s);
 }
 
 }  // namespace sdrgpu

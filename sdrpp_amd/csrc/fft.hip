@@ -856,6 +856,41 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     else passA_tile<256, 32, CP>(lds, g * 8 + r, in, frameStride, framesA, win, nz, 256, logN, tw1, tfull, scratchA);
 }
 
+// ---- the front end's per-block launch: pass A (frame straddling two pushes read in place) + the
+// VFO's first stage + its history carry + the tail copy, one launch (sdrgpu_frontend_*): the block is
+// small (a reference-size block has ~5 frames and 9,600 stage-1 outputs), so the stage's segments
+// are the small-call ones (32 outputs, one row batch each: 300 segments, 19 workgroups of 16).
+struct VfoCall {
+    FirArgs a;
+    int blocks;      // stage-1 workgroups (16 segments each)
+};
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fft_passA_vfo_kernel(
+    const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
+    int logN, const float2* __restrict__ tw, const float2* __restrict__ tfull, float2* __restrict__ scratch,
+    const float2* __restrict__ headp, int nh, SideCopy side, VfoCall v) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int ntiles = (N2 / 32) * frames;
+    int b = blockIdx.x;
+    if (b < ntiles) {
+        passA_tile<256, 32>(lds, b, in, frameStride, frames, win, nz, N2, logN, tw, tfull, scratch, headp, nh);
+        return;
+    }
+    b -= ntiles;
+    if (b < v.blocks) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        fir_rows_segment<32, 5, true, false, 32, 32, true>(v.a, ((long long)b * 8 + wave) * 2 + (lane >> 5), lane);
+        return;
+    }
+    b -= v.blocks;
+    if (b == 0) {   // the stage's history carry (fir.h:80)
+        fir_hist_copy<float2, true, false>(v.a);
+        return;
+    }
+    const int w = b - 1, nw = gridDim.x - ntiles - v.blocks - 1;   // spare workgroups: the side copies
+    for (int k = 0; k < side.count; k++)
+        for (int i = w * blockDim.x + threadIdx.x; i < side.n[k]; i += nw * blockDim.x) side.dst[k][i] = side.src[k][i];
+}
+
 // ---------------------------------------------------------------- host side
 struct FftPlan {
     int device = 0, N = 0, logN = 0, nz = 0;
@@ -1423,7 +1458,7 @@ extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long f
 }
 
 int sdrgpu::fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const float2* body, long long stride, int frames,
-                              float* out, const SideCopy& side, hipStream_t s) {
+                              float* out, const SideCopy& side, hipStream_t s, const VfoStage1* vfo) {
     if (!h || !body || frames <= 0 || nh < 0 || (nh > 0 && !head)) return SDRGPU_ESTATE;
     FftPlan& p = h->p;
     // the 64k plan's default tiles (256 x 256, 32 columns / 32 rows, one-column pass A); one chunk
@@ -1431,8 +1466,27 @@ int sdrgpu::fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const f
         return SDRGPU_ESTATE;
     SDRGPU_CHECK(p.scratch.ensure((size_t)frames * p.N * sizeof(float2)));
     p.cur = p.scratch.as<float2>();
-    SDRGPU_CHECK((launch_passA<256, 32>(p, body, stride, frames, s, head, nh, &side)));
+    SDRGPU_CHECK(time_mark(p, 0, s));
+    if (vfo) {
+        VfoCall v{vfo->a, (int)((((long long)vfo->M + 31) / 32 + 15) / 16)};
+        auto k = fft_passA_vfo_kernel;
+        const size_t lds = sizeof(float2) * (32 * Lds<256>::LS + 256 + 256);
+        SDRGPU_CHECK(set_lds(k, lds));
+        int spare = 0;
+        if (side.count > 0) {
+            int mx = 0;
+            for (int i = 0; i < side.count; i++) mx = std::max(mx, side.n[i]);
+            spare = std::max(1, std::min(64, (mx + 512 * 4 - 1) / (512 * 4)));   // ~4 elements per thread
+        }
+        const int g = 8 * frames + v.blocks + 1 + spare;
+        hipLaunchKernelGGL(k, dim3(g), dim3(512), lds, s, body, stride, frames, p.win.as<float>(), p.nz, p.N2, p.logN,
+                           p.tw1.as<float2>(), p.tfull.as<float2>(), p.cur, head, nh, side, v);
+        SDRGPU_HIP(hipGetLastError());
+    } else {
+        SDRGPU_CHECK((launch_passA<256, 32>(p, body, stride, frames, s, head, nh, &side)));
+    }
     SDRGPU_CHECK(dispatch_passB(p, frames, out, s));
+    SDRGPU_CHECK(time_mark(p, 1, s));
     return frames;
 }
 

@@ -135,8 +135,7 @@ __device__ __forceinline__ DT fir_fetch(const FirArgs& a, long long b) {
 // launch's extra workgroup, so a call needs no separate history kernel: next[k] = [hist | in]
 // [count + k], k < H (the xlator applied to `in` samples, as fir_fetch does).
 template <typename DT, bool XL, bool TAB = true>
-__device__ __forceinline__ bool fir_hist_block(const FirArgs& a) {
-    if (a.histNext == nullptr || blockIdx.x != gridDim.x - 1) return false;
+__device__ __forceinline__ void fir_hist_copy(const FirArgs& a) {
     const DT* hist = reinterpret_cast<const DT*>(a.hist);
     const DT* in = reinterpret_cast<const DT*>(a.in);
     DT* next = reinterpret_cast<DT*>(a.histNext);
@@ -151,6 +150,11 @@ __device__ __forceinline__ bool fir_hist_block(const FirArgs& a) {
         }
         next[k] = v;
     }
+}
+template <typename DT, bool XL, bool TAB = true>
+__device__ __forceinline__ bool fir_hist_block(const FirArgs& a) {
+    if (a.histNext == nullptr || blockIdx.x != gridDim.x - 1) return false;
+    fir_hist_copy<DT, XL, TAB>(a);
     return true;
 }
 

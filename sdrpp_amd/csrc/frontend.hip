@@ -21,6 +21,7 @@
 #include <map>
 #include <vector>
 #include "sdrgpu_internal.h"
+#include "fir_rows.h"
 
 namespace sdrgpu {
 __global__ void conjugate_kernel(float2* __restrict__ x, int n) {   // math/conjugate.h
@@ -82,6 +83,8 @@ struct sdrgpu_frontend {
     PipeSlot pipe[2];
     long long nextTicket = 0;
     int split = 1;   // fft_execute_split for pushes that complete frames (SDRGPU_FE_SPLIT=0, tuning: stitch copies)
+    // the first VFO's first stage inside that pass-A launch (SDRGPU_FE_FUSE=0, tuning: its own launch)
+    int fuse = 1;
 };
 
 static void destroy_parts(sdrgpu_frontend* f) {
@@ -133,6 +136,7 @@ extern "C" int sdrgpu_frontend_create(sdrgpu_frontend** out, int device, double 
     f->fftRate = fftRate;
     f->window = windowType;
     if (const char* e = tuning_env("SDRGPU_FE_SPLIT")) f->split = atoi(e);
+    if (const char* e = tuning_env("SDRGPU_FE_FUSE")) f->fuse = atoi(e);
     int rc = hipStreamCreateWithFlags(&f->s, hipStreamNonBlocking) == hipSuccess ? SDRGPU_OK : SDRGPU_EHIP;
     if (rc < 0) set_error("frontend_create: hipStreamCreate failed");
     if (rc >= 0) rc = fe_build_preproc(f);
@@ -264,18 +268,39 @@ struct CopySegs {
 
 // Core of a push: the preprocessed block `x` (m samples, device) -> VFOs + spectrum frames.
 static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s) {
-    for (auto& [id, v] : f->vfos) {
-        const int want = sdrgpu_block_out_count(v.vfo, m);
-        if (want < 0) return want;
-        SDRGPU_CHECK(v.out.ensure(sizeof(float2) * (size_t)std::max(want, 1)));
-        const int n = m > 0 ? block_run_owned(v.vfo, x, m, v.out.p, s) : 0;
-        if (n < 0) return n;
-        v.n = n;
-    }
     // frames with start s_j = nextFrame + j*stride and s_j + nz <= total + m
     const long long T = f->total, st = f->stride();
     int nf = 0;
     if (T + m >= f->nextFrame + f->nz) nf = (int)((T + m - f->nextFrame - f->nz) / st) + 1;
+    // The first VFO whose first stage is the row decimator runs that stage inside the spectrum's
+    // pass-A launch below (one launch fewer per block, DESIGN.md §3 per call); the others, and that
+    // one when the spectrum has no such launch, run on their own.
+    VfoStage1 vst;
+    VfoSlot* fused = nullptr;
+    for (auto& [id, v] : f->vfos) {
+        const int want = sdrgpu_block_out_count(v.vfo, m);
+        if (want < 0) return want;
+        SDRGPU_CHECK(v.out.ensure(sizeof(float2) * (size_t)std::max(want, 1)));
+        if (!fused && f->fuse && f->split && nf > 0 && m > 0) {
+            const int r = vfo_stage1_prepare(v.vfo, x, m, &vst);
+            if (r < 0) return r;
+            if (r) {
+                fused = &v;
+                continue;
+            }
+        }
+        const int n = m > 0 ? block_run_owned(v.vfo, x, m, v.out.p, s) : 0;
+        if (n < 0) return n;
+        v.n = n;
+    }
+    auto finish_fused = [&](bool launched) -> int {
+        if (!fused) return SDRGPU_OK;
+        const int n = launched ? vfo_stage1_finish(fused->vfo, vst, fused->out.p, s)
+                               : block_run_owned(fused->vfo, x, m, fused->out.p, s);
+        if (n < 0) return n;
+        fused->n = n;
+        return SDRGPU_OK;
+    };
     SDRGPU_CHECK(f->spectra.ensure(sizeof(float) * (size_t)std::max(nf, 1) * f->fftSize));
     float* spec = f->spectra.as<float>();
     if (nf > 0 && f->split) {
@@ -299,8 +324,9 @@ static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s)
             side.count = 1;
         }
         const int rc = fft_execute_split(f->fft, head > 0 ? f->tail[f->curTail].as<float2>() : nullptr, head, body, st, nf,
-                                         spec, side, s);
+                                         spec, side, s, fused ? &vst : nullptr);
         if (rc >= 0) {
+            SDRGPU_CHECK(finish_fused(true));
             f->nSpec = nf;
             f->nextFrame = nextAfterS;
             f->curTail = nbS;
@@ -310,6 +336,7 @@ static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s)
         }
         if (rc != SDRGPU_ESTATE) return rc;   // (ESTATE: this plan has no split path; stitch below)
     }
+    SDRGPU_CHECK(finish_fused(false));   // (no split launch: the prepared VFO runs on its own)
     int done = 0;
     // the stitched straddling frame and the new tail are built by one copy launch (up to four
     // device segments) before the spectrum: both read only the old tail and this block
