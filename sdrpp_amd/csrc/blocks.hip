@@ -11,6 +11,7 @@
 #include <type_traits>
 #include "sdrgpu_internal.h"
 #include "fir_rows.h"
+#include "fir_tail.h"
 
 namespace sdrgpu {
 
@@ -537,207 +538,10 @@ __global__ __launch_bounds__(WFM_TM) void wfm_short_kernel(
     out[m] = make_float2(acc, acc);
 }
 
-// ------------------------------------------------ FIR cascade tail (short calls)
-// The FIR stages behind a chain's first stage -- the RxVFO's decimator stages 2.. and its channel
-// low-pass: 9,600 -> 2,400 -> 1,200 -> 1,200 samples for a reference block -- in ONE launch
-// instead of one 4.5-6 us launch each. Workgroup w owns outputs [w M / G, (w + 1) M / G) of the
-// last stage and computes, stage by stage in LDS, exactly the outputs of the earlier stages its
-// window needs (halos recomputed, so workgroups never exchange data). Each output is fir_kernel's
-// fmaf chain -- phase p outer, padded tap q inner, the block's own [p][Q] tap table, the same
-// register window -- so a stage's outputs are bit-identical to fir_kernel's. The last workgroup
-// also writes every stage's next-call history (fir.h:80). Stage images use fir_kernel's
-// phase-major, row-swizzled LDS layout (conflict-free window reads). The kernel runs once per
-// call on a few CUs, so it is written for latency: one global round trip for all image loads,
-// power-of-two decimations (shifts, not divisions), stage loops kept rolled (small code).
-constexpr int TAIL_MAXS = 4;    // stages
-// consecutive outputs per thread (register window). Each thread's chain of D * Q FMAs per output is
-// the kernel's critical path (one or two waves per stage are busy), so fewer outputs per thread
-// (more waves) measured faster: per-call trace 12.0 / 10.3 / 10.0 / 15.5 us at K = 4 / 2 / 1 / 8;
-// prefetching the next tap chunk's LDS reads measured slower (13.8 us at K = 4, 12.0 at K = 2)
-constexpr int TAIL_K = 2;
-constexpr int TAIL_NT = 256;    // threads per workgroup
-constexpr int TAIL_PF = 16;     // image loads per thread issued together
-struct TailStage {
-    const float2* hist;   // H samples (newest last)
-    float2* histNext;     // next call's history: [hist || in][n + k], k < H
-    const float* taps;    // [D][Q] phase-major, zero past ntaps = H + 1
-    int H, n, D, dsh, Q, off, M;   // dsh = log2 D
-};
-struct TailArgs {
-    const float2* in;     // stage 0's input (n of stage 0 samples)
-    float2* out;          // last stage's output
-    int S, G;
-    int ldsEl;            // float2 elements of the largest workgroup's images (the taps follow)
-    int tapTotal;         // floats of all stages' tap tables
-    int var;              // timing variants (SDRGPU_TAIL_VAR, wrong results): 1 no stage loops, 2 no image loads
-    int tapOff[TAIL_MAXS];   // float offset of stage s's [D][Q] taps behind the images
-    TailStage st[TAIL_MAXS];
-};
-// Per workgroup and stage: outputs [a, b), image of [hist || in] elements [B, E) (B = off + a D,
-// so an image row is one output step), swizzle strides, LDS base. Returns the LDS elements.
-struct TailGeom { int a, b, B, E, RSK, RSP, base, nel; };
-__host__ __device__ inline int tail_geometry(const TailArgs& t, int w, TailGeom* g) {
-    const bool last = w == t.G - 1;
-    const int Ml = t.st[t.S - 1].M;
-    int lo = Ml * w / t.G, hi = Ml * (w + 1) / t.G;   // Ml * G < 2^31 (host limits)
-#pragma unroll
-    for (int s = TAIL_MAXS - 1; s >= 0; s--) {   // (static indices: g stays in registers)
-        if (s >= t.S) continue;
-        const TailStage& st = t.st[s];
-        TailGeom& q = g[s];
-        const int len = st.H + st.n;
-        q.a = lo;
-        q.b = hi;
-        if (lo < hi) {
-            q.B = st.off + lo * st.D;
-            q.E = st.off + (hi - 1) * st.D + st.H + 1;   // the last output's window end (<= len)
-        } else {
-            q.B = q.E = len;
-        }
-        if (last) {   // + the next call's history [n, len): off + (M - 1) D < n, so B stays aligned
-            q.B = q.B < st.n ? q.B : st.n;
-            q.E = len;
-        }
-        const int nthr = (hi - lo + TAIL_K - 1) / TAIL_K;
-        int rows = nthr * TAIL_K + st.Q + 2 * TAIL_K;
-        const int need = (q.E - q.B + st.D - 1) / st.D + 1;
-        rows = rows > need ? rows : need;
-        q.RSK = (rows + TAIL_K - 1) / TAIL_K;
-        q.RSP = TAIL_K * q.RSK + 1;
-        q.nel = st.D * q.RSK * TAIL_K;
-        // the previous stage's outputs this image holds: in[] indices of [B, E)
-        lo = q.B - st.H > 0 ? q.B - st.H : 0;
-        hi = q.E - st.H < st.n ? q.E - st.H : st.n;
-        if (lo >= hi) lo = hi = 0;
-    }
-    int base = 0;
-#pragma unroll
-    for (int s = 0; s < TAIL_MAXS; s++) {
-        if (s >= t.S) break;
-        g[s].base = base;
-        base += t.st[s].D * g[s].RSP;
-    }
-    return base;
-}
 __global__ __launch_bounds__(TAIL_NT) void fir_tail_kernel(TailArgs t) {
     extern __shared__ __attribute__((aligned(16))) float2 XS[];
     __shared__ TailGeom gs[TAIL_MAXS];
-    const int tid = threadIdx.x;
-    const bool last = blockIdx.x == gridDim.x - 1;
-    // every global load of the launch is issued in one batch (one memory round trip; a dependent
-    // round trip to HBM costs ~1-2 us, which is what this kernel is built to avoid): the stages'
-    // tap tables, the histories of stages >= 1 (H <= TAIL_NT, host-checked) and stage 0's image
-    // (<= TAIL_PF * TAIL_NT elements, host-checked). The geometry is wave-uniform (scalar).
-    TailGeom g[TAIL_MAXS];
-    tail_geometry(t, blockIdx.x, g);
-    constexpr int TAIL_TP = 2;   // tap loads per thread: <= 512 taps in all (host-checked)
-    float tap[TAIL_TP];
-#pragma unroll
-    for (int u = 0; u < TAIL_TP; u++) {
-        tap[u] = 0.f;
-        const int j = tid + u * TAIL_NT;
-#pragma unroll
-        for (int s = 0; s < TAIL_MAXS; s++) {
-            if (s >= t.S) break;
-            const int i = j - t.tapOff[s];
-            if (i >= 0 && i < t.st[s].D * t.st[s].Q) tap[u] = t.st[s].taps[i];
-        }
-    }
-    float2 hv[TAIL_MAXS];
-#pragma unroll
-    for (int s = 1; s < TAIL_MAXS; s++) {
-        if (s >= t.S) break;
-        const int e = g[s].B + tid;
-        hv[s] = (e < t.st[s].H && e < g[s].E) ? t.st[s].hist[e] : make_float2(0.f, 0.f);
-    }
-    const TailStage& s0 = t.st[0];
-    float2 v[TAIL_PF];
-#pragma unroll
-    for (int u = 0; u < TAIL_PF; u++) {
-        const int e = g[0].B + tid + u * TAIL_NT;
-        const float2* src = (e < g[0].E && t.var != 2) ? (e < s0.H ? s0.hist + e : t.in + (e - s0.H)) : nullptr;
-        v[u] = src ? *src : make_float2(0.f, 0.f);
-    }
-    // image element sx (from B) of stage s -> LDS index (fir_kernel's layout)
-    auto slot = [&](const TailGeom& q, int dsh, int sx) {
-        const int r = sx >> dsh;
-        return q.base + (sx & ((1 << dsh) - 1)) * q.RSP + (r & (TAIL_K - 1)) * q.RSK + r / TAIL_K;
-    };
-    float* TS = reinterpret_cast<float*>(XS + t.ldsEl);
-#pragma unroll
-    for (int u = 0; u < TAIL_TP; u++)
-        if (tid + u * TAIL_NT < t.tapTotal) TS[tid + u * TAIL_NT] = tap[u];
-#pragma unroll
-    for (int s = 0; s < TAIL_MAXS; s++)
-        if (tid == s && s < t.S) gs[s] = g[s];
-    {   // stage 0: D | TAIL_NT, so a thread's slots advance by a constant (fixed phase and lane)
-        int idx = slot(g[0], s0.dsh, tid);
-        const int inc = (TAIL_NT >> s0.dsh) / TAIL_K;
-#pragma unroll
-        for (int u = 0; u < TAIL_PF; u++) {
-            if (tid + u * TAIL_NT < g[0].nel) XS[idx] = v[u];
-            idx += inc;
-        }
-    }
-    // stages >= 1: history part [B, min(H, E)) and zeros past E; [max(B, H), E) is written by the
-    // stage before
-#pragma unroll
-    for (int s = 1; s < TAIL_MAXS; s++) {
-        if (s >= t.S) break;
-        const int H = t.st[s].H;
-        if (g[s].B + tid < H && g[s].B + tid < g[s].E) XS[slot(g[s], t.st[s].dsh, tid)] = hv[s];
-        for (int sx = (g[s].E - g[s].B) + tid; sx < g[s].nel; sx += TAIL_NT) XS[slot(g[s], t.st[s].dsh, sx)] = make_float2(0.f, 0.f);
-    }
-    __syncthreads();
-#pragma unroll 1
-    for (int s = 0; s < t.S; s++) {
-        const TailStage& st = t.st[s];
-        const TailGeom q = gs[s];
-        if (last)
-            for (int k = tid; k < st.H; k += TAIL_NT) st.histNext[k] = XS[slot(q, st.dsh, st.n + k - q.B)];
-        const int nthr = t.var == 1 ? 0 : (q.b - q.a + TAIL_K - 1) / TAIL_K;
-        for (int l = tid; l < nthr; l += TAIL_NT) {
-            float2 acc[TAIL_K];
-#pragma unroll
-            for (int i = 0; i < TAIL_K; i++) acc[i] = make_float2(0.f, 0.f);
-            constexpr int QC = 8;   // st.Q is a multiple of 8 (FirBlock::upload_taps)
-            for (int p = 0; p < st.D; p++) {
-                const float2* Xj[TAIL_K];
-#pragma unroll
-                for (int j = 0; j < TAIL_K; j++) Xj[j] = XS + q.base + p * q.RSP + j * q.RSK + l;
-                const float* Hp = TS + t.tapOff[s] + p * st.Q;   // wave-uniform LDS broadcasts
-                float2 w[TAIL_K];
-#pragma unroll
-                for (int i = 0; i < TAIL_K; i++) w[i] = Xj[i][0];
-                for (int q0 = 0; q0 < st.Q; q0 += QC) {
-                    float hv[QC];
-                    float2 nx[QC];
-#pragma unroll
-                    for (int u = 0; u < QC; u++) hv[u] = Hp[q0 + u];
-#pragma unroll
-                    for (int u = 0; u < QC; u++) nx[u] = Xj[u % TAIL_K][1 + (q0 + u) / TAIL_K];
-#pragma unroll
-                    for (int u = 0; u < QC; u++) {
-#pragma unroll
-                        for (int i = 0; i < TAIL_K; i++) mac(acc[i], w[(i + u) % TAIL_K], hv[u]);
-                        w[u % TAIL_K] = nx[u];
-                    }
-                }
-            }
-            const bool lastStage = s == t.S - 1;
-            const TailGeom* qn = &gs[lastStage ? s : s + 1];
-            const int dshN = t.st[lastStage ? s : s + 1].dsh, HN = t.st[lastStage ? s : s + 1].H;
-#pragma unroll
-            for (int i = 0; i < TAIL_K; i++) {
-                const int m = q.a + l * TAIL_K + i;
-                if (m < q.b) {
-                    if (lastStage) t.out[m] = acc[i];
-                    else XS[slot(*qn, dshN, HN + m - qn->B)] = acc[i];
-                }
-            }
-        }
-        __syncthreads();
-    }
+    fir_tail_block(t, blockIdx.x, blockIdx.x == gridDim.x - 1, XS, gs);
 }
 
 // ------------------------------------------------ polyphase resampler
@@ -1685,6 +1489,25 @@ int vfo_stage1_prepare(sdrgpu_block* vfo, const void* in, int count, VfoStage1* 
     st->count = count;
     st->out = c->scratch[0].p;
     return 1;
+}
+int vfo_tail_prepare(sdrgpu_block* vfo, const VfoStage1& st, void* out, TailArgs* t, size_t* lds) {
+    auto* c = dynamic_cast<ChainBlock*>(vfo->impl);
+    FirBlock* f[TAIL_MAXS];
+    const int ok = c->tail_plan(st.M, *t, f, *lds);
+    if (ok <= 0) return ok;
+    dynamic_cast<FirBlock*>(c->kids[0].get())->rows_commit(st.count, st.M);
+    t->in = reinterpret_cast<const float2*>(st.out);
+    t->out = reinterpret_cast<float2*>(out);
+    return 1;
+}
+int vfo_tail_commit(sdrgpu_block* vfo, const TailArgs& t) {
+    auto* c = dynamic_cast<ChainBlock*>(vfo->impl);
+    for (int i = 0; i < t.S; i++) {   // FirBlock::run's state update (as launch_tail)
+        auto* f = dynamic_cast<FirBlock*>(c->kids[i + 1].get());
+        f->cur ^= 1;
+        f->offset = f->offset + t.st[i].M * f->D - t.st[i].n;
+    }
+    return t.st[t.S - 1].M;
 }
 int vfo_stage1_finish(sdrgpu_block* vfo, const VfoStage1& st, void* out, hipStream_t s) {
     auto* c = dynamic_cast<ChainBlock*>(vfo->impl);

@@ -19,6 +19,7 @@
 #include "sdrgpu_internal.h"
 #include "fft_stages.h"
 #include "fir_rows.h"
+#include "fir_tail.h"
 
 #ifndef SDRGPU_PB_NT
 #define SDRGPU_PB_NT 1   // 64k pass B: streaming dB row stores (A/B builds: 0)
@@ -891,6 +892,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
         for (int i = w * blockDim.x + threadIdx.x; i < side.n[k]; i += nw * blockDim.x) side.dst[k][i] = side.src[k][i];
 }
 
+// ... and its pass-B launch: the pass-B tiles + the VFO's tail workgroups (fir_tail_block on the
+// first 256 threads of a 512-thread block), one launch for both (the tail needs only the stage-1
+// output the pass-A launch wrote)
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fft_passB_tail_kernel(
+    const float2* __restrict__ scratch, int frames, int N1, int logN, const float2* __restrict__ tw, float* __restrict__ out,
+    TailArgs t) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    __shared__ TailGeom gs[TAIL_MAXS];
+    const int ntiles = (N1 / 32) * frames;
+    if ((int)blockIdx.x < ntiles) {
+        passB_tile<256, 32, false>(lds, blockIdx.x, scratch, frames, N1, logN, tw, out, nullptr);
+        return;
+    }
+    const int w = blockIdx.x - ntiles;
+    fir_tail_block(t, w, w == t.G - 1, lds, gs);
+}
+
 // ---------------------------------------------------------------- host side
 struct FftPlan {
     int device = 0, N = 0, logN = 0, nz = 0;
@@ -940,6 +958,7 @@ struct FftPlan {
     long long tcalls = 0;
     int vfoCP = 0;                    // fused VFO launches: pass-A input cache policy (SDRGPU_FFT_VFO_CP, tuning)
     int vfoFuse = 1;                  // SDRGPU_FFT_VFO_FUSE=0 (tuning): spectrum and VFO as separate launch groups
+    int fuseTail = 1;                 // SDRGPU_FFT_FUSE_TAIL=0 (tuning): the front end's VFO tail as a launch of its own
 };
 static int time_mark(FftPlan& p, int which, hipStream_t s) {
     if (!p.timing) return SDRGPU_OK;
@@ -1314,6 +1333,7 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
             }
         }
     }
+    if (const char* e = tuning_env("SDRGPU_FFT_FUSE_TAIL")) p.fuseTail = atoi(e);
     if (rc >= 0 && hipStreamCreateWithFlags(&p.own, hipStreamNonBlocking) != hipSuccess) {
         set_error("fft_create: hipStreamCreate failed");
         rc = SDRGPU_EHIP;
@@ -1458,7 +1478,8 @@ extern "C" int sdrgpu_fft_execute_dev(sdrgpu_fft* h, const void* in, long long f
 }
 
 int sdrgpu::fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const float2* body, long long stride, int frames,
-                              float* out, const SideCopy& side, hipStream_t s, const VfoStage1* vfo) {
+                              float* out, const SideCopy& side, hipStream_t s, const VfoStage1* vfo, sdrgpu_block* vfoBlock,
+                              void* vfoOut, int* vfoN) {
     if (!h || !body || frames <= 0 || nh < 0 || (nh > 0 && !head)) return SDRGPU_ESTATE;
     FftPlan& p = h->p;
     // the 64k plan's default tiles (256 x 256, 32 columns / 32 rows, one-column pass A); one chunk
@@ -1467,11 +1488,17 @@ int sdrgpu::fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const f
     SDRGPU_CHECK(p.scratch.ensure((size_t)frames * p.N * sizeof(float2)));
     p.cur = p.scratch.as<float2>();
     SDRGPU_CHECK(time_mark(p, 0, s));
-    if (vfo) {
+    if (!vfo) {
+        SDRGPU_CHECK((launch_passA<256, 32>(p, body, stride, frames, s, head, nh, &side)));
+        SDRGPU_CHECK(dispatch_passB(p, frames, out, s));
+        SDRGPU_CHECK(time_mark(p, 1, s));
+        return frames;
+    }
+    const size_t ldsFFT = sizeof(float2) * (32 * Lds<256>::LS + 256 + 256);
+    {   // pass A + the VFO's stage 1 + its history carry + the tail copy
         VfoCall v{vfo->a, (int)((((long long)vfo->M + 31) / 32 + 15) / 16)};
         auto k = fft_passA_vfo_kernel;
-        const size_t lds = sizeof(float2) * (32 * Lds<256>::LS + 256 + 256);
-        SDRGPU_CHECK(set_lds(k, lds));
+        SDRGPU_CHECK(set_lds(k, ldsFFT));
         int spare = 0;
         if (side.count > 0) {
             int mx = 0;
@@ -1479,14 +1506,30 @@ int sdrgpu::fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const f
             spare = std::max(1, std::min(64, (mx + 512 * 4 - 1) / (512 * 4)));   // ~4 elements per thread
         }
         const int g = 8 * frames + v.blocks + 1 + spare;
-        hipLaunchKernelGGL(k, dim3(g), dim3(512), lds, s, body, stride, frames, p.win.as<float>(), p.nz, p.N2, p.logN,
+        hipLaunchKernelGGL(k, dim3(g), dim3(512), ldsFFT, s, body, stride, frames, p.win.as<float>(), p.nz, p.N2, p.logN,
                            p.tw1.as<float2>(), p.tfull.as<float2>(), p.cur, head, nh, side, v);
         SDRGPU_HIP(hipGetLastError());
-    } else {
-        SDRGPU_CHECK((launch_passA<256, 32>(p, body, stride, frames, s, head, nh, &side)));
+    }
+    // pass B + the VFO's later stages (one tail launch's workgroups) where the chain has that form
+    TailArgs t;
+    size_t ldsTail = 0;
+    const int tail = p.fuseTail ? vfo_tail_prepare(vfoBlock, *vfo, vfoOut, &t, &ldsTail) : 0;
+    if (tail < 0) return tail;
+    if (tail) {
+        auto k = fft_passB_tail_kernel;
+        const size_t lds = std::max(ldsFFT, ldsTail);
+        SDRGPU_CHECK(set_lds(k, lds));
+        hipLaunchKernelGGL(k, dim3(8 * frames + t.G), dim3(512), lds, s, p.cur, frames, p.N1, p.logN, p.tw2.as<float2>(), out, t);
+        SDRGPU_HIP(hipGetLastError());
+        *vfoN = vfo_tail_commit(vfoBlock, t);
+        SDRGPU_CHECK(time_mark(p, 1, s));
+        return frames;
     }
     SDRGPU_CHECK(dispatch_passB(p, frames, out, s));
     SDRGPU_CHECK(time_mark(p, 1, s));
+    const int n = vfo_stage1_finish(vfoBlock, *vfo, vfoOut, s);
+    if (n < 0) return n;
+    *vfoN = n;
     return frames;
 }
 

@@ -293,10 +293,9 @@ static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s)
         if (n < 0) return n;
         v.n = n;
     }
-    auto finish_fused = [&](bool launched) -> int {
+    auto run_unfused = [&]() -> int {   // the prepared VFO on its own (no split launch took it)
         if (!fused) return SDRGPU_OK;
-        const int n = launched ? vfo_stage1_finish(fused->vfo, vst, fused->out.p, s)
-                               : block_run_owned(fused->vfo, x, m, fused->out.p, s);
+        const int n = block_run_owned(fused->vfo, x, m, fused->out.p, s);
         if (n < 0) return n;
         fused->n = n;
         return SDRGPU_OK;
@@ -323,10 +322,12 @@ static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s)
             side.n[0] = newLenS;
             side.count = 1;
         }
+        int vn = 0;
         const int rc = fft_execute_split(f->fft, head > 0 ? f->tail[f->curTail].as<float2>() : nullptr, head, body, st, nf,
-                                         spec, side, s, fused ? &vst : nullptr);
+                                         spec, side, s, fused ? &vst : nullptr, fused ? fused->vfo : nullptr,
+                                         fused ? fused->out.p : nullptr, &vn);
         if (rc >= 0) {
-            SDRGPU_CHECK(finish_fused(true));
+            if (fused) fused->n = vn;
             f->nSpec = nf;
             f->nextFrame = nextAfterS;
             f->curTail = nbS;
@@ -336,7 +337,7 @@ static int fe_consume(sdrgpu_frontend* f, const float2* x, int m, hipStream_t s)
         }
         if (rc != SDRGPU_ESTATE) return rc;   // (ESTATE: this plan has no split path; stitch below)
     }
-    SDRGPU_CHECK(finish_fused(false));   // (no split launch: the prepared VFO runs on its own)
+    SDRGPU_CHECK(run_unfused());   // (no split launch: the prepared VFO runs on its own)
     int done = 0;
     // the stitched straddling frame and the new tail are built by one copy launch (up to four
     // device segments) before the spectrum: both read only the old tail and this block

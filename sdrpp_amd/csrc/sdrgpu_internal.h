@@ -158,12 +158,14 @@ struct SideCopy {
 // body[0, nz - nh)], frame f >= 1 starts at body + f * stride - nh. The pass-A launch reads frame 0
 // from both buffers (no stitch copy) and runs `side` with spare workgroups. Returns frames, or
 // SDRGPU_ESTATE when the plan has no such path (the caller then stitches and calls fft_execute_owned).
-// vfo (non-null): the VfoStage1 (fir_rows.h) the pass-A launch also runs (its segments, its history
-// workgroup); the caller then calls vfo_stage1_finish. Returns SDRGPU_ESTATE (nothing launched) where
-// the plan has no split path.
+// vfo (non-null): a prepared VfoStage1 (fir_rows.h) of vfoBlock that the pass-A launch also runs
+// (its segments, its history workgroup); the pass-B launch then carries the VFO's tail workgroups
+// where its later stages have that form, else they run after it. The VFO's output count goes to
+// *vfoN. Returns SDRGPU_ESTATE (nothing launched, the VFO untouched) where the plan has no split path.
 struct VfoStage1;
 int fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const float2* body, long long stride, int frames, float* out,
-                      const SideCopy& side, hipStream_t s, const VfoStage1* vfo = nullptr);
+                      const SideCopy& side, hipStream_t s, const VfoStage1* vfo = nullptr, sdrgpu_block* vfoBlock = nullptr,
+                      void* vfoOut = nullptr, int* vfoN = nullptr);
 // fp64-interior spectrum (fft64.hip): the opt-in parity mode behind sdrgpu_fft_set_precision
 struct Fft64Plan;
 int fft64_create(Fft64Plan** out, int N);
