@@ -637,7 +637,10 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_
 // stages, where the one-workgroup persistent kernel issues both in order from the same waves (its
 // compute and memory times added: DESIGN.md §3 round 3). No software prefetch (no spare VGPRs at
 // four waves per SIMD): the second workgroup is the prefetch.
-template <int CP>
+// RELOAD: each half loads its own column of the pair (8-B loads; the first half with the default
+// cache policy, so the second half's loads of the same 128-B lines hit the cache, the second
+// streaming) instead of keeping the odd column in registers through the first half.
+template <int CP, bool RELOAD = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fft_passA_1m2_kernel(
     const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
     int logN, const float2* __restrict__ tw, const double2* __restrict__ wt, float2* __restrict__ scratch) {
@@ -660,7 +663,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     const unsigned o = (unsigned)(t * N2 + b * S + 2 * cp);
     const int rowB = T * N2 * 8;
     float2 v0[16], v1[16];
-    {
+    if constexpr (!RELOAD) {
         float4 q[16];
         float2 w[16];
 #pragma unroll
@@ -674,14 +677,31 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
             v1[r] = make_float2(q[r].z * w[r].y, q[r].w * w[r].y);
         }
     }
-    dft16(v0);
-    dft16(v1);
+    if constexpr (!RELOAD) {
+        dft16(v0);
+        dft16(v1);
+    }
+    // RELOAD: column 2 cp + h of the pair, windowed, first stage
+    auto load_col = [&](auto hc, float2 (&v)[16]) {
+        constexpr int h = decltype(hc)::value;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const float2 x = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, (o + h) * 8 + r * rowB, 0, h ? 2 : 0));
+            const float w = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, (o + h) * 4 + r * rowB / 2, 0, 0));
+            v[r] = make_float2(x.x * w, x.y * w);
+        }
+        dft16(v);
+    };
     const __amdgpu_buffer_rsrc_t rs = brsrc(scratch + (f << logN), 0x7fffffffu);
     const int c1 = tid % P, t1 = tid / P;   // middle / last stage: local column c1, thread t1 of it
     // one half: the column pair's even (h = 0, v0) or odd (h = 1, v1) member of every thread
     auto half = [&](auto hc, const float2 (&v)[16]) {
         constexpr int h = decltype(hc)::value;
         __syncthreads();   // (h = 0: twl staged; h = 1: the even columns' last-stage reads done)
+        // laundered thread index: the LDS / store addresses are recomputed per half, not hoisted
+        int tv = tid;
+        asm volatile("" : "+v"(tv));
+        const int cp = tv % P, t = tv / P, c1 = tv % P, t1 = tv / P;
         float2* seq = lds + cp * LS;
 #pragma unroll
         for (int r = 0; r < 16; r++) seq[pad16(t * 16 + r)] = v[r];
@@ -715,8 +735,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
             if (m < 15) cur = zmul(cur, step);
         }
     };
-    half(std::integral_constant<int, 0>{}, v0);
-    half(std::integral_constant<int, 1>{}, v1);
+    if constexpr (RELOAD) {
+        load_col(std::integral_constant<int, 0>{}, v0);
+        half(std::integral_constant<int, 0>{}, v0);
+        load_col(std::integral_constant<int, 1>{}, v1);
+        half(std::integral_constant<int, 1>{}, v1);
+    } else {
+        half(std::integral_constant<int, 0>{}, v0);
+        half(std::integral_constant<int, 1>{}, v1);
+    }
 }
 
 // ---- 1M pass B, persistent and software-pipelined (N2 = 1024) -------------------------------
@@ -1188,9 +1215,9 @@ static int launch_passB_1m(FftPlan& p, int frames, float* out, hipStream_t s) {
     return SDRGPU_OK;
 }
 
-template <int CP>
+template <int CP, bool RELOAD = false>
 static int launch_passA_1m2(FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
-    auto k = fft_passA_1m2_kernel<CP>;
+    auto k = fft_passA_1m2_kernel<CP, RELOAD>;
     const size_t lds = sizeof(float2) * (8 * Lds<1024>::LS + 1024 + 256);
     SDRGPU_CHECK(set_lds(k, lds));
     hipLaunchKernelGGL(k, dim3((p.N2 / 16) * frames), dim3(512), lds, s, in, stride, frames, p.win.as<float>(), p.nz, p.N2,
@@ -1202,9 +1229,10 @@ static int launch_passA_1m2(FftPlan& p, const float2* in, long long stride, int 
 // the persistent 1M passes for one chunk, with the tuning variants. Pass B reads the layout pass A
 // wrote: tile-major (pass A VAR 128, the default) or row-major (every other variant).
 static int dispatch_1m(FftPlan& p, const float2* xc, long long stride, int nf, float* o, hipStream_t s) {
-    if (p.pipe1m == 5 || p.pipe1m == 6) {   // two-workgroup pass A (5: streaming input loads, 6: cached)
+    if (p.pipe1m >= 5 && p.pipe1m <= 7) {   // two-workgroup pass A (5: streaming input loads, 6: cached, 7: reload)
         if (p.pipe1m == 5) SDRGPU_CHECK(launch_passA_1m2<2>(p, xc, stride, nf, s));
-        else SDRGPU_CHECK(launch_passA_1m2<0>(p, xc, stride, nf, s));
+        else if (p.pipe1m == 6) SDRGPU_CHECK(launch_passA_1m2<0>(p, xc, stride, nf, s));
+        else SDRGPU_CHECK((launch_passA_1m2<0, true>(p, xc, stride, nf, s)));
         return launch_passB_1m<8, 0, 64 | 128>(p, nf, o, s);
     }
     if (p.pipe1m == 2) {   // (tuning) non-temporal streaming accesses, row-major

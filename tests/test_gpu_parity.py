@@ -605,7 +605,7 @@ def test_fft_1m_batch_multi_chunk(nz, stride, rng):
         db_check(rows[j], oracle.fft_truth_power(xs, nz, N, w), N, ref32_fft_db(xs, nz, N, w))
 
 
-@pytest.mark.parametrize("variant", ["5", "6"])
+@pytest.mark.parametrize("variant", ["5", "6", "7"])
 def test_fft_1m_two_workgroup_pass_a_bit_identical(variant, rng, monkeypatch):
     """The two-workgroups-per-CU 1M pass A (fft_passA_1m2_kernel; SDRGPU_FFT_1M=5 streaming / 6
     cached input loads) is the default pass A's arithmetic in another schedule: every row of a
