@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void fir_kernel(FirArgs a) {
             const float2 ph0 = nco_at(a, b0 - a.H + tid);
             const float2* __restrict__ S = a.nstep;
 #pragma unroll
-            for (int u = 0; u < PF; u++) pf[u] = cmulf(pf[u], cmulf(ph0, S[u]));
+            for (int u = 0; u < PF; u++) pf[u] = xlate_slot(pf[u], ph0, S[u]);
         }
         if (a.simple) {
             // D | NT and K | NT/D: the slot's phase is fixed, its row advances by NT/D
@@ -205,71 +205,113 @@ constexpr int MF_KS = 12;                   // k steps of 4: k < 48 >= 16 + Qp -
 constexpr int MF_GZ = 64;                   // gz entries per phase
 constexpr int mf_rows(int nw) { return 256 * nw + 4 * MF_KS; }   // span rows per phase
 
-template <int NW, bool XL, bool QUAD>   // NW waves per workgroup, 256 outputs each
-__global__ __launch_bounds__(64 * NW) void fir_mfma_kernel(FirArgs a) {
+// HALF (round 4): only half of the D phases' span rows are in LDS at a time -- a thread's span
+// loads all belong to one phase (NT % D == 0), so the threads of the upper phases keep theirs in
+// registers while the MFMAs run over the lower phases, then store them into the same LDS. Half the
+// LDS per workgroup: four workgroups (16 waves) per CU instead of two, the same MFMA chains in the
+// same order (bit-identical outputs).
+template <int NW, bool XL, bool QUAD, bool HALF = false>   // NW waves per workgroup, 256 outputs each
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 1))) void fir_mfma_kernel(FirArgs a) {
     if (fir_hist_block<float2, XL>(a)) return;
     constexpr int NT = 64 * NW, MF_TM = 256 * NW, MF_ROWS = mf_rows(NW);
     constexpr int PF = (MF_ROWS * 8 + NT - 1) / NT;    // load slots per thread for D <= 8
     constexpr int QOFF = QUAD ? 1 : 0;
+    constexpr int NH = HALF ? 2 : 1;                   // phase halves through LDS
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float2* X = reinterpret_cast<float2*>(smem);
     float* gz = reinterpret_cast<float*>(smem + a.tapsLdsOff);
     const int tid = threadIdx.x, tile = blockIdx.x;
     const int D = a.D, RSP = a.RSP, dsh = a.dshift;   // D a power of two dividing NT (host-checked)
+    const int DH = D / NH;                            // phases in LDS at a time
     {
         const float* __restrict__ g = reinterpret_cast<const float*>(a.taps);
         for (int i = tid; i < D * MF_GZ; i += NT) gz[i] = g[i];
     }
-    auto lds_index = [&](int sx) {
+    auto lds_index = [&](int sx) {   // (HALF: the phase's slot within its half)
         const int r = sx >> dsh, p = sx & (D - 1);
-        return p * RSP + r + (r >> 4);
+        return (p % DH) * RSP + r + (r >> 4);
     };
     const int mFirst = tile * a.TMS - QOFF;
     const long long b0 = (long long)a.offset0 + (long long)mFirst * D;
     const int span = MF_ROWS * D;
     const bool interior = (b0 >= a.H) && (b0 + span <= (long long)a.H + a.count);
-    int sxRest = tid;
+    float2 pf[PF];
     if (interior) {
-        const float2* __restrict__ src = reinterpret_cast<const float2*>(a.in) + (b0 - a.H);
-        float2 pf[PF];
+        // XL: the NCO phase of slot 0 is computed before the PF loads are issued (its sincos
+        // temporaries would otherwise be live next to the 2 x PF loaded registers)
+        float2 ph0 = make_float2(1.f, 0.f);
+        if constexpr (XL) {
+            ph0 = nco_at(a, b0 - a.H + tid);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // one wave-uniform buffer resource and ONE per-lane offset for all PF loads, the slot step
+        // in the scalar offset (no per-slot 64-bit address registers; interior: no range check needed)
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float2*>(reinterpret_cast<const float2*>(a.in) + (b0 - a.H)), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
         for (int u = 0; u < PF; u++) {
             const int sx = tid + u * NT;
-            if (sx < span) pf[u] = src[sx];
+            if (sx < span) pf[u] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rsrc, tid * 8, u * NT * 8, 0));
         }
         if constexpr (XL) {
-            const float2 ph0 = nco_at(a, b0 - a.H + tid);
-            const float2* __restrict__ S = a.nstep;
+            // the wave-uniform step table through the constant address space: scalar loads, so
+            // the 2 x PF step values do not take VGPRs next to the PF loaded samples
+            const __attribute__((address_space(4))) float* S = (const __attribute__((address_space(4))) float*)a.nstep;
 #pragma unroll
-            for (int u = 0; u < PF; u++) pf[u] = cmulf(pf[u], cmulf(ph0, S[u]));
+            for (int u = 0; u < PF; u++) pf[u] = xlate_slot(pf[u], ph0, make_float2(S[2 * u], S[2 * u + 1]));
         }
-        // slot u: phase tid % D fixed, row advancing by NT / D (+ its pad rows)
-        int idx = lds_index(tid);
-        const int inc = (NT >> dsh) + (NT >> dsh) / 16;
-#pragma unroll
-        for (int u = 0; u < PF; u++) {
-            if (tid + u * NT < span) X[idx] = pf[u];
-            idx += inc;
-        }
-        sxRest = tid + PF * NT;
     }
-    for (int sx = sxRest; sx < span; sx += NT) X[lds_index(sx)] = fir_fetch<float2, XL>(a, b0 + sx);
-    __syncthreads();
-
     const int lane = tid & 63, o = (tid >> 6) * 256;
     const int i = lane & 15, kk = lane >> 4;   // A row i / B column j = i, k offset kk
     f32x4_t cre = {0.f, 0.f, 0.f, 0.f}, cim = {0.f, 0.f, 0.f, 0.f};
-    for (int p = 0; p < D; p++) {
-        const float2* Xp = X + p * RSP;
-        const float* gp = gz + p * MF_GZ + 15 - i + kk;   // B[k0 + kk][i] = g_p[k0 + kk - i]
-        const int r0 = o + 16 * i + kk;
+    const int myHalf = (tid & (D - 1)) / DH;   // the phase half this thread's span slots belong to
+    auto mfma_half = [&](int h) {
+        for (int p = h * DH; p < (h + 1) * DH; p++) {
+            const float2* Xp = X + (p - h * DH) * RSP;
+            const float* gp = gz + p * MF_GZ + 15 - i + kk;   // B[k0 + kk][i] = g_p[k0 + kk - i]
+            const int r0 = o + 16 * i + kk;
 #pragma unroll
-        for (int s = 0; s < MF_KS; s++) {
-            const int r = r0 + 4 * s;
-            const float2 xa = Xp[r + (r >> 4)];
-            const float bb = gp[4 * s];
-            cre = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.x, bb, cre, 0, 0, 0);
-            cim = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.y, bb, cim, 0, 0, 0);
+            for (int s = 0; s < MF_KS; s++) {
+                const int r = r0 + 4 * s;
+                const float2 xa = Xp[r + (r >> 4)];
+                const float bb = gp[4 * s];
+                cre = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.x, bb, cre, 0, 0, 0);
+                cim = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.y, bb, cim, 0, 0, 0);
+                // HALF: the upper half's PF samples are still live through these MFMAs; fence
+                // the LDS loads in groups of 4 k steps so they are not all hoisted (no spill)
+                if constexpr (HALF) if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    };
+    // the interior and edge tiles run separate half loops: pf is not live across the edge path's
+    // NCO fetches (one shared loop keeps it live there and spills the HALF kernel)
+    if (interior) {
+#pragma unroll
+        for (int h = 0; h < NH; h++) {
+            if (h > 0) __syncthreads();   // every MFMA read of the previous half is done
+            if (myHalf == h) {
+                // slot u: phase tid % D fixed, row advancing by NT / D (+ its pad rows)
+                int idx = lds_index(tid);
+                const int inc = (NT >> dsh) + (NT >> dsh) / 16;
+#pragma unroll
+                for (int u = 0; u < PF; u++) {
+                    if (tid + u * NT < span) X[idx] = pf[u];
+                    idx += inc;
+                }
+            }
+            // (HALF runs only for D <= 8, where the PF slots cover the span: host-checked)
+            if constexpr (!HALF)
+                for (int sx = tid + PF * NT; sx < span; sx += NT) X[lds_index(sx)] = fir_fetch<float2, XL>(a, b0 + sx);
+            __syncthreads();
+            mfma_half(h);
+        }
+    } else {
+        for (int h = 0; h < NH; h++) {
+            if (h > 0) __syncthreads();
+            for (int sx = tid; sx < span; sx += NT)
+                if (((sx & (D - 1)) / DH) == h) X[lds_index(sx)] = fir_fetch<float2, XL>(a, b0 + sx);
+            __syncthreads();
+            mfma_half(h);
         }
     }
     // accumulator element e of this lane: row (lane >> 4) * 4 + e, column lane & 15
@@ -347,7 +389,7 @@ __global__ __launch_bounds__(256) void fir_mfma_ps_kernel(FirArgs a) {
             const float2 ph0 = nco_at(a, b0 - a.H + tid);
             const float2* __restrict__ S = a.nstep;
 #pragma unroll
-            for (int u = 0; u < PF; u++) pf[u] = cmulf(pf[u], cmulf(ph0, S[u]));
+            for (int u = 0; u < PF; u++) pf[u] = xlate_slot(pf[u], ph0, S[u]);
         }
 #pragma unroll
         for (int u = 0; u < PF; u++) {
@@ -680,6 +722,7 @@ struct FirBlock : Block {
         if (const char* e = tuning_env("SDRGPU_FIR_LDS_KB")) ldsCap = std::max(8, atoi(e));
         if (const char* e = tuning_env("SDRGPU_FIR_MFMA")) useMfma = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FIR_MFMA_NW")) mfNW = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FIR_MFMA_HALF")) mfHalf = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FIR_MFMA_PS")) usePS = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FIR_ROWS")) useRows = atoi(e);
         SDRGPU_CHECK(init_stream());
@@ -875,14 +918,15 @@ struct FirBlock : Block {
     int useMfma = 1;        // SDRGPU_FIR_MFMA (tuning): 0 off, 1 auto, 2 also below 16 taps per phase
     DevBuf gzTaps;
     template <int NW, bool XL, bool QD>
-    int launch_mfma(FirArgs& a, int tiles, size_t lds, hipStream_t s) {
-        auto k = fir_mfma_kernel<NW, XL, QD>;
+    int launch_mfma(FirArgs& a, int tiles, size_t lds, bool half, hipStream_t s) {
+        auto k = half ? fir_mfma_kernel<NW, XL, QD, true> : fir_mfma_kernel<NW, XL, QD, false>;
         SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(k, dim3(tiles + (a.histNext ? 1 : 0)), dim3(64 * NW), lds, s, a);
         SDRGPU_HIP(hipGetLastError());
         return SDRGPU_OK;
     }
     int mfNW = 4;           // SDRGPU_FIR_MFMA_NW (tuning): waves (x 256 outputs) per workgroup, 4 or 2 (2: 4 WG/CU, measured 13% slower on C3)
+    int mfHalf = 0;         // SDRGPU_FIR_MFMA_HALF (tuning): half the phases' span in LDS at a time (fir_mfma_kernel HALF)
     template <int NW>
     int run_mfma_nw(const void* in, int count, void* out, int M, hipStream_t s) {
         constexpr int MF_TM = 256 * NW, MF_ROWS = mf_rows(NW);
@@ -897,13 +941,15 @@ struct FirBlock : Block {
         a.dshift = __builtin_ctz((unsigned)D);
         a.invDev = invDev;
         a.nstep = xl ? nco.step_for(64 * NW) : nullptr;
-        const size_t xb = sizeof(float2) * (size_t)D * a.RSP;
+        // HALF needs two phase halves (D >= 2) and the PF load slots covering the span (D <= 8)
+        const bool half = mfHalf && D >= 2 && D <= 8;
+        const size_t xb = std::max(sizeof(float2) * (size_t)(half ? D / 2 : D) * a.RSP, sizeof(float2) * (size_t)MF_TM);
         a.tapsLdsOff = (int)((xb + 15) / 16 * 16);
         const size_t lds = a.tapsLdsOff + sizeof(float) * D * MF_GZ;
         const int tiles = (M + a.TMS - 1) / a.TMS;
         a.ntiles = tiles;
-        if (xl) return quad ? launch_mfma<NW, true, true>(a, tiles, lds, s) : launch_mfma<NW, true, false>(a, tiles, lds, s);
-        return quad ? launch_mfma<NW, false, true>(a, tiles, lds, s) : launch_mfma<NW, false, false>(a, tiles, lds, s);
+        if (xl) return quad ? launch_mfma<NW, true, true>(a, tiles, lds, half, s) : launch_mfma<NW, true, false>(a, tiles, lds, half, s);
+        return quad ? launch_mfma<NW, false, true>(a, tiles, lds, half, s) : launch_mfma<NW, false, false>(a, tiles, lds, half, s);
     }
     int run_mfma(const void* in, int count, void* out, int M, hipStream_t s) {
         return mfNW == 4 ? run_mfma_nw<4>(in, count, out, M, s) : run_mfma_nw<2>(in, count, out, M, s);

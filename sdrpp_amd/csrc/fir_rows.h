@@ -12,6 +12,18 @@ __device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
     return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
+// x * (ph0 * step): the xlator's per-slot product, each complex result pinned to plain VGPRs.
+// Left to itself the SLP vectoriser packs a run of these into v_pk_fma pairs that compute both
+// signs of every term (twice the live registers per slot: the PF-slot kernels spilled on it).
+// The arithmetic is the same two cmulf's.
+__device__ __forceinline__ float2 xlate_slot(float2 x, float2 ph0, float2 step) {
+    float2 ph = cmulf(ph0, step);
+    asm volatile("" : "+v"(ph.x), "+v"(ph.y));
+    float2 r = cmulf(x, ph);
+    asm volatile("" : "+v"(r.x), "+v"(r.y));
+    return r;
+}
+
 // Two-level NCO table: phasor(i) = Phi[i >> 12] * Plo[i & 4095], with
 // Plo[k] = exp(i w k) (fixed per configuration, fp64 -> float on the host) and
 // Phi[j] = exp(i (theta0 + w 4096 j)) (per call, fp64 on the device). Two cached

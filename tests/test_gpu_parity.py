@@ -405,6 +405,34 @@ def test_rows_kernel_d8_on_request(ntaps, quad, rng, monkeypatch):
             assert_close_c(yg, yo, fir_atol(taps, x), "rows FIR D=8")
 
 
+@pytest.mark.parametrize("nw", ["4", "2"])
+@pytest.mark.parametrize("quad,xl", [(True, True), (False, True), (False, False)])
+def test_mfma_half_phase_lds_bit_identical(nw, quad, xl, rng, monkeypatch):
+    # fir_mfma_kernel HALF (SDRGPU_FIR_MFMA_HALF=1, read at block creation) stages half of the D
+    # phases' span in LDS at a time: the same MFMA chains in the same order, so its outputs must
+    # equal the default kernel's bit for bit, across calls (history, NCO phase, quadrature carry)
+    fs = 61.44e6
+    taps = dsp.low_pass(3.0e6, 912000.0, fs)
+    w = 2 * np.pi * (-1.5e6 / fs)
+    dev = 2 * np.pi * 100e3 / (fs / 8)
+
+    def make():
+        if quad:
+            return dsp.DDCFM(w, taps, 8, dev)
+        return dsp.DDC(w, taps, 8) if xl else dsp.FIR(taps, 8)
+    monkeypatch.setenv("SDRGPU_TUNING", "1")
+    monkeypatch.setenv("SDRGPU_FIR_MFMA_NW", nw)
+    monkeypatch.setenv("SDRGPU_FIR_MFMA_HALF", "0")
+    g0 = make()
+    monkeypatch.setenv("SDRGPU_FIR_MFMA_HALF", "1")
+    g1 = make()
+    for n in [307200, 12345, 8, 1 << 20]:
+        x = iq(rng, n)
+        y0, y1 = g0.process(x), g1.process(x)
+        assert len(y0) == len(y1)
+        np.testing.assert_array_equal(y1, y0)
+
+
 def test_registered_host_buffers_dma_directly(rng):
     # sdrgpu_host_register'ed in/out buffers take the direct-DMA path of the host process calls
     # (no staging copy); the results are identical to the staged path
