@@ -54,17 +54,22 @@ def build_lib(force=False, variant=None, defines=()):
     os.makedirs(build, exist_ok=True)
     headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     headers.append(os.path.join(ROOT, "include", "sdrgpu.h"))
-    objs = []
+    objs, cmds = [], []
     for src, extra in SOURCES:
         path = os.path.join(CSRC, src)
         obj = os.path.join(build, src + ".o")
         objs.append(obj)
         if force or _stale(obj, [path] + headers):
             lang = ["-x", "hip"] if src.endswith(".hip") else []
-            _run([HIPCC, "--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17",
-                  "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
-                  "-I", os.path.join(ROOT, "include")] + ["-D" + d for d in defines] + extra + lang +
-                 ["-c", path, "-o", obj])
+            cmds.append([HIPCC, "--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17",
+                         "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+                         "-I", os.path.join(ROOT, "include")] + ["-D" + d for d in defines] + extra + lang +
+                        ["-c", path, "-o", obj])
+    # translation units compile in parallel (at most 8 hipcc processes: the CPU share here and well
+    # under the GPU box's -j16)
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        list(ex.map(_run, cmds))
     lib = os.path.join(libdir, "libsdrgpu.so")
     if force or _stale(lib, objs):
         _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs + ["-ldl"])

@@ -8,8 +8,12 @@
 
 namespace sdrgpu {
 
+// The contraction is spelled out: left to -ffp-contract=fast, a*b - c*d becomes fma(a, b, -cd) in one
+// kernel and fma(-c, d, ab) in another (the SLP vectoriser's packed form picks the other product),
+// and the spectrum launches' VFO stage 1 then differed from fir_rows_kernel's in the last bit
+// (r4b: test_spectrum_vfo_fused). With explicit fmaf there is one rounding sequence everywhere.
 __device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
-    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+    return make_float2(fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x));
 }
 
 // x * (ph0 * step): the xlator's per-slot product, each complex result pinned to plain VGPRs.

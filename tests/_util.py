@@ -31,12 +31,15 @@ def db_check(db_gpu, power_true, N, ref32_db=None, floor_db=60.0):
     2. per bin, in fp32 ulps of the correctly rounded dB of the exact DFT (db_ulp_errors), against
        pocketfft's ulps on the SAME frame (round 4; replaces round 3's 8x ratio of two single-bin dB
        maxima): within-1-ulp fraction >= pocketfft's - 1 point and p99.9 <= pocketfft's + 4 ulp
-       (frames with >= 1000 bins in range), worst bin <= 4x pocketfft's worst + 16 ulp. Measured over
-       the 510-frame corpus (corpus_ulp_rows, profiles/r4/spectrum_corpus_*.json): fraction -0.59
-       points at worst, p99.9 +3 ulp, worst bin 68 vs 17 ulp (4.0x) on one frame -- a heavy-tailed
-       statistic, which is why the corpus test (test_spectrum_ulp_corpus) bounds the worst bins over
-       all frames as well;
-    3. normwise: || |X_gpu| - |X_true| ||_2 <= 4 * eps32 * log2(N) * ||X_true||_2 (all bins).
+       (frames with >= 1000 bins in range). Measured over the 510-frame corpus (corpus_ulp_rows,
+       profiles/r4/spectrum_corpus_*.json): fraction -0.59 points at worst, p99.9 +3 ulp;
+    3. worst bin, per frame, in magnitude: max_k | |X_gpu,k| - |X_true,k| | <= 2x pocketfft's on the
+       same frame (+ eps32 x the rms bin magnitude). The worst bin in dB ulps is not a per-frame bar:
+       it is set by the smallest in-range bins (the absolute error divided by a bin 60 dB down), a
+       heavy-tailed statistic -- r4b: a 64k frame at 102 ulp where pocketfft's worst was 21 ulp, while
+       its fraction, p99.9 and rms matched pocketfft's. The ulp worst bin is bounded over the corpus
+       instead (test_spectrum_ulp_corpus: <= 1.25x pocketfft's worst over all frames of a size);
+    4. normwise: || |X_gpu| - |X_true| ||_2 <= 4 * eps32 * log2(N) * ||X_true||_2 (all bins).
     Without a reference-class FFT the bound is 2e-4 dB."""
     db_true = 10.0 * np.log10(np.maximum(power_true, 1e-300))
     peak = db_true.max()
@@ -56,7 +59,13 @@ def db_check(db_gpu, power_true, N, ref32_db=None, floor_db=60.0):
         if eg.size >= 1000:
             assert sg["frac_le_1ulp"] >= sr["frac_le_1ulp"] - 0.01, (sg, sr)
             assert sg["p999"] <= sr["p999"] + 4.0, (sg, sr)
-        assert sg["max"] <= 4.0 * sr["max"] + 16.0, (sg, sr)
+        mt = np.sqrt(np.asarray(power_true, np.float64))[sel]
+        ag = np.abs(np.sqrt(10.0 ** (db_gpu.astype(np.float64)[sel] / 10.0)) - mt).max()
+        ar = np.abs(np.sqrt(10.0 ** (ref32_db.astype(np.float64)[sel] / 10.0)) - mt).max()
+        rms = np.sqrt(np.mean(np.asarray(power_true, np.float64)))
+        write_report("spectrum_worst_bin", {"N": int(N), "bins": int(eg.size), "ulp_gpu": sg, "ulp_pocketfft": sr,
+                                            "abs_gpu": float(ag), "abs_pocketfft": float(ar), "rms_mag": float(rms)})
+        assert ag <= 2.0 * ar + EPS32 * rms, (ag, ar, rms, sg, sr)
     else:
         assert np.all(err <= np.maximum(2e-4, 2.0 * ulp)), f"max dB err {err.max():.3e}"
     mag_gpu = np.sqrt(10.0 ** (db_gpu.astype(np.float64) / 10.0))

@@ -801,11 +801,18 @@ def test_spectrum_f64_within_1ulp(kind, N, nz, rng):
     e = db_ulp_errors(db, truth, floor_db=200.0)
     s = ulp_summary(e)
     exact = float(np.mean(e == 0))
-    write_report("spectrum_ulp_f64", {"case": kind, "N": N, "nz": nz, "gpu_f64": s, "frac_exact": exact})
+    # exactness is asked of the bins within 160 dB of the peak. Below that an fp64 evaluation's own
+    # error (~eps64 x the frame's energy) reaches the fp32 dB rounding boundaries: the AES17 table -- a
+    # quantised tone over a -200 dB floor -- rounds 0.15% of its bins the other way (r4b, all of them
+    # deep), and an independent fp64 four-step evaluation of it disagrees with numpy's on 4% of its bins,
+    # every one below -160 dB and none above (tools/f64_calibration.py, profiles/r4/f64_calibration_aes17.json)
+    t64 = 10.0 * np.log10(np.maximum(np.asarray(truth, np.float64), 1e-300))
+    near = (t64[t64 >= t64.max() - 200.0] >= t64.max() - 160.0)
+    exact160 = float(np.mean(e[near] == 0))
+    write_report("spectrum_ulp_f64", {"case": kind, "N": N, "nz": nz, "gpu_f64": s, "frac_exact": exact,
+                                      "bins_160dB": int(near.sum()), "frac_exact_160dB": exact160})
     assert s["max"] <= 1.0, s
-    # (the AES17 table -- a 14-bit quantised tone -- reaches 200 dB below its peak, where both fp64
-    # evaluations lose most digits; random and tonal frames were exact on every bin)
-    assert exact >= (0.999 if kind == "aes17" else 0.9999), (s, exact)
+    assert exact160 >= 0.9999, (s, exact160)
     f.set_precision("f32")   # back to the fp32 kernels: same plan, FFTW-class bar
     assert f.precision == "f32"
     e32 = db_ulp_errors(f.logmag(x), truth)
