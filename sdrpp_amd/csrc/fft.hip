@@ -946,16 +946,32 @@ struct VfoWork {
     FirArgs a;       // stage 1 (vfo_stage1_prepare)
     int frame0;      // global frame index of this launch's first pass-A frame
     int hist;        // this launch's last workgroup writes the stage's next-call history
+    int rs32;        // the call's stage has < kRowsMinOutputs outputs: 32-output segments
 };
 constexpr int kVfoRowBatch = 32;   // rows per load batch of the stage-1 segments in these launches
 
+// The segments are those fir_rows_kernel runs for a call of the same size (128 outputs, or 32 below
+// kRowsMinOutputs: launch_rows): a segment's xlator phasors are nco(segment start) x e^{i w D r}, so
+// the segment boundaries are part of the arithmetic, and equal boundaries give equal bits.
 __device__ __forceinline__ void vfo_frame_block(const VfoWork& v, int g) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;   // 8 waves x 2 groups = 16 segments
-    const long long seg = ((long long)(v.frame0 + g) * 8 + wave) * 2 + (lane >> 5);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;   // 8 waves x 2 groups
+    if (v.rs32) {   // 64 segments of 32 outputs per frame, 4 per group
+        for (int k = 0; k < 4; k++) {
+            const long long seg = (long long)(v.frame0 + g) * 64 + k * 16 + wave * 2 + (lane >> 5);
+            fir_rows_segment<32, 5, true, false, 32, 32, true>(v.a, seg, lane);
+        }
+        return;
+    }
+    const long long seg = ((long long)(v.frame0 + g) * 8 + wave) * 2 + (lane >> 5);   // 16 segments of 128
     fir_rows_segment<32, 5, true, false, 128, kVfoRowBatch, true>(v.a, seg, lane);
 }
 
-template <bool ZM, int CP>
+// XG: XCD-grouped frames. Workgroups x, x + 8, x + 16, ... run on one XCD (round-robin dispatch), so
+// workgroup 8 k + x takes item k % 9 of frame 8 (k / 9) + x: a frame's stage-1 workgroup (item 0,
+// dispatched first) and its 8 column tiles share one XCD's L2, and the second reader of each IQ line
+// finds it there instead of crossing the fabric to the Infinity Cache. Ungrouped, a frame's 9
+// consecutive workgroups land on all eight XCDs.
+template <bool ZM, int CP, bool XG = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fft_vfo_kernel(
     int nB, const float2* __restrict__ scratchB, int framesB, float* __restrict__ outB, float* __restrict__ zoomB,
     const float2* __restrict__ in, long long frameStride, int framesA, const float* __restrict__ win, int nz,
@@ -970,7 +986,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
         passB_tile<256, 32, ZM>(lds, blockIdx.x, scratchB, framesB, 256, logN, tw2, outB, zoomB);
         return;
     }
-    const int i = blockIdx.x - nB, g = i / 9, r = i % 9;   // frame g: 8 column tiles, then its VFO block
+    const int i = blockIdx.x - nB;   // (nB = 8 x pass-B frames: XCD lane of i = that of blockIdx.x)
+    int g, r;                        // frame g: 8 column tiles (r < 8), its VFO block (r = 8)
+    if constexpr (XG) {
+        const int k = i >> 3, kk = k % 9;
+        g = 8 * (k / 9) + (i & 7);
+        r = kk == 0 ? 8 : kk - 1;
+        if (g >= framesA) return;    // (padding of the last group of 8 frames)
+    } else {
+        g = i / 9;
+        r = i % 9;
+    }
     if (r == 8) vfo_frame_block(v, g);
     else passA_tile<256, 32, CP>(lds, g * 8 + r, in, frameStride, framesA, win, nz, 256, logN, tw1, tfull, scratchA);
 }
@@ -1077,6 +1103,7 @@ struct FftPlan {
     int vfoCP = 0;                    // fused VFO launches: pass-A input cache policy (SDRGPU_FFT_VFO_CP, tuning)
     int vfoFuse = 1;                  // SDRGPU_FFT_VFO_FUSE=0 (tuning): spectrum and VFO as separate launch groups
     int fuseTail = 1;                 // SDRGPU_FFT_FUSE_TAIL=0 (tuning): the front end's VFO tail as a launch of its own
+    int vfoXcd = 0;                   // SDRGPU_FFT_VFO_XCD (tuning): fft_vfo_kernel's XCD-grouped frames (XG)
 };
 static int time_mark(FftPlan& p, int which, hipStream_t s) {
     if (!p.timing) return SDRGPU_OK;
@@ -1439,6 +1466,7 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         if (const char* e = tuning_env("SDRGPU_FFT_1M_SB")) p.sB1m = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_VFO_CP")) p.vfoCP = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_VFO_FUSE")) p.vfoFuse = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_VFO_XCD")) p.vfoXcd = atoi(e);
         if (rc >= 0 && p.N1 == 1024 && p.N2 == 1024) {   // fp64 W_N^(256 j), W_N^j for the 1M pass A
             std::vector<double2> t(512);
             for (int j = 0; j < 256; j++) {
@@ -1704,14 +1732,14 @@ extern "C" int sdrgpu_fft_execute_zoom_dev(sdrgpu_fft* h, const void* in, long l
 
 // The fused launch group (fft_vfo_kernel): A(0)+V(0); [B(c-1) + A(c)+V(c)] for c = 1..; B(last) +
 // the stage's history workgroup. Scratch alternates between two buffers as in fft_execute.
-template <bool ZM, int CP>
+template <bool ZM, int CP, bool XG = false>
 static int launch_vfo(FftPlan& p, const float2* scratchB, int framesB, float* outB, float* zoomB, const float2* in,
                       int framesA, float2* scratchA, VfoWork v, hipStream_t s) {
-    auto k = fft_vfo_kernel<ZM, CP>;
+    auto k = fft_vfo_kernel<ZM, CP, XG>;
     const size_t lds = sizeof(float2) * (32 * Lds<256>::LS + 256 + 256);
     SDRGPU_CHECK(set_lds(k, lds));
     const int nB = 8 * framesB;
-    const int g = nB + 9 * framesA + (v.hist ? 1 : 0);
+    const int g = nB + (XG ? 72 * ((framesA + 7) / 8) : 9 * framesA) + (v.hist ? 1 : 0);
     hipLaunchKernelGGL(k, dim3(g), dim3(512), lds, s, nB, scratchB, framesB, outB, zoomB, in, (long long)p.N, framesA,
                        p.win.as<float>(), p.nz, p.logN, p.tw1.as<float2>(), p.tw2.as<float2>(), p.tfull.as<float2>(),
                        scratchA, v);
@@ -1720,6 +1748,8 @@ static int launch_vfo(FftPlan& p, const float2* scratchB, int framesB, float* ou
 }
 static int dispatch_vfo(FftPlan& p, bool zm, const float2* scratchB, int framesB, float* outB, float* zoomB,
                         const float2* in, int framesA, float2* scratchA, const VfoWork& v, hipStream_t s) {
+    if (p.vfoXcd) return zm ? launch_vfo<true, 0, true>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
+                            : launch_vfo<false, 0, true>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
     if (zm) return p.vfoCP == 2 ? launch_vfo<true, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
                                 : launch_vfo<true, 0>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
     return p.vfoCP == 2 ? launch_vfo<false, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
@@ -1738,7 +1768,7 @@ static int fft_execute_vfo(FftPlan& p, const float2* x, int frames, float* out, 
     float2* sc[2] = {p.scratch.as<float2>(), p.scratch2.as<float2>()};
     const long long zw = p.N / 32;
     auto zoomAt = [&](long long f0) { return zoom ? zoom + f0 * zw : nullptr; };
-    VfoWork v{st.a, 0, 0};
+    VfoWork v{st.a, 0, 0, st.M < kRowsMinOutputs ? 1 : 0};
     SDRGPU_CHECK(time_mark(p, 0, s));
     SDRGPU_CHECK(dispatch_vfo(p, zoom != nullptr, nullptr, 0, nullptr, nullptr, x, std::min(cf, frames), sc[0], v, s));
     for (int c = 1; c < nchunks; c++) {

@@ -933,6 +933,18 @@ def test_spectrum_zoom_vfo_fused(frames_list, pre, chunk_mb, rng, monkeypatch):
     _fused_vs_separate(frames_list, pre, rng, zoom=True)
 
 
+@pytest.mark.parametrize("frames_list,pre,chunk_mb", [([13], 0, None), ([9, 4], 1001, 1), ([21], 77, 8)])
+def test_spectrum_vfo_fused_xcd(frames_list, pre, chunk_mb, rng, monkeypatch):
+    """The XCD-grouped fused launches (SDRGPU_FFT_VFO_XCD, fft_vfo_kernel<.., XG>: a frame's stage-1
+    workgroup and column tiles on one XCD; frame counts that are not multiples of 8 leave padding
+    workgroups): rows, zoom rows and VFO output bit-identical to the separate launches."""
+    monkeypatch.setenv("SDRGPU_TUNING", "1")
+    monkeypatch.setenv("SDRGPU_FFT_VFO_XCD", "1")
+    if chunk_mb:
+        monkeypatch.setenv("SDRGPU_FFT_CHUNK_MB", str(chunk_mb))
+    _fused_vs_separate(frames_list, pre, rng, zoom=True)
+
+
 # ------------------------------------------------- waterfall zoom fused into the spectrum
 @pytest.mark.parametrize("frames,chunk_mb,zsize", [(3, None, 2048), (9, 1, 2048), (4, None, 1800), (5, 1, 4096)])
 def test_spectrum_zoom_rows(frames, chunk_mb, zsize, rng, monkeypatch):

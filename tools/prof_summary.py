@@ -20,7 +20,7 @@ PEAK = 8000.0
 GROUPS = {
     "c5": r"fft_vfo_kernel<true|fft_passA_kernel<256, 32>|fft_merged_kernel<256, 32, 256, 32|fft_passB_kernel<256, 32, true>",
     "c2": r"fft_passA_1m_kernel|fft_passB_1m_kernel",
-    "c3": r"fir_mfma_kernel<4, true, true>",
+    "c3": r"fir_mfma_kernel<4, true, true",
     "c4": r"chan2_kernel<1024, false>",
     "c4g": r"chan2_kernel<1024, true>",
 }
@@ -42,6 +42,8 @@ def summarise(out, tag, cfg, pattern=None):
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     steps, warm = line["steps"], line["warmup"]
     n = len(rows)
+    if n == 0:
+        raise ValueError(f"{cfg}: no dispatch matches {rx.pattern}")
     if n % (steps + warm):
         raise ValueError(f"{cfg}: {n} group dispatches is not a multiple of {steps + warm} steps")
     dps = n // (steps + warm)
