@@ -284,6 +284,7 @@ def spectrum_ulp_report(dev=0, seed=20261017):
         X = np.fft.fft(xw.astype(np.complex128))
         p64 = X.real ** 2 + X.imag ** 2
         e = ulps(dsp.FFTSpectrum(N, nz, 6, device=dev).logmag(x), p64)
+        e64 = ulps(dsp.FFTSpectrum(N, nz, 6, device=dev, precision="f64").logmag(x), p64)
         Xr = scipy.fft.fft(xw, workers=1)
         pr = Xr.real.astype(np.float32) ** 2 + Xr.imag.astype(np.float32) ** 2
         with np.errstate(divide="ignore"):
@@ -291,8 +292,38 @@ def spectrum_ulp_report(dev=0, seed=20261017):
         out[f"random_N{N}"] = {"bins": int(e.size), "max_ulp": float(e.max()), "p99_ulp": float(np.percentile(e, 99)),
                                "frac_le_1ulp": round(float(np.mean(e <= 1.0)), 4),
                                "pocketfft_max_ulp": float(er.max()),
-                               "pocketfft_frac_le_1ulp": round(float(np.mean(er <= 1.0)), 4)}
-    out["source"] = "measured live in this run (fp64 numpy truth)"
+                               "pocketfft_frac_le_1ulp": round(float(np.mean(er <= 1.0)), 4),
+                               "f64_mode_max_ulp": float(e64.max()), "f64_mode_frac_exact": round(float(np.mean(e64 == 0)), 6)}
+    out["source"] = "measured live in this run (fp64 numpy truth); f64_mode = sdrgpu_fft_set_precision(h, 1)"
+    return out
+
+
+def spectrum_f64_cost(dev, stream, reps=5):
+    """Cost of the fp64-interior parity mode (sdrgpu_fft_set_precision(h, 1)) against the fp32 kernels
+    on the same device batch: 64k BH7 over 2^26 samples (1,024 back-to-back frames) and the C2 1M plan
+    (nz = 1e6) over 32 frames; HIP events on the bench stream, median of `reps` calls after a warm-up."""
+    out = {}
+    for N, nz, frames in ((65536, 65536, 1024), (1 << 20, 1000000, 32)):
+        x = torch.empty(2 * nz * frames, dtype=torch.float32, device="cuda").uniform_(-1, 1)
+        o = torch.empty(N * frames, dtype=torch.float32, device="cuda")
+        r = {}
+        for prec in ("f32", "f64"):
+            f = dsp.FFTSpectrum(N, nz, 6, device=dev, precision=prec)
+            ts = []
+            for k in range(reps + 1):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                f.execute_dev(x.data_ptr(), nz, frames, o.data_ptr(), stream.cuda_stream)
+                e1.record(stream)
+                e1.synchronize()
+                if k:
+                    ts.append(e0.elapsed_time(e1))
+            r[prec] = float(np.median(ts))
+            del f
+        out[f"N{N}"] = {"frames": frames, "samples": nz * frames, "ms_f32": round(r["f32"], 4), "ms_f64": round(r["f64"], 4),
+                        "f64_over_f32": round(r["f64"] / r["f32"], 3),
+                        "MSps_f64": round(nz * frames / r["f64"] / 1e3, 1)}
+        del x, o
     return out
 
 
@@ -601,6 +632,7 @@ def main():
             out["gather"] = head["gather"]
         if not a.no_ulp:
             out["spectrum_ulp"] = spectrum_ulp_report(dev)
+            out["spectrum_f64_mode_cost"] = spectrum_f64_cost(dev, stream)
         if world == 1 and not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline("c4" if a.config == "c4g" else a.config, a.cpu_seconds, head["bytes_per_sample"])
             out["speedup_vs_cpu_all_cores"] = round(out["value"] / out["cpu_baseline"]["value"], 1)

@@ -926,7 +926,9 @@ struct FirBlock : Block {
         return SDRGPU_OK;
     }
     int mfNW = 4;           // SDRGPU_FIR_MFMA_NW (tuning): waves (x 256 outputs) per workgroup, 4 or 2 (2: 4 WG/CU, measured 13% slower on C3)
-    int mfHalf = 0;         // SDRGPU_FIR_MFMA_HALF (tuning): half the phases' span in LDS at a time (fir_mfma_kernel HALF)
+    // fir_mfma_kernel HALF: half the phases' span in LDS at a time, 4 workgroups per CU (105 VGPRs, no
+    // spill); C3 kernel 0.842 -> 0.787 ms (3 interleaved runs, r4d). SDRGPU_FIR_MFMA_HALF=0 (tuning) off
+    int mfHalf = 1;
     template <int NW>
     int run_mfma_nw(const void* in, int count, void* out, int M, hipStream_t s) {
         constexpr int MF_TM = 256 * NW, MF_ROWS = mf_rows(NW);

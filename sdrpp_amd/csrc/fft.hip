@@ -628,124 +628,6 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_
 }
 #undef SDRGPU_PA1M_ISSUE
 
-// ---- 1M pass A at two workgroups per CU (round 4) ------------------------------------------
-// The same 16-column tile and arithmetic as fft_passA_1m_kernel<16, CP, 128> (16-B row loads of
-// column pairs, the tile-major intermediate, bit-identical outputs), but the three-stage column FFT
-// runs through LDS eight columns at a time: the even columns of every thread's pair first, then
-// the odd ones (the odd column waits in registers meanwhile). Half the LDS (80 KB) lets two
-// 512-thread workgroups share a CU, so one workgroup's loads and stores overlap the other's
-// stages, where the one-workgroup persistent kernel issues both in order from the same waves (its
-// compute and memory times added: DESIGN.md §3 round 3). No software prefetch (no spare VGPRs at
-// four waves per SIMD): the second workgroup is the prefetch.
-// RELOAD: each half loads its own column of the pair (8-B loads; the first half with the default
-// cache policy, so the second half's loads of the same 128-B lines hit the cache, the second
-// streaming) instead of keeping the odd column in registers through the first half.
-template <int CP, bool RELOAD = false>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fft_passA_1m2_kernel(
-    const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
-    int logN, const float2* __restrict__ tw, const double2* __restrict__ wt, float2* __restrict__ scratch) {
-    constexpr int L = 1024, S = 16, P = 8, T = L / 16, LS = Lds<L>::LS;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    float2* twl = lds + P * LS;
-    float2* tw16 = twl + L;
-    const int tid = threadIdx.x;
-    const int cp = tid % P, t = tid / P;
-    for (int i = tid; i < L; i += 512) twl[i] = tw[i];   // (the first barrier below orders both)
-    for (int i = tid; i < 256; i += 512) tw16[i] = tw[(i >> 4) * (i & 15) * (L / 256)];
-    const int nb = N2 / S;
-    if ((int)blockIdx.x >= nb * frames) return;
-    const int b = blockIdx.x % nb;
-    const long long f = blockIdx.x / nb;
-    // loads as fft_passA_1m_kernel: the resources end at nz (zero-padded rows read 0), the row step
-    // in the per-lane offset (the range check ignores soffset)
-    const __amdgpu_buffer_rsrc_t rx = brsrc(in + f * frameStride, (unsigned)nz * 8u);
-    const __amdgpu_buffer_rsrc_t rw = brsrc(win, (unsigned)nz * 4u);
-    const unsigned o = (unsigned)(t * N2 + b * S + 2 * cp);
-    const int rowB = T * N2 * 8;
-    float2 v0[16], v1[16];
-    if constexpr (!RELOAD) {
-        float4 q[16];
-        float2 w[16];
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            q[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, o * 8 + r * rowB, 0, CP));
-            w[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rw, o * 4 + r * rowB / 2, 0, 0));
-        }
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            v0[r] = make_float2(q[r].x * w[r].x, q[r].y * w[r].x);
-            v1[r] = make_float2(q[r].z * w[r].y, q[r].w * w[r].y);
-        }
-    }
-    if constexpr (!RELOAD) {
-        dft16(v0);
-        dft16(v1);
-    }
-    // RELOAD: column 2 cp + h of the pair, windowed, first stage
-    auto load_col = [&](auto hc, float2 (&v)[16]) {
-        constexpr int h = decltype(hc)::value;
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const float2 x = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, (o + h) * 8 + r * rowB, 0, h ? 2 : 0));
-            const float w = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, (o + h) * 4 + r * rowB / 2, 0, 0));
-            v[r] = make_float2(x.x * w, x.y * w);
-        }
-        dft16(v);
-    };
-    const __amdgpu_buffer_rsrc_t rs = brsrc(scratch + (f << logN), 0x7fffffffu);
-    const int c1 = tid % P, t1 = tid / P;   // middle / last stage: local column c1, thread t1 of it
-    // one half: the column pair's even (h = 0, v0) or odd (h = 1, v1) member of every thread
-    auto half = [&](auto hc, const float2 (&v)[16]) {
-        constexpr int h = decltype(hc)::value;
-        __syncthreads();   // (h = 0: twl staged; h = 1: the even columns' last-stage reads done)
-        // laundered thread index: the LDS / store addresses are recomputed per half, not hoisted
-        int tv = tid;
-        asm volatile("" : "+v"(tv));
-        const int cp = tv % P, t = tv / P, c1 = tv % P, t1 = tv / P;
-        float2* seq = lds + cp * LS;
-#pragma unroll
-        for (int r = 0; r < 16; r++) seq[pad16(t * 16 + r)] = v[r];
-        __syncthreads();
-        stage_lds_v<L, 16, 16, 1, true>(lds + c1 * LS, twl, t1, tw16);   // (two barriers inside)
-        const int col = b * S + 2 * c1 + h;
-        double2 cur = zmul(wt[(col * t1) >> 8], wt[256 + ((col * t1) & 255)]);
-        const double2 step = zmul(wt[(64 * col) >> 8], wt[256 + ((64 * col) & 255)]);
-        float2 y[16];
-#pragma unroll
-        for (int b4 = 0; b4 < 4; b4++) {   // last stage (radix 4, NS = 256): k1 = t1 + 64 m, m = b4 + 4 r
-            const int j = t1 + b4 * T;
-            float2 u[4];
-#pragma unroll
-            for (int r = 0; r < 4; r++) u[r] = lds[c1 * LS + pad16(j + r * (L / 4))];
-#pragma unroll
-            for (int r = 1; r < 4; r++) u[r] = cmul(u[r], twl[r * j]);
-            dft4v(u);
-#pragma unroll
-            for (int r = 0; r < 4; r++) y[b4 + 4 * r] = u[r];
-        }
-        // tile-major intermediate [b][k1][16 columns] (pass B's VAR 128 layout); the offset is advanced
-        // through an opaque register (no 16 precomputed offsets)
-        unsigned vo = (unsigned)(b * L * S + t1 * S + 2 * c1 + h) * 8u;
-#pragma unroll
-        for (int m = 0; m < 16; m++) {
-            const float2 a = cmul(y[m], make_float2((float)cur.x, (float)cur.y));
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(bu2, a), rs, vo, 0, 0);
-            vo += (unsigned)(T * S * 8);
-            asm volatile("" : "+v"(vo));
-            if (m < 15) cur = zmul(cur, step);
-        }
-    };
-    if constexpr (RELOAD) {
-        load_col(std::integral_constant<int, 0>{}, v0);
-        half(std::integral_constant<int, 0>{}, v0);
-        load_col(std::integral_constant<int, 1>{}, v1);
-        half(std::integral_constant<int, 1>{}, v1);
-    } else {
-        half(std::integral_constant<int, 0>{}, v0);
-        half(std::integral_constant<int, 1>{}, v1);
-    }
-}
-
 // ---- 1M pass B, persistent and software-pipelined (N2 = 1024) -------------------------------
 // Same transform as fft_passB_kernel<1024, S>, each workgroup walking tiles with the next tile's
 // 16 row values per thread loaded while the current tile is transformed and stored.
@@ -1103,7 +985,9 @@ struct FftPlan {
     int vfoCP = 0;                    // fused VFO launches: pass-A input cache policy (SDRGPU_FFT_VFO_CP, tuning)
     int vfoFuse = 1;                  // SDRGPU_FFT_VFO_FUSE=0 (tuning): spectrum and VFO as separate launch groups
     int fuseTail = 1;                 // SDRGPU_FFT_FUSE_TAIL=0 (tuning): the front end's VFO tail as a launch of its own
-    int vfoXcd = 0;                   // SDRGPU_FFT_VFO_XCD (tuning): fft_vfo_kernel's XCD-grouped frames (XG)
+    // fft_vfo_kernel's XCD-grouped frames (XG; SDRGPU_FFT_VFO_XCD=0 off, tuning): C5 spectrum + stage-1
+    // group 1.732 -> 1.694 ms, step 1.820 -> 1.782 ms (3 interleaved runs, r4d)
+    int vfoXcd = 1;
 };
 static int time_mark(FftPlan& p, int which, hipStream_t s) {
     if (!p.timing) return SDRGPU_OK;
@@ -1242,26 +1126,9 @@ static int launch_passB_1m(FftPlan& p, int frames, float* out, hipStream_t s) {
     return SDRGPU_OK;
 }
 
-template <int CP, bool RELOAD = false>
-static int launch_passA_1m2(FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
-    auto k = fft_passA_1m2_kernel<CP, RELOAD>;
-    const size_t lds = sizeof(float2) * (8 * Lds<1024>::LS + 1024 + 256);
-    SDRGPU_CHECK(set_lds(k, lds));
-    hipLaunchKernelGGL(k, dim3((p.N2 / 16) * frames), dim3(512), lds, s, in, stride, frames, p.win.as<float>(), p.nz, p.N2,
-                       p.logN, p.tw1.as<float2>(), p.wt.as<double2>(), p.cur);
-    SDRGPU_HIP(hipGetLastError());
-    return SDRGPU_OK;
-}
-
 // the persistent 1M passes for one chunk, with the tuning variants. Pass B reads the layout pass A
 // wrote: tile-major (pass A VAR 128, the default) or row-major (every other variant).
 static int dispatch_1m(FftPlan& p, const float2* xc, long long stride, int nf, float* o, hipStream_t s) {
-    if (p.pipe1m >= 5 && p.pipe1m <= 7) {   // two-workgroup pass A (5: streaming input loads, 6: cached, 7: reload)
-        if (p.pipe1m == 5) SDRGPU_CHECK(launch_passA_1m2<2>(p, xc, stride, nf, s));
-        else if (p.pipe1m == 6) SDRGPU_CHECK(launch_passA_1m2<0>(p, xc, stride, nf, s));
-        else SDRGPU_CHECK((launch_passA_1m2<0, true>(p, xc, stride, nf, s)));
-        return launch_passB_1m<8, 0, 64 | 128>(p, nf, o, s);
-    }
     if (p.pipe1m == 2) {   // (tuning) non-temporal streaming accesses, row-major
         SDRGPU_CHECK((launch_passA_1m<16, 2, 0>(p, xc, stride, nf, s)));
         return launch_passB_1m<16, 2>(p, nf, o, s);

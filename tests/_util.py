@@ -33,8 +33,9 @@ def db_check(db_gpu, power_true, N, ref32_db=None, floor_db=60.0):
        maxima): within-1-ulp fraction >= pocketfft's - 1 point and p99.9 <= pocketfft's + 4 ulp
        (frames with >= 1000 bins in range). Measured over the 510-frame corpus (corpus_ulp_rows,
        profiles/r4/spectrum_corpus_*.json): fraction -0.59 points at worst, p99.9 +3 ulp;
-    3. worst bin, per frame, in magnitude: max_k | |X_gpu,k| - |X_true,k| | <= 2x pocketfft's on the
-       same frame (+ eps32 x the rms bin magnitude). The worst bin in dB ulps is not a per-frame bar:
+    3. worst bin, per frame, in magnitude: every | |X_gpu,k| - |X_true,k| | <= 2x pocketfft's worst on
+       the same frame + the magnitude step of one fp32 ulp of that bin's dB value (measured r4d: at most
+       1.33x over 30 random frames, 64 to 1M points). The worst bin in dB ulps is not a per-frame bar:
        it is set by the smallest in-range bins (the absolute error divided by a bin 60 dB down), a
        heavy-tailed statistic -- r4b: a 64k frame at 102 ulp where pocketfft's worst was 21 ulp, while
        its fraction, p99.9 and rms matched pocketfft's. The ulp worst bin is bounded over the corpus
@@ -60,12 +61,15 @@ def db_check(db_gpu, power_true, N, ref32_db=None, floor_db=60.0):
             assert sg["frac_le_1ulp"] >= sr["frac_le_1ulp"] - 0.01, (sg, sr)
             assert sg["p999"] <= sr["p999"] + 4.0, (sg, sr)
         mt = np.sqrt(np.asarray(power_true, np.float64))[sel]
-        ag = np.abs(np.sqrt(10.0 ** (db_gpu.astype(np.float64)[sel] / 10.0)) - mt).max()
+        dg = np.abs(np.sqrt(10.0 ** (db_gpu.astype(np.float64)[sel] / 10.0)) - mt)
         ar = np.abs(np.sqrt(10.0 ** (ref32_db.astype(np.float64)[sel] / 10.0)) - mt).max()
-        rms = np.sqrt(np.mean(np.asarray(power_true, np.float64)))
+        # per bin, the magnitude step of one fp32 ulp of its dB value (the row's own quantisation:
+        # tonal frames with a few bins in range sit at it, r4b C1 frames: 1 ulp both, 2.4x in magnitude)
+        q = mt * (np.log(10.0) / 20.0) * np.spacing(np.abs(db_true[sel]).astype(np.float32)).astype(np.float64)
         write_report("spectrum_worst_bin", {"N": int(N), "bins": int(eg.size), "ulp_gpu": sg, "ulp_pocketfft": sr,
-                                            "abs_gpu": float(ag), "abs_pocketfft": float(ar), "rms_mag": float(rms)})
-        assert ag <= 2.0 * ar + EPS32 * rms, (ag, ar, rms, sg, sr)
+                                            "abs_gpu": float(dg.max()), "abs_pocketfft": float(ar),
+                                            "excess_over_q": float((dg - q).max())})
+        assert np.all(dg <= 2.0 * ar + q), (float(dg.max()), float(ar), float((dg - q).max()), sg, sr)
     else:
         assert np.all(err <= np.maximum(2e-4, 2.0 * ulp)), f"max dB err {err.max():.3e}"
     mag_gpu = np.sqrt(10.0 ** (db_gpu.astype(np.float64) / 10.0))

@@ -633,25 +633,6 @@ def test_fft_1m_batch_multi_chunk(nz, stride, rng):
         db_check(rows[j], oracle.fft_truth_power(xs, nz, N, w), N, ref32_fft_db(xs, nz, N, w))
 
 
-@pytest.mark.parametrize("variant", ["5", "6", "7"])
-def test_fft_1m_two_workgroup_pass_a_bit_identical(variant, rng, monkeypatch):
-    """The two-workgroups-per-CU 1M pass A (fft_passA_1m2_kernel; SDRGPU_FFT_1M=5 streaming / 6
-    cached input loads) is the default pass A's arithmetic in another schedule: every row of a
-    ragged two-chunk batch with zero padding is bit-identical to the default kernels'."""
-    import torch
-    N, nz, frames = 1 << 20, 1000000, 17
-    x = iq(rng, nz * frames)
-    d_x = torch.from_numpy(x.view(np.float32)).cuda()
-    ref = torch.empty(frames * N, dtype=torch.float32, device="cuda")
-    got = torch.empty(frames * N, dtype=torch.float32, device="cuda")
-    dsp.FFTSpectrum(N, nz, 6).execute_dev(d_x.data_ptr(), nz, frames, ref.data_ptr())
-    monkeypatch.setenv("SDRGPU_TUNING", "1")
-    monkeypatch.setenv("SDRGPU_FFT_1M", variant)
-    dsp.FFTSpectrum(N, nz, 6).execute_dev(d_x.data_ptr(), nz, frames, got.data_ptr())
-    torch.cuda.synchronize()
-    assert torch.equal(ref, got), float((ref - got).abs().max())
-
-
 def test_process_dev_across_streams(rng):
     """A handle driven from two streams in turn (the NCO table, history and quadrature state are
     per handle) gives the same output stream as one stream: each call waits for the previous one."""
