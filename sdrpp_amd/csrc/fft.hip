@@ -480,18 +480,98 @@ __device__ __forceinline__ void tile_fb(int T, int nb, int& b, long long& f) {
 // bit 6 XCD-grouped column blocks (S = 8); bits 4 / 5 measurement only (below). Measured and
 // removed (r3, C2 step, 3 interleaved runs, one box): the last stage + 8-B stores one column at a
 // time (2.22 vs 1.95 ms), the four-step fp64 tables staged in LDS (2.17 vs 1.95 ms).
-template <int S, int CP, int VAR>   // CP: cache-policy bits of the streaming accesses (0, or 2 = nt; tuning)
+// ---- 1M pass B, persistent and software-pipelined (N2 = 1024) -------------------------------
+// Same transform as fft_passB_kernel<1024, S>, each workgroup walking tiles with the next tile's
+// 16 row values per thread loaded while the current tile is transformed and stored.
+template <int S, int CP, int VAR = 0>   // VAR (measurement only): 16 loads tile 0 only, 32 stores dropped
+__device__ __forceinline__ void passB_1m_body(int tile0, int step, const float2* __restrict__ scratch, int frames,
+                                              int N1, int logN, const float2* __restrict__ tw, float* __restrict__ out) {
+    constexpr int L = 1024, T = L / 16;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    constexpr int XG = (VAR & 64) ? 32 / S : 1;   // XCD grouping of row blocks (bit 6): 128-B dB lines
+    constexpr bool TMAJ = VAR & 128;              // bit 7: the tile-major intermediate of pass A at 16 columns
+    float2* twl = lds + S * Lds<L>::LS;   // stage twiddles, staged once per workgroup
+    float2* tw16 = twl + L;                // the middle stage's, bank-conflict-free (stage_lds)
+    const int tid = threadIdx.x;
+    for (int i = tid; i < L; i += S * T) twl[i] = tw[i];   // (first barrier below orders both)
+    for (int i = tid; i < 256; i += S * T) tw16[i] = tw[(i >> 4) * (i & 15) * (L / 256)];
+    const int sF = tid / T, tF = tid % T;
+    const int nb = N1 / S;
+    const int ntiles = nb * frames;
+    float2 fr[16];
+#define SDRGPU_PB1M_ISSUE(TILE)                                                                                       \
+    do {                                                                                                              \
+        int b_;                                                                                                       \
+        long long f_;                                                                                                 \
+        tile_fb<XG>((TILE), nb, b_, f_);                                                                              \
+        if (VAR & 16) { b_ = 0; f_ = 0; }                                                                             \
+        const __amdgpu_buffer_rsrc_t rs_ = brsrc(scratch + (f_ << logN), 0x7fffffffu);                                \
+        const unsigned o_ = TMAJ ? (unsigned)((tF / 16) * L * 16 + (b_ * S + sF) * 16 + tF % 16) * 8u                 \
+                                 : (unsigned)((b_ * S + sF) * L + tF) * 8u;                                            \
+        _Pragma("unroll") for (int r = 0; r < 16; r++)                                                               \
+            fr[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs_, o_, r * (TMAJ ? 4 * L * 16 * 8 : T * 8), CP)); \
+    } while (0)
+    int tile = tile0;
+    if (tile < ntiles) SDRGPU_PB1M_ISSUE(tile);
+    for (; tile < ntiles; tile += step) {
+        float2 v[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) v[r] = fr[r];
+        if (tile + step < ntiles) SDRGPU_PB1M_ISSUE(tile + step);
+        // the LDS addresses below are loop-invariant; recomputing them per tile (laundered thread
+        // index) keeps ~40 hoisted address registers from spilling the prefetched tile
+        int tv = tid;
+        asm volatile("" : "+v"(tv));
+        const int sF2 = tv / T, tF2 = tv % T, sL2 = tv % S, tL2 = tv / S;
+        __syncthreads();   // the previous tile's last LDS reads are done
+        stage_first<L>(lds + sF2 * Lds<L>::LS, v, tF2);
+        __syncthreads();
+        int b;
+        long long f;
+        tile_fb<XG>(tile, nb, b, f);
+        const __amdgpu_buffer_rsrc_t ro = brsrc(out + (f << logN) + b * S, (VAR & 32) ? 0u : 0x7fffffffu);
+        stages_rest<L, true>(lds, twl, sL2, tL2, [&](int k2, float2 y) {
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, db_of(y)), ro, (unsigned)(sL2 + N1 * k2) * 4u, 0, CP);
+        }, tw16);
+    }
+}
+#undef SDRGPU_PB1M_ISSUE
+
+template <int S, int CP, int VAR = 0>
+__global__ __launch_bounds__(S * 1024 / 16) void fft_passB_1m_kernel(const float2* __restrict__ scratch, int frames, int N1,
+                                                                    int logN, const float2* __restrict__ tw,
+                                                                    float* __restrict__ out) {
+    passB_1m_body<S, CP, VAR>(blockIdx.x, gridDim.x, scratch, frames, N1, logN, tw, out);
+}
+
+// MERGED (round 4, fft_merged_1m launches): the workgroup first runs its share of the previous
+// chunk's pass-B tiles (mb), then this pass A. Both walk tiles blockIdx.x + k gridDim.x; they share
+// nothing (pass A writes the other scratch buffer). Pass B's twiddles sit inside pass A's data
+// region: pass A's first barrier orders its first LDS write after every pass-B read. (The pass-A
+// code stays in the kernel body: moved into a device function, the compiler's allocation changed
+// and the kernel spilled 24 VGPRs.)
+struct MergeB {
+    const float2* scratch;
+    int frames, N1;
+    float* out;
+    const float2* tw;
+};
+template <int S, int CP, int VAR, bool MERGED = false>   // CP: cache-policy bits of the streaming accesses (0, or 2 = nt; tuning)
 __global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_eu(S < 16 ? 2 : 1))) void fft_passA_1m_kernel(
     const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
-    int logN, const float2* __restrict__ tw, const double2* __restrict__ wt, float2* __restrict__ scratch) {
+    int logN, const float2* __restrict__ tw, const double2* __restrict__ wt, float2* __restrict__ scratch, MergeB mb) {
+    if constexpr (MERGED) {
+        if (mb.frames) passB_1m_body<8, 0, 64 | 128>(blockIdx.x, gridDim.x, mb.scratch, mb.frames, mb.N1, logN, mb.tw, mb.out);
+        if (!frames) return;
+    }
     constexpr int L = 1024, P = S / 2, T = L / 16, NT = P * T, LS = Lds<L>::LS;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
     constexpr bool MIDCOL = VAR & 1, LAUNDER = VAR & 8;
     constexpr bool NOLOAD = VAR & 16, NOSTORE = VAR & 32;   // (measurement only: wrong results)
     constexpr int XG = ((VAR & 64) && S < 16) ? 16 / S : 1;   // XCD grouping of column blocks (bit 6): 128-B row lines
     // bit 7: tile-major intermediate [b][k1][c] (each tile's 128 KB written contiguously; pass B
     // then reads 128-B pieces of 16 columns) instead of row-major [k1][n2]
     constexpr bool TMAJ = VAR & 128;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
     float2* twl = lds + S * LS;
     float2* tw16 = twl + L;   // the middle stage's twiddles, bank-conflict-free (stage_lds)
     const int tid = threadIdx.x;
@@ -627,63 +707,6 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_
     }
 }
 #undef SDRGPU_PA1M_ISSUE
-
-// ---- 1M pass B, persistent and software-pipelined (N2 = 1024) -------------------------------
-// Same transform as fft_passB_kernel<1024, S>, each workgroup walking tiles with the next tile's
-// 16 row values per thread loaded while the current tile is transformed and stored.
-template <int S, int CP, int VAR = 0>   // VAR (measurement only): 16 loads tile 0 only, 32 stores dropped
-__global__ __launch_bounds__(S * 1024 / 16) void fft_passB_1m_kernel(const float2* __restrict__ scratch, int frames, int N1,
-                                                                    int logN, const float2* __restrict__ tw,
-                                                                    float* __restrict__ out) {
-    constexpr int L = 1024, T = L / 16;
-    constexpr int XG = (VAR & 64) ? 32 / S : 1;   // XCD grouping of row blocks (bit 6): 128-B dB lines
-    constexpr bool TMAJ = VAR & 128;              // bit 7: the tile-major intermediate of pass A at 16 columns
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    float2* twl = lds + S * Lds<L>::LS;   // stage twiddles, staged once per workgroup
-    float2* tw16 = twl + L;                // the middle stage's, bank-conflict-free (stage_lds)
-    const int tid = threadIdx.x;
-    for (int i = tid; i < L; i += S * T) twl[i] = tw[i];   // (first barrier below orders both)
-    for (int i = tid; i < 256; i += S * T) tw16[i] = tw[(i >> 4) * (i & 15) * (L / 256)];
-    const int sF = tid / T, tF = tid % T;
-    const int nb = N1 / S;
-    const int ntiles = nb * frames;
-    float2 fr[16];
-#define SDRGPU_PB1M_ISSUE(TILE)                                                                                       \
-    do {                                                                                                              \
-        int b_;                                                                                                       \
-        long long f_;                                                                                                 \
-        tile_fb<XG>((TILE), nb, b_, f_);                                                                              \
-        if (VAR & 16) { b_ = 0; f_ = 0; }                                                                             \
-        const __amdgpu_buffer_rsrc_t rs_ = brsrc(scratch + (f_ << logN), 0x7fffffffu);                                \
-        const unsigned o_ = TMAJ ? (unsigned)((tF / 16) * L * 16 + (b_ * S + sF) * 16 + tF % 16) * 8u                 \
-                                 : (unsigned)((b_ * S + sF) * L + tF) * 8u;                                            \
-        _Pragma("unroll") for (int r = 0; r < 16; r++)                                                               \
-            fr[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs_, o_, r * (TMAJ ? 4 * L * 16 * 8 : T * 8), CP)); \
-    } while (0)
-    int tile = blockIdx.x;
-    if (tile < ntiles) SDRGPU_PB1M_ISSUE(tile);
-    for (; tile < ntiles; tile += gridDim.x) {
-        float2 v[16];
-#pragma unroll
-        for (int r = 0; r < 16; r++) v[r] = fr[r];
-        if (tile + (int)gridDim.x < ntiles) SDRGPU_PB1M_ISSUE(tile + (int)gridDim.x);
-        // the LDS addresses below are loop-invariant; recomputing them per tile (laundered thread
-        // index) keeps ~40 hoisted address registers from spilling the prefetched tile
-        int tv = tid;
-        asm volatile("" : "+v"(tv));
-        const int sF2 = tv / T, tF2 = tv % T, sL2 = tv % S, tL2 = tv / S;
-        __syncthreads();   // the previous tile's last LDS reads are done
-        stage_first<L>(lds + sF2 * Lds<L>::LS, v, tF2);
-        __syncthreads();
-        int b;
-        long long f;
-        tile_fb<XG>(tile, nb, b, f);
-        const __amdgpu_buffer_rsrc_t ro = brsrc(out + (f << logN) + b * S, (VAR & 32) ? 0u : 0x7fffffffu);
-        stages_rest<L, true>(lds, twl, sL2, tL2, [&](int k2, float2 y) {
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, db_of(y)), ro, (unsigned)(sL2 + N1 * k2) * 4u, 0, CP);
-        }, tw16);
-    }
-}
 
 // ---- pass B: S rows of length N2 per tile, dB out, transposed store -----------------
 // Stage 1 maps threads row-contiguous (coalesced row reads); the last stage maps the row
@@ -853,7 +876,11 @@ __device__ __forceinline__ void vfo_frame_block(const VfoWork& v, int g) {
 // dispatched first) and its 8 column tiles share one XCD's L2, and the second reader of each IQ line
 // finds it there instead of crossing the fabric to the Infinity Cache. Ungrouped, a frame's 9
 // consecutive workgroups land on all eight XCDs.
-template <bool ZM, int CP, bool XG = false>
+// XG 2 (tuning): also interleaves the two passes -- XCD x's workgroups take, per group of 17, one
+// frame's 8 pass-B row tiles and then one frame's 9 pass-A items, instead of every pass-B tile of
+// the launch first (the Infinity-Cache reads of pass B beside the HBM reads of pass A all launch
+// long, rather than one phase after the other).
+template <bool ZM, int CP, int XG = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fft_vfo_kernel(
     int nB, const float2* __restrict__ scratchB, int framesB, float* __restrict__ outB, float* __restrict__ zoomB,
     const float2* __restrict__ in, long long frameStride, int framesA, const float* __restrict__ win, int nz,
@@ -864,13 +891,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
         (void)fir_hist_block<float2, true, false>(v.a);
         return;
     }
+    int g, r;                        // pass-A frame g: 8 column tiles (r < 8), its VFO block (r = 8)
+    if constexpr (XG == 2) {
+        const int i = blockIdx.x, k = i >> 3, kk = k % 17;
+        const int gs = 8 * (k / 17) + (i & 7);   // frame slot of this XCD lane
+        if (kk < 8) {
+            if (gs < framesB) passB_tile<256, 32, ZM>(lds, gs * 8 + kk, scratchB, framesB, 256, logN, tw2, outB, zoomB);
+            return;
+        }
+        g = gs;
+        r = kk == 8 ? 8 : kk - 9;
+        if (g >= framesA) return;
+    } else {
     if ((int)blockIdx.x < nB) {
         passB_tile<256, 32, ZM>(lds, blockIdx.x, scratchB, framesB, 256, logN, tw2, outB, zoomB);
         return;
     }
     const int i = blockIdx.x - nB;   // (nB = 8 x pass-B frames: XCD lane of i = that of blockIdx.x)
-    int g, r;                        // frame g: 8 column tiles (r < 8), its VFO block (r = 8)
-    if constexpr (XG) {
+    if constexpr (XG == 1) {
         const int k = i >> 3, kk = k % 9;
         g = 8 * (k / 9) + (i & 7);
         r = kk == 0 ? 8 : kk - 1;
@@ -878,6 +916,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     } else {
         g = i / 9;
         r = i % 9;
+    }
     }
     if (r == 8) vfo_frame_block(v, g);
     else passA_tile<256, 32, CP>(lds, g * 8 + r, in, frameStride, framesA, win, nz, 256, logN, tw1, tfull, scratchA);
@@ -945,7 +984,8 @@ struct FftPlan {
     float2* cur = nullptr;            // scratch buffer of the chunk being launched
     int sa2 = 0;                      // paired pass-A columns per workgroup (0: paired kernel off)
     int pipe1m = 1;                   // N1 = N2 = 1024: persistent software-pipelined passes (SDRGPU_FFT_1M=0 off)
-    int gridA = 0, gridB = 0;         // their grids (resident workgroups)
+    int gridA = 0, gridB = 0, gridM = 0;   // their grids (resident workgroups); gridM: the merged 1M launches
+    int merge1m = 0;                  // SDRGPU_FFT_MERGE_1M (tuning): merged pass-B(c-1) + pass-A(c) launches
     // pass-A variant (SDRGPU_FFT_1M_VAR, tuning: fft_passA_1m_kernel's VAR). Default 128: the
     // tile-major intermediate (each pass-A tile's 128 KB written contiguously, 1 KB per store
     // instruction instead of eight 128-B row pieces; pass B reads 16-column pieces of 128 B):
@@ -1103,7 +1143,7 @@ static int launch_passA_1m(FftPlan& p, const float2* in, long long stride, int f
     }
     const int ntiles = (p.N2 / S) * frames;
     hipLaunchKernelGGL(k, dim3(std::min(p.gridA, ntiles)), dim3(S / 2 * 64), lds, s, in, stride, frames, p.win.as<float>(),
-                       p.nz, p.N2, p.logN, p.tw1.as<float2>(), p.wt.as<double2>(), p.cur);
+                       p.nz, p.N2, p.logN, p.tw1.as<float2>(), p.wt.as<double2>(), p.cur, MergeB{});
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
@@ -1122,6 +1162,27 @@ static int launch_passB_1m(FftPlan& p, int frames, float* out, hipStream_t s) {
     const int ntiles = (p.N1 / S) * frames;
     hipLaunchKernelGGL(k, dim3(std::min(p.gridB, ntiles)), dim3(S * 64), lds, s, p.cur, frames, p.N1, p.logN,
                        p.tw2.as<float2>(), out);
+    SDRGPU_HIP(hipGetLastError());
+    return SDRGPU_OK;
+}
+
+// one merged 1M launch (fft_passA_1m_kernel<16, 2, 128, MERGED>): pass B of framesB frames of scratchB
+// (0: none), then pass A of framesA frames into scratchA (0: none)
+static int launch_merged_1m(FftPlan& p, const float2* scratchB, int framesB, float* outB, const float2* in, long long stride,
+                            int framesA, float2* scratchA, hipStream_t s) {
+    auto k = fft_passA_1m_kernel<16, 2, 128, true>;
+    const size_t lds = sizeof(float2) * (16 * Lds<1024>::LS + 1024 + 256);
+    SDRGPU_CHECK(set_lds(k, lds));
+    if (!p.gridM) {
+        int per = 0, cus = 0;
+        SDRGPU_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k, 512, lds));
+        SDRGPU_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p.device));
+        p.gridM = std::max(1, per) * cus;
+    }
+    const int tiles = std::max((p.N1 / 8) * framesB, (p.N2 / 16) * framesA);
+    hipLaunchKernelGGL(k, dim3(std::min(p.gridM, tiles)), dim3(512), lds, s, in, stride, framesA, p.win.as<float>(), p.nz,
+                       p.N2, p.logN, p.tw1.as<float2>(), p.wt.as<double2>(), scratchA,
+                       MergeB{scratchB, framesB, p.N1, outB, p.tw2.as<float2>()});
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
@@ -1327,6 +1388,7 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         p.sa2 = p.N1 >= 512 ? 16 : 0;
         if (const char* e = tuning_env("SDRGPU_FFT_SA2")) p.sa2 = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_1M")) p.pipe1m = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_MERGE_1M")) p.merge1m = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_1M_VAR")) p.var1m = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_1M_VARB")) p.var1mB = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_1M_SA")) p.sA1m = atoi(e);
@@ -1469,6 +1531,22 @@ static int fft_execute_body(sdrgpu_fft* h, const void* in, long long frameStride
         SDRGPU_HIP(hipEventRecord(p.evFork, s));
         SDRGPU_HIP(hipStreamWaitEvent(p.s2, p.evFork, 0));
     }
+    if (pipe1m_ok(p, paired) && !pipe && !zoom && p.merge1m && nchunks > 1 && p.var1m == 128 && p.sA1m == 16 && p.sB1m == 8 &&
+        p.var1mB == 64) {
+        // A(0); [B(c - 1) + A(c)] for c = 1 ..; B(last): the chunks alternate between two scratch buffers
+        SDRGPU_CHECK(p.scratch2.ensure(p.scratch.bytes));
+        float2* sc[2] = {p.scratch.as<float2>(), p.scratch2.as<float2>()};
+        const int cf = p.chunkFrames;
+        SDRGPU_CHECK(launch_merged_1m(p, nullptr, 0, nullptr, x, frameStride, std::min(cf, frames), sc[0], s));
+        for (int c = 1; c < nchunks; c++) {
+            const int fB = (c - 1) * cf, fA = c * cf;
+            SDRGPU_CHECK(launch_merged_1m(p, sc[(c - 1) & 1], cf, out + (long long)fB * p.N, x + (long long)fA * frameStride,
+                                          frameStride, std::min(cf, frames - fA), sc[c & 1], s));
+        }
+        const int fL = (nchunks - 1) * cf;
+        SDRGPU_CHECK(launch_merged_1m(p, sc[(nchunks - 1) & 1], frames - fL, out + (long long)fL * p.N, nullptr, 0, 0, nullptr, s));
+        return frames;
+    }
     for (int c = 0; c < nchunks; c++) {
         const int f0 = c * p.chunkFrames;
         const int nf = std::min(p.chunkFrames, frames - f0);
@@ -1599,14 +1677,15 @@ extern "C" int sdrgpu_fft_execute_zoom_dev(sdrgpu_fft* h, const void* in, long l
 
 // The fused launch group (fft_vfo_kernel): A(0)+V(0); [B(c-1) + A(c)+V(c)] for c = 1..; B(last) +
 // the stage's history workgroup. Scratch alternates between two buffers as in fft_execute.
-template <bool ZM, int CP, bool XG = false>
+template <bool ZM, int CP, int XG = 0>
 static int launch_vfo(FftPlan& p, const float2* scratchB, int framesB, float* outB, float* zoomB, const float2* in,
                       int framesA, float2* scratchA, VfoWork v, hipStream_t s) {
     auto k = fft_vfo_kernel<ZM, CP, XG>;
     const size_t lds = sizeof(float2) * (32 * Lds<256>::LS + 256 + 256);
     SDRGPU_CHECK(set_lds(k, lds));
     const int nB = 8 * framesB;
-    const int g = nB + (XG ? 72 * ((framesA + 7) / 8) : 9 * framesA) + (v.hist ? 1 : 0);
+    const int g = (XG == 2 ? 136 * ((std::max(framesA, framesB) + 7) / 8)
+                           : nB + (XG ? 72 * ((framesA + 7) / 8) : 9 * framesA)) + (v.hist ? 1 : 0);
     hipLaunchKernelGGL(k, dim3(g), dim3(512), lds, s, nB, scratchB, framesB, outB, zoomB, in, (long long)p.N, framesA,
                        p.win.as<float>(), p.nz, p.logN, p.tw1.as<float2>(), p.tw2.as<float2>(), p.tfull.as<float2>(),
                        scratchA, v);
@@ -1615,8 +1694,10 @@ static int launch_vfo(FftPlan& p, const float2* scratchB, int framesB, float* ou
 }
 static int dispatch_vfo(FftPlan& p, bool zm, const float2* scratchB, int framesB, float* outB, float* zoomB,
                         const float2* in, int framesA, float2* scratchA, const VfoWork& v, hipStream_t s) {
-    if (p.vfoXcd) return zm ? launch_vfo<true, 0, true>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
-                            : launch_vfo<false, 0, true>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
+    if (p.vfoXcd == 2) return zm ? launch_vfo<true, 0, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
+                                 : launch_vfo<false, 0, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
+    if (p.vfoXcd) return zm ? launch_vfo<true, 0, 1>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
+                            : launch_vfo<false, 0, 1>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
     if (zm) return p.vfoCP == 2 ? launch_vfo<true, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
                                 : launch_vfo<true, 0>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
     return p.vfoCP == 2 ? launch_vfo<false, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)

@@ -633,6 +633,28 @@ def test_fft_1m_batch_multi_chunk(nz, stride, rng):
         db_check(rows[j], oracle.fft_truth_power(xs, nz, N, w), N, ref32_fft_db(xs, nz, N, w))
 
 
+@pytest.mark.parametrize("chunk_mb,frames", [(16, 5), (None, 17)])
+def test_fft_1m_merged_launches_bit_identical(chunk_mb, frames, rng, monkeypatch):
+    """The merged 1M launches (SDRGPU_FFT_MERGE_1M, fft_merged_1m_kernel: pass B of chunk c - 1 and
+    pass A of chunk c in one persistent launch, scratch alternating between two buffers) run the default
+    passes' tile code: every row of a ragged multi-chunk zero-padded batch is bit-identical."""
+    import torch
+    N, nz = 1 << 20, 1000000
+    x = iq(rng, nz * frames)
+    d_x = torch.from_numpy(x.view(np.float32)).cuda()
+    ref = torch.empty(frames * N, dtype=torch.float32, device="cuda")
+    got = torch.empty(frames * N, dtype=torch.float32, device="cuda")
+    monkeypatch.setenv("SDRGPU_TUNING", "1")
+    if chunk_mb:
+        monkeypatch.setenv("SDRGPU_FFT_CHUNK_MB", str(chunk_mb))
+    monkeypatch.setenv("SDRGPU_FFT_MERGE_1M", "0")
+    dsp.FFTSpectrum(N, nz, 6).execute_dev(d_x.data_ptr(), nz, frames, ref.data_ptr())
+    monkeypatch.setenv("SDRGPU_FFT_MERGE_1M", "1")
+    dsp.FFTSpectrum(N, nz, 6).execute_dev(d_x.data_ptr(), nz, frames, got.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(ref, got), float((ref - got).abs().max())
+
+
 def test_process_dev_across_streams(rng):
     """A handle driven from two streams in turn (the NCO table, history and quadrature state are
     per handle) gives the same output stream as one stream: each call waits for the previous one."""
@@ -914,13 +936,15 @@ def test_spectrum_zoom_vfo_fused(frames_list, pre, chunk_mb, rng, monkeypatch):
     _fused_vs_separate(frames_list, pre, rng, zoom=True)
 
 
+@pytest.mark.parametrize("mode", ["0", "2"])
 @pytest.mark.parametrize("frames_list,pre,chunk_mb", [([13], 0, None), ([9, 4], 1001, 1), ([21], 77, 8)])
-def test_spectrum_vfo_fused_xcd(frames_list, pre, chunk_mb, rng, monkeypatch):
-    """The XCD-grouped fused launches (SDRGPU_FFT_VFO_XCD, fft_vfo_kernel<.., XG>: a frame's stage-1
-    workgroup and column tiles on one XCD; frame counts that are not multiples of 8 leave padding
-    workgroups): rows, zoom rows and VFO output bit-identical to the separate launches."""
+def test_spectrum_vfo_fused_xcd(frames_list, pre, chunk_mb, mode, rng, monkeypatch):
+    """The other fused launch orders (SDRGPU_FFT_VFO_XCD: 0 = a frame's 9 workgroups consecutive, over
+    all XCDs; 2 = XCD-grouped and pass B interleaved with pass A; the default 1 runs in the tests
+    above), frame counts that are not multiples of 8 (padding workgroups) and 1 / 8 MB chunks: rows,
+    zoom rows and VFO output bit-identical to the separate launches."""
     monkeypatch.setenv("SDRGPU_TUNING", "1")
-    monkeypatch.setenv("SDRGPU_FFT_VFO_XCD", "1")
+    monkeypatch.setenv("SDRGPU_FFT_VFO_XCD", mode)
     if chunk_mb:
         monkeypatch.setenv("SDRGPU_FFT_CHUNK_MB", str(chunk_mb))
     _fused_vs_separate(frames_list, pre, rng, zoom=True)

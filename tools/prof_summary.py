@@ -9,7 +9,8 @@ dispatches-per-step of them). Reported per step:
   * rocprof_ms_timed  -- the timed steps only (what the bench's HIP events bracket)
   * event_ms          -- the bench line's roofline.kernel_ms from the same process
   * frac_*            -- algorithmic bytes / time / 8 TB/s for each of the three
-Usage: python tools/prof_summary.py <gpurun_out dir> <TAG> <config> [config ...]"""
+Usage: python tools/prof_summary.py <gpurun_out dir> <TAG> <config> [config ...]
+       python tools/prof_summary.py --combined <gpurun_out dir> <TAG>   (session step benchprof)"""
 import csv
 import json
 import os
@@ -19,7 +20,7 @@ import sys
 PEAK = 8000.0
 GROUPS = {
     "c5": r"fft_vfo_kernel<true|fft_passA_kernel<256, 32>|fft_merged_kernel<256, 32, 256, 32|fft_passB_kernel<256, 32, true>",
-    "c2": r"fft_passA_1m_kernel|fft_passB_1m_kernel",
+    "c2": r"fft_passA_1m_kernel<16, 2, 128|fft_passB_1m_kernel<8, 0, 192",
     "c3": r"fir_mfma_kernel<4, true, true",
     "c4": r"chan2_kernel<1024, false>",
     "c4g": r"chan2_kernel<1024, true>",
@@ -40,6 +41,42 @@ def summarise(out, tag, cfg, pattern=None):
     rx = re.compile(pattern or GROUPS[cfg])
     rows = [r for r in csv.DictReader(open(trace)) if rx.search(r["Kernel_Name"])]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    return reduce_rows(cfg, rows, line)
+
+
+BENCH_ORDER = ["c5", "c2", "c3", "c4", "c4g"]   # bench.py main(): the head config, then the others in this order
+
+
+def summarise_combined(out, tag):
+    """`benchprof` step: ONE default bench process under rocprofv3; every config's group dispatches are
+    taken from the window between its first dispatch and the next config's first dispatch (the live
+    ulp report, the fp64-mode cost and the per-call runs come after all configs)."""
+    trace = os.path.join(out, f"{tag}_benchprof", "run_kernel_trace.csv")
+    line = line_of(os.path.join(out, f"{tag}_bench.json"))
+    allrows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
+    order = [line.get("config_key", "c5")] + [c for c in BENCH_ORDER if c in line.get("configs", {})]
+    first = {}
+    for c in order:
+        rx = re.compile(GROUPS[c])
+        ts = [int(r["Start_Timestamp"]) for r in allrows if rx.search(r["Kernel_Name"])]
+        first[c] = ts[0] if ts else None
+    res = {}
+    for i, c in enumerate(order):
+        rx = re.compile(GROUPS[c])
+        lo = first[c]
+        hi = next((first[n] for n in order[i + 1:] if first[n] is not None and first[n] > lo), None) if lo else None
+        rows = [r for r in allrows if rx.search(r["Kernel_Name"]) and int(r["Start_Timestamp"]) >= (lo or 0)
+                and (hi is None or int(r["Start_Timestamp"]) < hi)]
+        sub = line if i == 0 else dict(line["configs"][c], steps=line["steps"], warmup=line["warmup"])
+        try:
+            res[c] = reduce_rows(c, rows, sub)
+        except (ValueError, KeyError) as e:
+            res[c] = {"error": str(e)}
+    return res
+
+
+def reduce_rows(cfg, rows, line):
+    rx = re.compile(GROUPS[cfg])
     steps, warm = line["steps"], line["warmup"]
     n = len(rows)
     if n == 0:
@@ -74,6 +111,9 @@ def summarise(out, tag, cfg, pattern=None):
 
 
 def main():
+    if sys.argv[1] == "--combined":
+        print(json.dumps(summarise_combined(sys.argv[2], sys.argv[3]), indent=1))
+        return
     out, tag, cfgs = sys.argv[1], sys.argv[2], sys.argv[3:]
     res = {}
     for c in cfgs:

@@ -6,6 +6,8 @@
 #   corpus  spectrum ulp corpus (tools/fft_corpus.py), in-tree build + CORPUS_VARIANTS lib_<v> builds
 #   smoke   __graft_entry__.smoke()
 #   bench   the default bench line (all configs, CPU legs, per-call)   -> TAG_bench.json
+#   benchprof the default bench under rocprofv3 --kernel-trace --stats: the line and its trace from one
+#           process -> TAG_bench.json, TAG_benchprof/, TAG_benchprof_summary.json
 #   prof    per config in PROF_CFGS: rocprofv3 --kernel-trace --stats around `bench.py --config c
 #           --no-sub --no-cpu --no-ulp`; the same process's JSON line is kept next to the stats, and
 #           tools/prof_summary.py reduces both to TAG_prof_summary.json (timed dispatches only)
@@ -52,6 +54,12 @@ for step in $STEPS_LIST; do
   bench)
     timeout -k 10 700 python bench.py ${BENCH_ARGS:-} > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"
     st bench $? ;;
+  benchprof)   # the default bench line and its kernel trace from ONE process (prof_summary --combined)
+    prof x timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_benchprof" -o run -- \
+      python3 "$R/bench.py" ${BENCH_ARGS:-} > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"
+    st benchprof $?
+    python tools/prof_summary.py --combined "$OUT" "$TAG" > "$OUT/${TAG}_benchprof_summary.json" 2>> "$ST"
+    st benchprof_summary $? ;;
   prof)
     for c in $PROF_CFGS; do
       prof x timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof_$c" -o run -- \
