@@ -210,7 +210,11 @@ constexpr int mf_rows(int nw) { return 256 * nw + 4 * MF_KS; }   // span rows pe
 // registers while the MFMAs run over the lower phases, then store them into the same LDS. Half the
 // LDS per workgroup: four workgroups (16 waves) per CU instead of two, the same MFMA chains in the
 // same order (bit-identical outputs).
-template <int NW, bool XL, bool QUAD, bool HALF = false>   // NW waves per workgroup, 256 outputs each
+// DC (round 4): the decimation as a compile-time constant (0: a.D at run time). C3's D = 8 then has a
+// constant span, so the PF load / store slots need no range guards (only the last is partial) and the
+// LDS indices fold: the SQ counters showed the SIMD ~90% busy with MFMA + VALU issue (no co-issue on
+// the f32 matrix path), so every VALU instruction saved is kernel time.
+template <int NW, bool XL, bool QUAD, bool HALF = false, int DC = 0>   // NW waves per workgroup, 256 outputs each
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 1))) void fir_mfma_kernel(FirArgs a) {
     if (fir_hist_block<float2, XL>(a)) return;
     constexpr int NT = 64 * NW, MF_TM = 256 * NW, MF_ROWS = mf_rows(NW);
@@ -221,7 +225,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(HALF ? 
     float2* X = reinterpret_cast<float2*>(smem);
     float* gz = reinterpret_cast<float*>(smem + a.tapsLdsOff);
     const int tid = threadIdx.x, tile = blockIdx.x;
-    const int D = a.D, RSP = a.RSP, dsh = a.dshift;   // D a power of two dividing NT (host-checked)
+    // D a power of two dividing NT (host-checked); RSP = MF_ROWS + MF_ROWS / 16 + 1 (run_mfma_nw)
+    const int D = DC ? DC : a.D, RSP = DC ? MF_ROWS + MF_ROWS / 16 + 1 : a.RSP;
+    const int dsh = DC ? __builtin_ctz((unsigned)(DC ? DC : 1)) : a.dshift;
     const int DH = D / NH;                            // phases in LDS at a time
     {
         const float* __restrict__ g = reinterpret_cast<const float*>(a.taps);
@@ -723,6 +729,7 @@ struct FirBlock : Block {
         if (const char* e = tuning_env("SDRGPU_FIR_MFMA")) useMfma = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FIR_MFMA_NW")) mfNW = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FIR_MFMA_HALF")) mfHalf = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FIR_MFMA_DC")) mfDc = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FIR_MFMA_PS")) usePS = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FIR_ROWS")) useRows = atoi(e);
         SDRGPU_CHECK(init_stream());
@@ -919,7 +926,8 @@ struct FirBlock : Block {
     DevBuf gzTaps;
     template <int NW, bool XL, bool QD>
     int launch_mfma(FirArgs& a, int tiles, size_t lds, bool half, hipStream_t s) {
-        auto k = half ? fir_mfma_kernel<NW, XL, QD, true> : fir_mfma_kernel<NW, XL, QD, false>;
+        auto k = half ? (a.D == 8 && mfDc ? fir_mfma_kernel<NW, XL, QD, true, 8> : fir_mfma_kernel<NW, XL, QD, true>)
+                      : (a.D == 8 && mfDc ? fir_mfma_kernel<NW, XL, QD, false, 8> : fir_mfma_kernel<NW, XL, QD, false>);
         SDRGPU_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(k, dim3(tiles + (a.histNext ? 1 : 0)), dim3(64 * NW), lds, s, a);
         SDRGPU_HIP(hipGetLastError());
@@ -929,6 +937,7 @@ struct FirBlock : Block {
     // fir_mfma_kernel HALF: half the phases' span in LDS at a time, 4 workgroups per CU (105 VGPRs, no
     // spill); C3 kernel 0.842 -> 0.787 ms (3 interleaved runs, r4d). SDRGPU_FIR_MFMA_HALF=0 (tuning) off
     int mfHalf = 1;
+    int mfDc = 1;           // SDRGPU_FIR_MFMA_DC=0 (tuning): D = 8 as a run-time value (fir_mfma_kernel DC)
     template <int NW>
     int run_mfma_nw(const void* in, int count, void* out, int M, hipStream_t s) {
         constexpr int MF_TM = 256 * NW, MF_ROWS = mf_rows(NW);

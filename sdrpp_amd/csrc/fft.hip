@@ -870,12 +870,23 @@ __device__ __forceinline__ void vfo_frame_block(const VfoWork& v, int g) {
     const long long seg = ((long long)(v.frame0 + g) * 8 + wave) * 2 + (lane >> 5);   // 16 segments of 128
     fir_rows_segment<32, 5, true, false, 128, kVfoRowBatch, true>(v.a, seg, lane);
 }
+// (XG 3) quarter q of frame g's stage-1 outputs: 16 segments of 32 outputs, one per D-lane group, one
+// row batch each -- a workgroup that lives one load round, like the column tiles beside it
+__device__ __forceinline__ void vfo_quarter_block(const VfoWork& v, int g, int q) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const long long seg = (long long)(v.frame0 + g) * 64 + q * 16 + wave * 2 + (lane >> 5);
+    fir_rows_segment<32, 5, true, false, 32, 32, true>(v.a, seg, lane);
+}
 
 // XG: XCD-grouped frames. Workgroups x, x + 8, x + 16, ... run on one XCD (round-robin dispatch), so
 // workgroup 8 k + x takes item k % 9 of frame 8 (k / 9) + x: a frame's stage-1 workgroup (item 0,
 // dispatched first) and its 8 column tiles share one XCD's L2, and the second reader of each IQ line
 // finds it there instead of crossing the fabric to the Infinity Cache. Ungrouped, a frame's 9
 // consecutive workgroups land on all eight XCDs.
+// XG 3 (tuning): a frame's stage 1 as 4 quarter workgroups of 32-output segments (one row batch
+// each: they live one load round, as the 8 column tiles beside them do, so both read the frame's
+// lines at the same time); 32-output segments at every call size (fir_rows_kernel uses them below
+// kRowsMinOutputs only, so above it the two differ in the last bit).
 // XG 2 (tuning): also interleaves the two passes -- XCD x's workgroups take, per group of 17, one
 // frame's 8 pass-B row tiles and then one frame's 9 pass-A items, instead of every pass-B tile of
 // the launch first (the Infinity-Cache reads of pass B beside the HBM reads of pass A all launch
@@ -892,7 +903,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
         return;
     }
     int g, r;                        // pass-A frame g: 8 column tiles (r < 8), its VFO block (r = 8)
-    if constexpr (XG == 2) {
+    if constexpr (XG == 3) {
+        if ((int)blockIdx.x < nB) {
+            passB_tile<256, 32, ZM>(lds, blockIdx.x, scratchB, framesB, 256, logN, tw2, outB, zoomB);
+            return;
+        }
+        const int i = blockIdx.x - nB, k = i >> 3, kk = k % 12;
+        g = 8 * (k / 12) + (i & 7);
+        if (g >= framesA) return;
+        if (kk < 4) {
+            vfo_quarter_block(v, g, kk);
+            return;
+        }
+        passA_tile<256, 32, CP>(lds, g * 8 + kk - 4, in, frameStride, framesA, win, nz, 256, logN, tw1, tfull, scratchA);
+        return;
+    } else if constexpr (XG == 2) {
         const int i = blockIdx.x, k = i >> 3, kk = k % 17;
         const int gs = 8 * (k / 17) + (i & 7);   // frame slot of this XCD lane
         if (kk < 8) {
@@ -1685,7 +1710,8 @@ static int launch_vfo(FftPlan& p, const float2* scratchB, int framesB, float* ou
     SDRGPU_CHECK(set_lds(k, lds));
     const int nB = 8 * framesB;
     const int g = (XG == 2 ? 136 * ((std::max(framesA, framesB) + 7) / 8)
-                           : nB + (XG ? 72 * ((framesA + 7) / 8) : 9 * framesA)) + (v.hist ? 1 : 0);
+                           : nB + (XG == 3 ? 96 * ((framesA + 7) / 8) : XG ? 72 * ((framesA + 7) / 8) : 9 * framesA)) +
+                  (v.hist ? 1 : 0);
     hipLaunchKernelGGL(k, dim3(g), dim3(512), lds, s, nB, scratchB, framesB, outB, zoomB, in, (long long)p.N, framesA,
                        p.win.as<float>(), p.nz, p.logN, p.tw1.as<float2>(), p.tw2.as<float2>(), p.tfull.as<float2>(),
                        scratchA, v);
@@ -1694,6 +1720,8 @@ static int launch_vfo(FftPlan& p, const float2* scratchB, int framesB, float* ou
 }
 static int dispatch_vfo(FftPlan& p, bool zm, const float2* scratchB, int framesB, float* outB, float* zoomB,
                         const float2* in, int framesA, float2* scratchA, const VfoWork& v, hipStream_t s) {
+    if (p.vfoXcd == 3) return zm ? launch_vfo<true, 0, 3>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
+                                 : launch_vfo<false, 0, 3>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
     if (p.vfoXcd == 2) return zm ? launch_vfo<true, 0, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
                                  : launch_vfo<false, 0, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
     if (p.vfoXcd) return zm ? launch_vfo<true, 0, 1>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)

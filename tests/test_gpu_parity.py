@@ -420,17 +420,26 @@ def test_mfma_half_phase_lds_bit_identical(nw, quad, xl, rng, monkeypatch):
         if quad:
             return dsp.DDCFM(w, taps, 8, dev)
         return dsp.DDC(w, taps, 8) if xl else dsp.FIR(taps, 8)
+    # The same holds for DC (SDRGPU_FIR_MFMA_DC, the decimation as a compile-time constant): the
+    # reference kernel here is the full-LDS, run-time-D one; both others must match it bit for bit
     monkeypatch.setenv("SDRGPU_TUNING", "1")
     monkeypatch.setenv("SDRGPU_FIR_MFMA_NW", nw)
     monkeypatch.setenv("SDRGPU_FIR_MFMA_HALF", "0")
+    monkeypatch.setenv("SDRGPU_FIR_MFMA_DC", "0")
     g0 = make()
     monkeypatch.setenv("SDRGPU_FIR_MFMA_HALF", "1")
     g1 = make()
+    monkeypatch.setenv("SDRGPU_FIR_MFMA_DC", "1")
+    g2 = make()
+    monkeypatch.setenv("SDRGPU_FIR_MFMA_HALF", "0")
+    g3 = make()
     for n in [307200, 12345, 8, 1 << 20]:
         x = iq(rng, n)
-        y0, y1 = g0.process(x), g1.process(x)
-        assert len(y0) == len(y1)
+        y0, y1, y2, y3 = g0.process(x), g1.process(x), g2.process(x), g3.process(x)
+        assert len(y0) == len(y1) == len(y2) == len(y3)
         np.testing.assert_array_equal(y1, y0)
+        np.testing.assert_array_equal(y2, y0)
+        np.testing.assert_array_equal(y3, y0)
 
 
 def test_registered_host_buffers_dma_directly(rng):
