@@ -81,9 +81,9 @@ class C5:
             # the group: 8 B in (read once), 4 B dB + 4/32 B zoom rows out, 8/32 B VFO stage-1 out
             self.kernel_bytes = (12.0 + 4 / 32 + 8 / 32) * self.B
             self.kernel_name = ("spectrum N=65536 + zoom to 2048 + RxVFO stage 1 (D=32, 143 taps, xlator): "
-                                "fft_vfo_kernel<zoom,0,XG> x17 (each frame's stage-1 workgroup and 8 pass-A column "
-                                "tiles on one XCD, so the stage re-reads the IQ from that XCD's L2; pass B of the "
-                                "previous chunk)")
+                                "fft_vfo_kernel<zoom,0,3> x17 (each frame's 8 pass-A column tiles and 4 quarter-frame "
+                                "stage-1 workgroups on one XCD, all one load round, so the stage's read of the IQ is "
+                                "served by that XCD's L2; pass B of the previous chunk)")
             self.fft.set_timing(True)   # the group's own HIP events (the VFO's later stages are outside it)
         else:
             self.kernel_bytes = (12.0 + 4 / 32) * self.B            # spectrum: 8 B in, 4 B dB + 4/32 B zoom out
@@ -150,7 +150,7 @@ class C3:
         self.out = torch.empty(B // 8 + 64, dtype=torch.float32, device="cuda")
         self.bytes_per_sample = 8 + 4 / 8
         self.kernel_bytes = self.bytes_per_sample * B
-        self.kernel_name = "fir_mfma_kernel<4,XL,QUAD,HALF> (xlator + 256-tap FIR /8 on f32 MFMA + quadrature; half the phases' span in LDS at a time, 4 workgroups per CU)"
+        self.kernel_name = "fir_mfma_kernel<4,XL,QUAD,HALF,D=8> (xlator + 256-tap FIR /8 on f32 MFMA + quadrature; half the phases' span in LDS at a time, 4 workgroups per CU; D a compile-time constant)"
 
     def dominant(self, x, s):
         self.ddc.process_dev(x.data_ptr(), self.B, self.out.data_ptr(), s)

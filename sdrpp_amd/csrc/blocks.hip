@@ -823,14 +823,13 @@ struct FirBlock : Block {
         SDRGPU_HIP(hipGetLastError());
         return SDRGPU_OK;
     }
-    // D = 32: 128-output segments for big calls; a small call (a reference-size block: 9,600
-    // stage-1 outputs -> 75 segments, 10 workgroups, 62 us) takes 32-output segments instead
-    // (300 segments, one row batch each)
+    // D = 32: 32-output segments (one row batch each) at every call size, the segments the spectrum
+    // launches cut for a fused first stage (fft.hip vfo_quarter_block: same segments, same bits); a
+    // reference-size block (9,600 stage-1 outputs) is 300 segments, where 128-output ones were 75
+    // segments in 10 workgroups (62 us)
     template <int D, int QP, bool QD>
     int launch_rows(FirArgs& a, hipStream_t s) {
-        if constexpr (D == 32 && !QD) {
-            if (a.M < kRowsMinOutputs) return launch_rows_rs<D, QP, QD, 32>(a, s);
-        }
+        if constexpr (D == 32 && !QD) return launch_rows_rs<D, QP, QD, 32>(a, s);
         return launch_rows_rs<D, QP, QD>(a, s);
     }
     // taps per phase of the rows kernel: D = 32 exact (2..8), D = 8 padded to 16, 24 or 32

@@ -851,27 +851,20 @@ struct VfoWork {
     FirArgs a;       // stage 1 (vfo_stage1_prepare)
     int frame0;      // global frame index of this launch's first pass-A frame
     int hist;        // this launch's last workgroup writes the stage's next-call history
-    int rs32;        // the call's stage has < kRowsMinOutputs outputs: 32-output segments
 };
-constexpr int kVfoRowBatch = 32;   // rows per load batch of the stage-1 segments in these launches
 
-// The segments are those fir_rows_kernel runs for a call of the same size (128 outputs, or 32 below
-// kRowsMinOutputs: launch_rows): a segment's xlator phasors are nco(segment start) x e^{i w D r}, so
-// the segment boundaries are part of the arithmetic, and equal boundaries give equal bits.
+// The segments are those fir_rows_kernel runs (32 outputs, launch_rows): a segment's xlator phasors
+// are nco(segment start) x e^{i w D r}, so the segment boundaries are part of the arithmetic, and equal
+// boundaries give equal bits. (XG 0-2) one workgroup per frame: 64 segments, 4 per D-lane group.
 __device__ __forceinline__ void vfo_frame_block(const VfoWork& v, int g) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;   // 8 waves x 2 groups
-    if (v.rs32) {   // 64 segments of 32 outputs per frame, 4 per group
-        for (int k = 0; k < 4; k++) {
-            const long long seg = (long long)(v.frame0 + g) * 64 + k * 16 + wave * 2 + (lane >> 5);
-            fir_rows_segment<32, 5, true, false, 32, 32, true>(v.a, seg, lane);
-        }
-        return;
+    for (int k = 0; k < 4; k++) {
+        const long long seg = (long long)(v.frame0 + g) * 64 + k * 16 + wave * 2 + (lane >> 5);
+        fir_rows_segment<32, 5, true, false, 32, 32, true>(v.a, seg, lane);
     }
-    const long long seg = ((long long)(v.frame0 + g) * 8 + wave) * 2 + (lane >> 5);   // 16 segments of 128
-    fir_rows_segment<32, 5, true, false, 128, kVfoRowBatch, true>(v.a, seg, lane);
 }
-// (XG 3) quarter q of frame g's stage-1 outputs: 16 segments of 32 outputs, one per D-lane group, one
-// row batch each -- a workgroup that lives one load round, like the column tiles beside it
+// (XG 3, the default) quarter q of frame g's stage-1 outputs: 16 segments of 32 outputs, one per D-lane
+// group, one row batch each -- a workgroup that lives one load round, like the column tiles beside it
 __device__ __forceinline__ void vfo_quarter_block(const VfoWork& v, int g, int q) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const long long seg = (long long)(v.frame0 + g) * 64 + q * 16 + wave * 2 + (lane >> 5);
@@ -883,10 +876,10 @@ __device__ __forceinline__ void vfo_quarter_block(const VfoWork& v, int g, int q
 // dispatched first) and its 8 column tiles share one XCD's L2, and the second reader of each IQ line
 // finds it there instead of crossing the fabric to the Infinity Cache. Ungrouped, a frame's 9
 // consecutive workgroups land on all eight XCDs.
-// XG 3 (tuning): a frame's stage 1 as 4 quarter workgroups of 32-output segments (one row batch
-// each: they live one load round, as the 8 column tiles beside them do, so both read the frame's
-// lines at the same time); 32-output segments at every call size (fir_rows_kernel uses them below
-// kRowsMinOutputs only, so above it the two differ in the last bit).
+// XG 3 (the default): a frame's stage 1 as 4 quarter workgroups of 16 one-row-batch segments: they
+// live one load round, as the 8 column tiles beside them do, so all 12 read the frame's lines at the
+// same time and the second read is served by the XCD's L2. C5 PMC 36.7 -> 30.4 B/sample (fetch 23.5
+// -> 17.1), group 1.743 -> 1.696 ms (3 interleaved runs, r4g).
 // XG 2 (tuning): also interleaves the two passes -- XCD x's workgroups take, per group of 17, one
 // frame's 8 pass-B row tiles and then one frame's 9 pass-A items, instead of every pass-B tile of
 // the launch first (the Infinity-Cache reads of pass B beside the HBM reads of pass A all launch
@@ -1050,9 +1043,10 @@ struct FftPlan {
     int vfoCP = 0;                    // fused VFO launches: pass-A input cache policy (SDRGPU_FFT_VFO_CP, tuning)
     int vfoFuse = 1;                  // SDRGPU_FFT_VFO_FUSE=0 (tuning): spectrum and VFO as separate launch groups
     int fuseTail = 1;                 // SDRGPU_FFT_FUSE_TAIL=0 (tuning): the front end's VFO tail as a launch of its own
-    // fft_vfo_kernel's XCD-grouped frames (XG; SDRGPU_FFT_VFO_XCD=0 off, tuning): C5 spectrum + stage-1
-    // group 1.732 -> 1.694 ms, step 1.820 -> 1.782 ms (3 interleaved runs, r4d)
-    int vfoXcd = 1;
+    // fft_vfo_kernel's launch order (SDRGPU_FFT_VFO_XCD, tuning): 0 a frame's 9 workgroups consecutive;
+    // 1 XCD-grouped (group 1.732 -> 1.694 ms, r4d); 2 + passes interleaved (1.684 -> 1.679, noise, r4f);
+    // 3 XCD-grouped with quarter-frame stage-1 workgroups (1.743 -> 1.696 ms, r4g), the default
+    int vfoXcd = 3;
 };
 static int time_mark(FftPlan& p, int which, hipStream_t s) {
     if (!p.timing) return SDRGPU_OK;
@@ -1744,7 +1738,7 @@ static int fft_execute_vfo(FftPlan& p, const float2* x, int frames, float* out, 
     float2* sc[2] = {p.scratch.as<float2>(), p.scratch2.as<float2>()};
     const long long zw = p.N / 32;
     auto zoomAt = [&](long long f0) { return zoom ? zoom + f0 * zw : nullptr; };
-    VfoWork v{st.a, 0, 0, st.M < kRowsMinOutputs ? 1 : 0};
+    VfoWork v{st.a, 0, 0};
     SDRGPU_CHECK(time_mark(p, 0, s));
     SDRGPU_CHECK(dispatch_vfo(p, zoom != nullptr, nullptr, 0, nullptr, nullptr, x, std::min(cf, frames), sc[0], v, s));
     for (int c = 1; c < nchunks; c++) {

@@ -184,12 +184,14 @@ __device__ __forceinline__ bool fir_hist_block(const FirArgs& a) {
 // xor transpose-reduce (ds_swizzle), which leaves output D blk + p in lane p. Each sample is
 // read once (plus QP - 1 halo rows per segment). With QUAD a segment starts one output early
 // (that output only feeds y[m - 1] of the next) and stores RS - 1 outputs.
-// D = 32: segments of 64 or 256 outputs measured the same as 128; forcing 4 waves per SIMD
+// D = 32 (no quadrature) runs 32-output segments at every call size (round 4: the spectrum launches
+// compute the stage in one-load-round workgroups of such segments beside the column tiles, and the
+// separate kernel must cut the same segments to give the same bits; round 1-3 used 128 above 2^19
+// outputs). Earlier: segments of 64 or 256 outputs measured the same as 128; forcing 4 waves per SIMD
 // (128 VGPRs) spills and ran 10% slower; loading batch t + 1 while batch t computes (2 waves per
 // SIMD) was no faster. D = 8 (C3) measured equal to fir_mfma_kernel (0.84 vs 0.85 ms), so it
 // runs only on request (SDRGPU_FIR_ROWS=2).
 constexpr int ROWS_STEP = 512;  // e^{i w D u} table length (>= RS + QP - 1)
-constexpr int kRowsMinOutputs = 1 << 19;   // D = 32: 128-output segments from this many outputs per call
 template <int D> constexpr int rows_rs() { return D == 32 ? 128 : 256; }
 // One D-lane group's segment `seg` (lane = the thread's lane in its wave). BT0: rows per load batch
 // (default: D = 32 keeps 64 rows, 32 KB per wave, in flight at 2 waves per SIMD, 0.6% faster than
