@@ -85,6 +85,10 @@ class C5:
                                 "stage-1 workgroups on one XCD, all one load round, so the stage's read of the IQ is "
                                 "served by that XCD's L2; pass B of the previous chunk)")
             self.fft.set_timing(True)   # the group's own HIP events (the VFO's later stages are outside it)
+            self.roofline_note = ("the group includes the VFO's first stage (8 B/sample of input it shares with "
+                                  "the spectrum); round 3's group was the spectrum alone (1.371 ms) with the "
+                                  "stage as a separate 0.407-ms launch: on today's basis that work was 1.778 ms, "
+                                  "frac 0.233")
         else:
             self.kernel_bytes = (12.0 + 4 / 32) * self.B            # spectrum: 8 B in, 4 B dB + 4/32 B zoom out
             self.kernel_name = ("spectrum N=65536 + zoom to 2048: fft_passA_kernel<256,32> (chunk 0) + "
@@ -583,6 +587,8 @@ def config_result(config, a, world, B, elapsed, kern_ms, wl):
                       "kernel": wl.kernel_name, "kernel_ms": round(kern_ms, 4),
                       "algorithmic_bytes": round(wl.kernel_bytes)},
          "chain_hbm_GBs": round(wl.bytes_per_sample * value * 1e6 / world / 1e9, 1)}
+    if getattr(wl, "roofline_note", None):
+        r["roofline"]["note"] = wl.roofline_note
     if hasattr(wl, "flop_roofline"):
         r["roofline_flops"] = wl.flop_roofline(kern_ms)
     if getattr(wl, "gather_report", None):

@@ -1031,7 +1031,10 @@ struct FftPlan {
     sdrgpu_zoom* zoom = nullptr;      // execute_zoom's unfused zoom (sizes other than N / 32)
     int zoomSize = 0;
     hipStream_t s2 = nullptr;
-    hipEvent_t evFork = nullptr, evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr};
+    hipEvent_t evFork = nullptr, evJoin = nullptr, evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr};
+    // the fused VFO's later stages on the side stream, beside the last pass-B launch (SDRGPU_FFT_VFO_SIDE,
+    // tuning; 0: after it on the call's stream)
+    int vfoSide = 1;
     DevBuf scratch2;
     Fft64Plan* f64 = nullptr;         // sdrgpu_fft_set_precision(h, 1): the fp64-interior kernels (fft64.hip)
     // sdrgpu_fft_set_timing: HIP events around each call's spectrum launch group (the fused VFO
@@ -1048,6 +1051,18 @@ struct FftPlan {
     // 3 XCD-grouped with quarter-frame stage-1 workgroups (1.743 -> 1.696 ms, r4g), the default
     int vfoXcd = 3;
 };
+// the plan's side stream and its events (the two-stream pipeline; the fused VFO's later stages)
+static int ensure_side(FftPlan& p) {
+    if (p.s2) return SDRGPU_OK;
+    SDRGPU_HIP(hipStreamCreateWithFlags(&p.s2, hipStreamNonBlocking));
+    SDRGPU_HIP(hipEventCreateWithFlags(&p.evFork, hipEventDisableTiming));
+    SDRGPU_HIP(hipEventCreateWithFlags(&p.evJoin, hipEventDisableTiming));
+    for (int k = 0; k < 2; k++) {
+        SDRGPU_HIP(hipEventCreateWithFlags(&p.evA[k], hipEventDisableTiming));
+        SDRGPU_HIP(hipEventCreateWithFlags(&p.evB[k], hipEventDisableTiming));
+    }
+    return SDRGPU_OK;
+}
 static int time_mark(FftPlan& p, int which, hipStream_t s) {
     if (!p.timing) return SDRGPU_OK;
     SDRGPU_HIP(hipEventRecord(p.tev[p.tcalls % FftPlan::kTimed][which], s));
@@ -1415,6 +1430,7 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         if (const char* e = tuning_env("SDRGPU_FFT_VFO_CP")) p.vfoCP = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_VFO_FUSE")) p.vfoFuse = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_VFO_XCD")) p.vfoXcd = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_VFO_SIDE")) p.vfoSide = atoi(e);
         if (rc >= 0 && p.N1 == 1024 && p.N2 == 1024) {   // fp64 W_N^(256 j), W_N^j for the 1M pass A
             std::vector<double2> t(512);
             for (int j = 0; j < 256; j++) {
@@ -1538,14 +1554,7 @@ static int fft_execute_body(sdrgpu_fft* h, const void* in, long long frameStride
     }
     const bool pipe = p.pipe && nchunks > 1 && !zoom;
     if (pipe) {
-        if (!p.s2) {
-            SDRGPU_HIP(hipStreamCreateWithFlags(&p.s2, hipStreamNonBlocking));
-            SDRGPU_HIP(hipEventCreateWithFlags(&p.evFork, hipEventDisableTiming));
-            for (int k = 0; k < 2; k++) {
-                SDRGPU_HIP(hipEventCreateWithFlags(&p.evA[k], hipEventDisableTiming));
-                SDRGPU_HIP(hipEventCreateWithFlags(&p.evB[k], hipEventDisableTiming));
-            }
-        }
+        SDRGPU_CHECK(ensure_side(p));
         SDRGPU_CHECK(p.scratch2.ensure(p.scratch.bytes));
         SDRGPU_HIP(hipEventRecord(p.evFork, s));
         SDRGPU_HIP(hipStreamWaitEvent(p.s2, p.evFork, 0));
@@ -1729,8 +1738,11 @@ static bool vfo_fusable(const FftPlan& p, float* zoom, int zoomSize) {
     return p.vfoFuse && !p.f64 && p.N1 == 256 && p.N2 == 256 && p.sa == 32 && p.sb == 32 && p.sa2 == 0 && p.nz == p.N &&
            (zoom == nullptr || zoom_fusable(p, zoomSize));
 }
+// Returns the VFO's output count: its later stages (vfo_stage1_finish) need only the stage-1 outputs,
+// complete once the last pass-A launch is done, so they run on the plan's side stream beside the last
+// launch (pass B of the last chunk + the stage's history), and the call's stream joins them.
 static int fft_execute_vfo(FftPlan& p, const float2* x, int frames, float* out, float* zoom, const VfoStage1& st,
-                           hipStream_t s) {
+                           sdrgpu_block* vfo, void* vfoOut, hipStream_t s) {
     const int cf = p.chunkFrames;
     const int nchunks = (frames + cf - 1) / cf;
     SDRGPU_CHECK(p.scratch.ensure((size_t)std::min(cf, frames) * p.N * sizeof(float2)));
@@ -1747,11 +1759,25 @@ static int fft_execute_vfo(FftPlan& p, const float2* x, int frames, float* out, 
         SDRGPU_CHECK(dispatch_vfo(p, zoom != nullptr, sc[(c - 1) & 1], cf, out + (long long)fB * p.N, zoomAt(fB),
                                   x + (long long)fA * p.N, nfA, sc[c & 1], v, s));
     }
+    int m = 0;
+    if (p.vfoSide) {
+        SDRGPU_CHECK(ensure_side(p));
+        SDRGPU_HIP(hipEventRecord(p.evFork, s));
+        SDRGPU_HIP(hipStreamWaitEvent(p.s2, p.evFork, 0));
+        m = vfo_stage1_finish(vfo, st, vfoOut, p.s2);
+        if (m < 0) return m;
+        SDRGPU_HIP(hipEventRecord(p.evJoin, p.s2));
+    }
     const int fL = (nchunks - 1) * cf;
     v.hist = 1;
     SDRGPU_CHECK(dispatch_vfo(p, zoom != nullptr, sc[(nchunks - 1) & 1], frames - fL, out + (long long)fL * p.N, zoomAt(fL),
                               nullptr, 0, nullptr, v, s));
-    return time_mark(p, 1, s);
+    SDRGPU_CHECK(time_mark(p, 1, s));
+    if (p.vfoSide) {
+        SDRGPU_HIP(hipStreamWaitEvent(s, p.evJoin, 0));
+        return m;
+    }
+    return vfo_stage1_finish(vfo, st, vfoOut, s);
 }
 
 // Spectrum (+ the waterfall's zoom rows) + one RxVFO over the same device batch of back-to-back
@@ -1786,10 +1812,7 @@ extern "C" int sdrgpu_fft_execute_zoom_vfo_dev(sdrgpu_fft* h, const void* in, in
     VfoStage1 st;
     const int fuse = vfo_fusable(p, zoomOut, zoomSize) ? vfo_stage1_prepare(vfo, in, (int)count, &st) : 0;
     if (fuse < 0) return fuse;
-    if (fuse) {
-        SDRGPU_CHECK(fft_execute_vfo(p, (const float2*)in, frames, out, zoomOut, st, s));
-        return vfo_stage1_finish(vfo, st, vfoOut, s);
-    }
+    if (fuse) return fft_execute_vfo(p, (const float2*)in, frames, out, zoomOut, st, vfo, vfoOut, s);
     if (zoomOut && !(zoom_fusable(p, zoomSize) && !p.f64)) {
         SDRGPU_CHECK(fft_execute(h, in, p.N, frames, out, nullptr, s));
         if (!p.zoom || p.zoomSize != zoomSize) {
@@ -1881,6 +1904,7 @@ extern "C" int sdrgpu_fft_destroy(sdrgpu_fft* h) {
         (void)hipStreamSynchronize(h->p.s2);
         (void)hipStreamDestroy(h->p.s2);
         (void)hipEventDestroy(h->p.evFork);
+        (void)hipEventDestroy(h->p.evJoin);
         for (int k = 0; k < 2; k++) {
             (void)hipEventDestroy(h->p.evA[k]);
             (void)hipEventDestroy(h->p.evB[k]);
