@@ -1032,9 +1032,10 @@ struct FftPlan {
     int zoomSize = 0;
     hipStream_t s2 = nullptr;
     hipEvent_t evFork = nullptr, evJoin = nullptr, evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr};
-    // the fused VFO's later stages on the side stream, beside the last pass-B launch (SDRGPU_FFT_VFO_SIDE,
-    // tuning; 0: after it on the call's stream)
-    int vfoSide = 1;
+    // SDRGPU_FFT_VFO_SIDE=1 (tuning): the fused VFO's later stages on the side stream, beside the last
+    // pass-B launch. Measured slower: C5 step 1.725 vs 1.705 ms (3 interleaved runs, r4i; the overlap
+    // stretches the last launch more than it hides), so they run after it on the call's stream
+    int vfoSide = 0;
     DevBuf scratch2;
     Fft64Plan* f64 = nullptr;         // sdrgpu_fft_set_precision(h, 1): the fp64-interior kernels (fft64.hip)
     // sdrgpu_fft_set_timing: HIP events around each call's spectrum launch group (the fused VFO

@@ -34,6 +34,19 @@ __global__ __launch_bounds__(256) void mfma_loop(float* out, float a0, float b0,
     if (threadIdx.x == 0 && blockIdx.x == 0) ticks[0] = t1 - t0;
 }
 
+// operand / result layout probe of v_mfma_f32_4x4x1_16b_f32: D = A x B with A = lane id, B = 1 (which
+// lane's A lands in result register v of lane l), then A = 1, B = lane id
+__global__ void layout_probe(float* out) {
+    const float lane = (float)threadIdx.x;
+    f4 z = {0, 0, 0, 0};
+    const f4 da = __builtin_amdgcn_mfma_f32_4x4x1f32(lane, 1.0f, z, 0, 0, 0);
+    const f4 db = __builtin_amdgcn_mfma_f32_4x4x1f32(1.0f, lane, z, 0, 0, 0);
+    for (int v = 0; v < 4; v++) {
+        out[v * 64 + threadIdx.x] = da[v];
+        out[256 + v * 64 + threadIdx.x] = db[v];
+    }
+}
+
 int main() {
     float* out;
     long long* ticks;
@@ -67,6 +80,16 @@ int main() {
                    cyc_per_instr_per_wave);
         }
     }
-    printf("]}\n");
+    printf("], \"layout\": {");
+    hipLaunchKernelGGL(layout_probe, dim3(1), dim3(64), 0, 0, out);
+    float h[512];
+    hipMemcpy(h, out, sizeof(h), hipMemcpyDeviceToHost);
+    for (int w = 0; w < 2; w++) {
+        printf("%s\"%s\": [", w ? ", " : "", w ? "A1_Blane" : "Alane_B1");
+        for (int v = 0; v < 4; v++)
+            for (int l = 0; l < 64; l++) printf("%s%d", (v || l) ? "," : "", (int)h[w * 256 + v * 64 + l]);
+        printf("]");
+    }
+    printf("}}\n");
     return 0;
 }
