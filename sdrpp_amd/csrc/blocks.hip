@@ -1266,7 +1266,12 @@ struct ChainBlock : Block {
     // (complex data, real taps, no fused xlator / quadrature) -- in one fir_tail_kernel launch.
     // Returns 1 (done, *nout = outputs), 0 (not applicable: the per-kid path runs) or an error.
     static constexpr int kTailMaxIn = 1 << 15;   // first kid's outputs (a reference block: 9,600)
-    int tailMode = -1;                           // SDRGPU_VFO_TAIL (tuning): 0 off
+    // SDRGPU_VFO_TAIL (tuning): 0 off; 1 calls up to kTailMaxIn; 2 every size (big calls: thousands
+    // of tail workgroups, each ~TAIL_PF * TAIL_NT stage-0 samples)
+    int tailMode = -1;
+    // big calls: the workgroup count and image size depend only on (n0, the stages' offsets), which
+    // repeat call after call; the per-workgroup geometry scan is kept for the last key
+    struct TailKey { int n0 = -1; int off[TAIL_MAXS] = {}, H[TAIL_MAXS] = {}, Q[TAIL_MAXS] = {}; int G = 0, maxEl = 0; } tailCache;
     int tailVar = 0;                             // SDRGPU_TAIL_VAR (tuning, timing only): 1 no stage loops, 2 no image loads
     // The tail launch's arguments for kids[1..] on n0 samples of kid 0's output: 1 (t, f, lds
     // filled), 0 (not applicable: the per-kid path runs).
@@ -1278,7 +1283,8 @@ struct ChainBlock : Block {
         }
         const int S = (int)kids.size() - 1;
         if (!tailMode || S < 2 || S > TAIL_MAXS) return 0;
-        if (n0 > kTailMaxIn) return 0;
+        const bool big = n0 > kTailMaxIn;
+        if (big && tailMode < 2) return 0;
         for (int i = 0; i < S; i++) {
             f[i] = dynamic_cast<FirBlock*>(kids[i + 1].get());
             if (!f[i] || f[i]->in_dtype != SDRGPU_C64 || f[i]->ttype != SDRGPU_F32 || f[i]->xl || f[i]->quad ||
@@ -1304,18 +1310,36 @@ struct ChainBlock : Block {
             n = st.M;
         }
         // ~128 last-stage outputs per workgroup, more workgroups while stage 0's image exceeds one
-        // load batch (TAIL_PF per thread)
+        // load batch (TAIL_PF per thread); big calls start from ~512 per workgroup
         int maxEl = 0;
         TailGeom g[TAIL_MAXS];
-        for (t.G = std::min(std::max((n + 127) / 128, 1), 32);; t.G *= 2) {
-            int nel0 = 0;
-            maxEl = 0;
-            for (int w = 0; w < t.G; w++) {
-                maxEl = std::max(maxEl, tail_geometry(t, w, g));
-                nel0 = std::max(nel0, g[0].nel);
+        bool cached = big && tailCache.n0 == n0;
+        for (int i = 0; cached && i < S; i++)
+            cached = tailCache.off[i] == t.st[i].off && tailCache.H[i] == t.st[i].H && tailCache.Q[i] == t.st[i].Q;
+        if (cached) {
+            t.G = tailCache.G;
+            maxEl = tailCache.maxEl;
+        } else {
+            for (t.G = big ? std::max((n + 511) / 512, 1) : std::min(std::max((n + 127) / 128, 1), 32);; t.G *= 2) {
+                int nel0 = 0;
+                maxEl = 0;
+                for (int w = 0; w < t.G; w++) {
+                    maxEl = std::max(maxEl, tail_geometry(t, w, g));
+                    nel0 = std::max(nel0, g[0].nel);
+                }
+                if (nel0 <= TAIL_PF * TAIL_NT) break;
+                if ((!big && t.G >= 64) || t.G >= std::max(n, 1) || t.G >= (1 << 20)) return 0;
             }
-            if (nel0 <= TAIL_PF * TAIL_NT) break;
-            if (t.G >= 64 || t.G >= std::max(n, 1)) return 0;
+            if (big) {
+                tailCache.n0 = n0;
+                for (int i = 0; i < S; i++) {
+                    tailCache.off[i] = t.st[i].off;
+                    tailCache.H[i] = t.st[i].H;
+                    tailCache.Q[i] = t.st[i].Q;
+                }
+                tailCache.G = t.G;
+                tailCache.maxEl = maxEl;
+            }
         }
         t.ldsEl = maxEl;
         int tapF = 0;

@@ -47,7 +47,7 @@ struct TailGeom { int a, b, B, E, RSK, RSP, base, nel; };
 __host__ __device__ inline int tail_geometry(const TailArgs& t, int w, TailGeom* g) {
     const bool last = w == t.G - 1;
     const int Ml = t.st[t.S - 1].M;
-    int lo = Ml * w / t.G, hi = Ml * (w + 1) / t.G;   // Ml * G < 2^31 (host limits)
+    int lo = (int)((long long)Ml * w / t.G), hi = (int)((long long)Ml * (w + 1) / t.G);
 #pragma unroll
     for (int s = TAIL_MAXS - 1; s >= 0; s--) {   // (static indices: g stays in registers)
         if (s >= t.S) continue;

@@ -293,6 +293,39 @@ def test_fir_tail_rxvfo_vs_oracle(rng):
             assert_close_c(yg, yo, 5e-5, "rxvfo 512")
 
 
+def test_fir_tail_big_calls(rng, monkeypatch):
+    """SDRGPU_VFO_TAIL=2: the VFO's later stages as one tail launch at every call size (thousands of
+    workgroups on big calls, the per-(size, offsets) plan cached): against the oracle over ragged big
+    and small calls; the spectrum launches' fused stage 1 + tail bit-identical to the separate path
+    (both run the same tail); a 2^22-sample call's plan reused on the next equal call."""
+    import torch
+    monkeypatch.setenv("SDRGPU_TUNING", "1")
+    monkeypatch.setenv("SDRGPU_VFO_TAIL", "2")
+    fs, off = 61.44e6, 2.5e6
+    g = dsp.RxVFO(fs, 240000, 200000, off)
+    o = oracle.RxVFO(fs, 240000, 200000, off)
+    for n in [1 << 22, 1 << 22, 4099, 3 * 307200 + 17, 1 << 21]:
+        x = iq(rng, n)
+        yo, yg = o.process(x), g.process(x)
+        assert len(yg) == len(yo)
+        if len(yo):
+            assert_close_c(yg, yo, 5e-5, f"rxvfo big tail n={n}")
+    N, frames = 65536, 40
+    fa, fb = dsp.FFTSpectrum(N, N, 6), dsp.FFTSpectrum(N, N, 6)
+    va, vb = dsp.RxVFO(fs, 240000, 200000, off), dsp.RxVFO(fs, 240000, 200000, off)
+    for _ in range(2):
+        x = iq(rng, frames * N)
+        d_x = torch.from_numpy(x.view(np.float32)).cuda()
+        ra, rb = torch.empty(frames * N, device="cuda"), torch.empty(frames * N, device="cuda")
+        oa, ob = torch.empty(2 * (frames * N // 256 + 64), device="cuda"), torch.empty(2 * (frames * N // 256 + 64), device="cuda")
+        ma = fa.execute_vfo_dev(d_x.data_ptr(), frames, ra.data_ptr(), va, oa.data_ptr())
+        fb.execute_dev(d_x.data_ptr(), N, frames, rb.data_ptr())
+        mb = vb.process_dev(d_x.data_ptr(), frames * N, ob.data_ptr())
+        torch.cuda.synchronize()
+        assert ma == mb
+        assert torch.equal(oa[:2 * ma], ob[:2 * mb])
+
+
 def _quad_bound(y_ref, y_prev0, e_fir, inv_dev):
     """Per-sample bound on the quadrature output (quadrature.h:41-56) of an FIR output stream
     known to within e_fir (absolute) of y_ref: an error e in y_i turns arg(y_i) by at most
