@@ -1269,6 +1269,7 @@ struct ChainBlock : Block {
     // SDRGPU_VFO_TAIL (tuning): 0 off; 1 calls up to kTailMaxIn; 2 every size (big calls: thousands
     // of tail workgroups, each ~TAIL_PF * TAIL_NT stage-0 samples)
     int tailMode = -1;
+    int tailBigOut = 512;   // big calls: last-stage outputs per workgroup to start from (SDRGPU_TAIL_OUT, tuning)
     // big calls: the workgroup count and image size depend only on (n0, the stages' offsets), which
     // repeat call after call; the per-workgroup geometry scan is kept for the last key
     struct TailKey { int n0 = -1; int off[TAIL_MAXS] = {}, H[TAIL_MAXS] = {}, Q[TAIL_MAXS] = {}; int G = 0, maxEl = 0; } tailCache;
@@ -1280,6 +1281,7 @@ struct ChainBlock : Block {
             const char* e = tuning_env("SDRGPU_VFO_TAIL");
             tailMode = e ? atoi(e) : 1;
             if (const char* v = tuning_env("SDRGPU_TAIL_VAR")) tailVar = atoi(v);
+            if (const char* v = tuning_env("SDRGPU_TAIL_OUT")) tailBigOut = std::max(8, atoi(v));
         }
         const int S = (int)kids.size() - 1;
         if (!tailMode || S < 2 || S > TAIL_MAXS) return 0;
@@ -1320,7 +1322,7 @@ struct ChainBlock : Block {
             t.G = tailCache.G;
             maxEl = tailCache.maxEl;
         } else {
-            for (t.G = big ? std::max((n + 511) / 512, 1) : std::min(std::max((n + 127) / 128, 1), 32);; t.G *= 2) {
+            for (t.G = big ? std::max((n + tailBigOut - 1) / tailBigOut, 1) : std::min(std::max((n + 127) / 128, 1), 32);; t.G *= 2) {
                 int nel0 = 0;
                 maxEl = 0;
                 for (int w = 0; w < t.G; w++) {
