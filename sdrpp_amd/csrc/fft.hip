@@ -1724,8 +1724,13 @@ static int launch_vfo(FftPlan& p, const float2* scratchB, int framesB, float* ou
 }
 static int dispatch_vfo(FftPlan& p, bool zm, const float2* scratchB, int framesB, float* outB, float* zoomB,
                         const float2* in, int framesA, float2* scratchA, const VfoWork& v, hipStream_t s) {
-    if (p.vfoXcd == 3) return zm ? launch_vfo<true, 0, 3>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
-                                 : launch_vfo<false, 0, 3>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
+    if (p.vfoXcd == 3) {
+        if (p.vfoCP == 2)   // (tuning) streaming pass-A input loads: the stage's L2 hits, no Infinity-Cache allocation
+            return zm ? launch_vfo<true, 2, 3>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
+                      : launch_vfo<false, 2, 3>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
+        return zm ? launch_vfo<true, 0, 3>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
+                  : launch_vfo<false, 0, 3>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
+    }
     if (p.vfoXcd == 2) return zm ? launch_vfo<true, 0, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
                                  : launch_vfo<false, 0, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
     if (p.vfoXcd) return zm ? launch_vfo<true, 0, 1>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)

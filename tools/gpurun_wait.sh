@@ -7,7 +7,7 @@ LOG=$1; TO=$2; shift 2
 for i in $(seq 1 30); do
   /usr/local/graft/bin/gpurun --timeout "$TO" -- "$@" > "$LOG" 2>&1
   rc=$?
-  if grep -q 'nothing was charged' "$LOG" && ! grep -q 'status=ok' "$LOG"; then
+  if grep -qE 'nothing was charged|status=transient' "$LOG" && ! grep -q 'status=ok' "$LOG"; then
     sleep 120
     continue
   fi
