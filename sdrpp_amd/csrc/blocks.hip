@@ -1266,8 +1266,10 @@ struct ChainBlock : Block {
     // (complex data, real taps, no fused xlator / quadrature) -- in one fir_tail_kernel launch.
     // Returns 1 (done, *nout = outputs), 0 (not applicable: the per-kid path runs) or an error.
     static constexpr int kTailMaxIn = 1 << 15;   // first kid's outputs (a reference block: 9,600)
-    // SDRGPU_VFO_TAIL (tuning): 0 off; 1 calls up to kTailMaxIn; 2 every size (big calls: thousands
-    // of tail workgroups, each ~TAIL_PF * TAIL_NT stage-0 samples)
+    // SDRGPU_VFO_TAIL (tuning): 0 off; 1 calls up to kTailMaxIn; 2 (default) every size (big calls:
+    // thousands of tail workgroups, each ~TAIL_PF * TAIL_NT stage-0 samples: the C5 step's three
+    // later-stage launches become one, 1.760 -> 1.747 ms, 3 interleaved runs, r4j; 512 last-stage
+    // outputs per workgroup to start from measured best of 32 / 64 / 128 / 512, r4l)
     int tailMode = -1;
     int tailBigOut = 512;   // big calls: last-stage outputs per workgroup to start from (SDRGPU_TAIL_OUT, tuning)
     // big calls: the workgroup count and image size depend only on (n0, the stages' offsets), which
@@ -1279,7 +1281,7 @@ struct ChainBlock : Block {
     int tail_plan(int n0, TailArgs& t, FirBlock** f, size_t& lds) {
         if (tailMode < 0) {
             const char* e = tuning_env("SDRGPU_VFO_TAIL");
-            tailMode = e ? atoi(e) : 1;
+            tailMode = e ? atoi(e) : 2;
             if (const char* v = tuning_env("SDRGPU_TAIL_VAR")) tailVar = atoi(v);
             if (const char* v = tuning_env("SDRGPU_TAIL_OUT")) tailBigOut = std::max(8, atoi(v));
         }

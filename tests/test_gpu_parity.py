@@ -281,7 +281,7 @@ def test_fir_tail_bit_identical_to_stage_launches(kind, args, monkeypatch, rng):
 
 
 def test_fir_tail_rxvfo_vs_oracle(rng):
-    """The default RxVFO path at the reference block size (tail on, MFMA stage 2 on big calls)
+    """The default RxVFO path at the reference block size (one tail launch at every size)
     against the oracle, ragged calls switching between the tail and the per-stage path."""
     g = dsp.RxVFO(61.44e6, 120000, 90000, 7e5)
     o = oracle.RxVFO(61.44e6, 120000, 90000, 7e5)
@@ -294,7 +294,7 @@ def test_fir_tail_rxvfo_vs_oracle(rng):
 
 
 def test_fir_tail_big_calls(rng, monkeypatch):
-    """SDRGPU_VFO_TAIL=2: the VFO's later stages as one tail launch at every call size (thousands of
+    """SDRGPU_VFO_TAIL=2 (the default): the VFO's later stages as one tail launch at every call size (thousands of
     workgroups on big calls, the per-(size, offsets) plan cached): against the oracle over ragged big
     and small calls; the spectrum launches' fused stage 1 + tail bit-identical to the separate path
     (both run the same tail); a 2^22-sample call's plan reused on the next equal call."""
