@@ -114,6 +114,10 @@ int sdrgpu_fft_execute_zoom_vfo_dev(sdrgpu_fft* h, const void* in, int frames, f
  * min(n, calls, 256) group times in ms, oldest first, waiting for them */
 int sdrgpu_fft_set_timing(sdrgpu_fft* h, int on);
 int sdrgpu_fft_group_times(sdrgpu_fft* h, float* ms, int n);
+/* Diagnostics of the persistent spectrum + VFO launch (tuning SDRGPU_FFT_VFO_PERSIST): the number
+ * of bounded dependency waits that timed out in the last call of `frames` frames (0 = every
+ * dependency was met). Synchronises the device. */
+int sdrgpu_fft_persist_errors(sdrgpu_fft* h, int frames);
 /* drop-in for IQFrontEnd::handler: in = host complex_t[nz]; out = host float[N] or NULL
  * (acquireFFTBuffer may return NULL; the spectrum is then computed but not written). */
 int sdrgpu_fft_logmag(sdrgpu_fft* h, const void* in, float* out);

@@ -69,6 +69,7 @@ def _load():
         "sdrgpu_fft_execute_zoom_vfo_dev": (i, [vp, vp, i, vp, vp, i, vp, vp, vp]),
         "sdrgpu_fft_set_timing": (i, [vp, i]),
         "sdrgpu_fft_group_times": (i, [vp, fp, i]),
+        "sdrgpu_fft_persist_errors": (i, [vp, i]),
         "sdrgpu_fft_execute_zoom_dev": (i, [vp, vp, ll, i, vp, vp, i, vp]),
         "sdrgpu_fft_logmag": (i, [vp, vp, vp]),
         "sdrgpu_fft_size": (i, [vp]),

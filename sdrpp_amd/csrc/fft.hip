@@ -940,6 +940,107 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     else passA_tile<256, 32, CP>(lds, g * 8 + r, in, frameStride, framesA, win, nz, 256, logN, tw1, tfull, scratchA);
 }
 
+// ---- the C5 launch group as ONE persistent launch with per-frame dataflow (round 4, tuning:
+// SDRGPU_FFT_VFO_PERSIST). Each workgroup reads its XCD id (HW_REG_XCC_ID) and takes items from that
+// XCD's queue: frame f = 8 j + x belongs to XCD x; its 12 first-pass items (4 stage-1 quarters, 8
+// column tiles) come at queue step j and its 8 pass-B row tiles at step j + lag, so pass B of a frame
+// runs on the XCD that wrote its intermediate, a few frames later, from that XCD's L2 / the Infinity
+// Cache -- no launch boundaries, no chunk drains, and the intermediate's working set is ~lag frames
+// per XCD instead of a 128-MB chunk. The intermediate lives in a ring of R frame slots per XCD.
+// Dependencies (same XCD, so one L2 is the coherence point; the producer drains its stores before
+// counting, the consumer drops its L1 before reading):
+//   pass-B tile of f   waits for the 8 column tiles of f   (aDone[f] == 8)
+//   column tile of f   waits for the 8 pass-B tiles of f - 8 R, the slot's previous user (bDone == 8)
+// Every wait points at an item dequeued earlier by a running workgroup, so there is no deadlock for
+// any residency; every spin is bounded (on timeout the kernel raises err[0] and goes on).
+constexpr int kPersistRing = 32;   // slots per XCD
+struct PersistWork {
+    VfoWork v;
+    int frames, lag;
+    int* q;          // [8] per-XCD item counters (zeroed per call)
+    int* aDone;      // [frames]
+    int* bDone;      // [frames]
+    int* err;        // [1] spin timeouts
+};
+__device__ __forceinline__ bool persist_wait(const int* c, int target, int* err) {
+    for (int k = 0; k < (1 << 22); k++) {
+        if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+}
+// (the item bodies as separate functions: inlined into one loop their registers add up and the
+// kernel spilled 37 VGPRs at the 128-VGPR budget)
+__device__ __attribute__((noinline)) void persist_quarter(const VfoWork& v, int f, int q) { vfo_quarter_block(v, f, q); }
+__device__ __attribute__((noinline)) void persist_tile_a(float2* lds, int r, const float2* x, long long N, const float* win,
+                                                         int nz, int logN, const float2* tw1, const float2* tfull, float2* slot) {
+    passA_tile<256, 32, 0>(lds, r, x, N, 1, win, nz, 256, logN, tw1, tfull, slot);
+}
+template <bool ZM>
+__device__ __attribute__((noinline)) void persist_tile_b(float2* lds, int r, const float2* slot, int logN, const float2* tw2,
+                                                         float* o, float* z) {
+    passB_tile<256, 32, ZM>(lds, r, slot, 1, 256, logN, tw2, o, z);
+}
+template <bool ZM>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fft_vfo_persist_kernel(
+    const float2* __restrict__ in, float* __restrict__ out, float* __restrict__ zoom, const float* __restrict__ win, int nz,
+    int logN, const float2* __restrict__ tw1, const float2* __restrict__ tw2, const float2* __restrict__ tfull,
+    float2* __restrict__ ring, PersistWork w) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    __shared__ int item;
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0) (void)fir_hist_copy<float2, true, false>(w.v.a);   // the stage's history carry (fir.h:80)
+    const int x = (int)(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7);   // HW_REG_XCC_ID[2:0]
+    const int J = (w.frames - x + 7) / 8;   // this XCD's frames: f = 8 j + x, j < J
+    const int L = w.lag;
+    const int a = J < L ? J : L, b = J < L ? L : J, c2 = J < L ? 0 : 20;
+    const int total = 20 * J;
+    const long long N = 1LL << logN;
+    for (;;) {
+        __syncthreads();   // (the previous item's last LDS reads and its use of `item` are done)
+        if (tid == 0) item = __hip_atomic_fetch_add(&w.q[x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        int i = item;
+        if (i >= total) break;
+        int st, k;   // queue step, item within it: k < 12 first pass (0-3 quarters, 4-11 tiles), k >= 12 pass B
+        if (i < 12 * a) {
+            st = i / 12; k = i % 12;
+        } else if ((i -= 12 * a) < c2 * (b - a)) {
+            st = a + i / c2; k = i % c2;
+        } else {
+            i -= c2 * (b - a);
+            st = b + i / 8; k = 12 + i % 8;
+        }
+        if (k < 12) {
+            const int j = st, f = 8 * j + x;
+            if (k < 4) {
+                persist_quarter(w.v, f, k);
+                continue;
+            }
+            float2* slot = ring + (long long)(x * kPersistRing + j % kPersistRing) * N;
+            if (j >= kPersistRing) {   // the slot's previous frame must be out of pass B
+                if (tid == 0) (void)persist_wait(&w.bDone[f - 8 * kPersistRing], 8, w.err);
+                __syncthreads();
+            }
+            persist_tile_a(lds, k - 4, in + (long long)f * N, N, win, nz, logN, tw1, tfull, slot);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's intermediate stores are in L2
+            __syncthreads();
+            if (tid == 0) __hip_atomic_fetch_add(&w.aDone[f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const int j = st - L, f = 8 * j + x;
+            const float2* slot = ring + (long long)(x * kPersistRing + j % kPersistRing) * N;
+            if (tid == 0) (void)persist_wait(&w.aDone[f], 8, w.err);
+            __syncthreads();
+            asm volatile("buffer_inv sc0" ::: "memory");   // no stale L1 lines of the slot's previous frame
+            persist_tile_b<ZM>(lds, k - 12, slot, logN, tw2, out + (long long)f * N, ZM ? zoom + (long long)f * (N / 32) : nullptr);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (its slot reads are done before the slot is freed)
+            __syncthreads();
+            if (tid == 0) __hip_atomic_fetch_add(&w.bDone[f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // ---- the front end's per-block launch: pass A (frame straddling two pushes read in place) + the
 // VFO's first stage + its history carry + the tail copy, one launch (sdrgpu_frontend_*): the block is
 // small (a reference-size block has ~5 frames and 9,600 stage-1 outputs), so the stage's segments
@@ -1036,6 +1137,10 @@ struct FftPlan {
     // pass-B launch. Measured slower: C5 step 1.725 vs 1.705 ms (3 interleaved runs, r4i; the overlap
     // stretches the last launch more than it hides), so they run after it on the call's stream
     int vfoSide = 0;
+    int vfoPersist = 0;   // SDRGPU_FFT_VFO_PERSIST (tuning): the group as one persistent dataflow launch
+    int persistLag = 6;   // SDRGPU_FFT_PERSIST_LAG (tuning): queue steps between a frame's two passes
+    DevBuf persistCtl;    // its counters: q[8], aDone[frames], bDone[frames], err
+    int gridP = 0;
     DevBuf scratch2;
     Fft64Plan* f64 = nullptr;         // sdrgpu_fft_set_precision(h, 1): the fp64-interior kernels (fft64.hip)
     // sdrgpu_fft_set_timing: HIP events around each call's spectrum launch group (the fused VFO
@@ -1432,6 +1537,8 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         if (const char* e = tuning_env("SDRGPU_FFT_VFO_FUSE")) p.vfoFuse = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_VFO_XCD")) p.vfoXcd = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_VFO_SIDE")) p.vfoSide = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_VFO_PERSIST")) p.vfoPersist = atoi(e);
+        if (const char* e = tuning_env("SDRGPU_FFT_PERSIST_LAG")) p.persistLag = std::max(1, atoi(e));
         if (rc >= 0 && p.N1 == 1024 && p.N2 == 1024) {   // fp64 W_N^(256 j), W_N^j for the 1M pass A
             std::vector<double2> t(512);
             for (int j = 0; j < 256; j++) {
@@ -1747,8 +1854,49 @@ static bool vfo_fusable(const FftPlan& p, float* zoom, int zoomSize) {
 // Returns the VFO's output count: its later stages (vfo_stage1_finish) need only the stage-1 outputs,
 // complete once the last pass-A launch is done, so they run on the plan's side stream beside the last
 // launch (pass B of the last chunk + the stage's history), and the call's stream joins them.
+// the group as one fft_vfo_persist_kernel launch (SPX devices: 8 XCDs, read by HW_REG_XCC_ID)
+static int fft_execute_vfo_persist(FftPlan& p, const float2* x, int frames, float* out, float* zoom, const VfoStage1& st,
+                                   hipStream_t s) {
+    SDRGPU_CHECK(p.scratch.ensure((size_t)8 * kPersistRing * p.N * sizeof(float2)));
+    const size_t ctl = sizeof(int) * (8 + 2 * (size_t)frames + 1);
+    SDRGPU_CHECK(p.persistCtl.ensure(ctl));
+    int* c = p.persistCtl.as<int>();
+    SDRGPU_HIP(hipMemsetAsync(c, 0, ctl, s));
+    PersistWork w{VfoWork{st.a, 0, 0}, frames, p.persistLag, c, c + 8, c + 8 + frames, c + 8 + 2 * frames};
+    auto k = zoom ? fft_vfo_persist_kernel<true> : fft_vfo_persist_kernel<false>;
+    const size_t lds = sizeof(float2) * (32 * Lds<256>::LS + 256 + 256);
+    SDRGPU_CHECK(set_lds(k, lds));
+    if (!p.gridP) {
+        int per = 0, cus = 0;
+        SDRGPU_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k, 512, lds));
+        SDRGPU_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p.device));
+        p.gridP = std::max(1, std::min(per, 2)) * cus;
+    }
+    SDRGPU_CHECK(time_mark(p, 0, s));
+    hipLaunchKernelGGL(k, dim3(p.gridP), dim3(512), lds, s, x, out, zoom, p.win.as<float>(), p.nz, p.logN,
+                       p.tw1.as<float2>(), p.tw2.as<float2>(), p.tfull.as<float2>(), p.scratch.as<float2>(), w);
+    SDRGPU_HIP(hipGetLastError());
+    return time_mark(p, 1, s);
+}
+// spin timeouts of the last persistent launch (synchronises the plan's stream; tests)
+extern "C" int sdrgpu_fft_persist_errors(sdrgpu_fft* h, int frames) {
+    if (!h || !h->p.persistCtl.p) return 0;
+    int e = 0;
+    SDRGPU_HIP(hipDeviceSynchronize());
+    SDRGPU_HIP(hipMemcpy(&e, h->p.persistCtl.as<int>() + 8 + 2 * frames, sizeof(int), hipMemcpyDeviceToHost));
+    return e;
+}
+
 static int fft_execute_vfo(FftPlan& p, const float2* x, int frames, float* out, float* zoom, const VfoStage1& st,
                            sdrgpu_block* vfo, void* vfoOut, hipStream_t s) {
+    if (p.vfoPersist) {
+        int cus = 0;
+        SDRGPU_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p.device));
+        if (cus == 256) {
+            SDRGPU_CHECK(fft_execute_vfo_persist(p, x, frames, out, zoom, st, s));
+            return vfo_stage1_finish(vfo, st, vfoOut, s);
+        }
+    }
     const int cf = p.chunkFrames;
     const int nchunks = (frames + cf - 1) / cf;
     SDRGPU_CHECK(p.scratch.ensure((size_t)std::min(cf, frames) * p.N * sizeof(float2)));

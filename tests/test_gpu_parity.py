@@ -992,6 +992,18 @@ def test_spectrum_vfo_fused_xcd(frames_list, pre, chunk_mb, mode, rng, monkeypat
     _fused_vs_separate(frames_list, pre, rng, zoom=True)
 
 
+@pytest.mark.parametrize("frames_list,pre", [([13], 0), ([9, 4], 1001), ([300], 77)])
+def test_spectrum_vfo_persistent(frames_list, pre, rng, monkeypatch):
+    """The C5 group as one persistent dataflow launch (SDRGPU_FFT_VFO_PERSIST: per-XCD queues, pass B of
+    a frame after its 8 column tiles, a 32-slot intermediate ring per XCD, reused past 8 x 32 frames at
+    300 frames): rows, zoom rows and VFO output bit-identical to the separate launches (a dependency
+    wait that timed out would leave stale intermediate rows: the bit-identity catches it)."""
+    monkeypatch.setenv("SDRGPU_TUNING", "1")
+    monkeypatch.setenv("SDRGPU_FFT_VFO_PERSIST", "1")
+    monkeypatch.setenv("SDRGPU_FFT_PERSIST_LAG", "2")
+    _fused_vs_separate(frames_list, pre, rng, zoom=True)
+
+
 # ------------------------------------------------- waterfall zoom fused into the spectrum
 @pytest.mark.parametrize("frames,chunk_mb,zsize", [(3, None, 2048), (9, 1, 2048), (4, None, 1800), (5, 1, 4096)])
 def test_spectrum_zoom_rows(frames, chunk_mb, zsize, rng, monkeypatch):
