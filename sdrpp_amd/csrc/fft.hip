@@ -997,9 +997,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     const int a = J < L ? J : L, b = J < L ? L : J, c2 = J < L ? 0 : 20;
     const int total = 20 * J;
     const long long N = 1LL << logN;
+    // the next item's index is drawn while the current one runs (an atomic round trip per item would
+    // otherwise serialise with the work)
+    int nxt = 0;
+    if (tid == 0) nxt = __hip_atomic_fetch_add(&w.q[x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (;;) {
         __syncthreads();   // (the previous item's last LDS reads and its use of `item` are done)
-        if (tid == 0) item = __hip_atomic_fetch_add(&w.q[x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) {
+            item = nxt;
+            if (nxt < total) nxt = __hip_atomic_fetch_add(&w.q[x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         __syncthreads();
         int i = item;
         if (i >= total) break;
