@@ -982,7 +982,7 @@ __device__ __attribute__((noinline)) void persist_tile_b(float2* lds, int r, con
                                                          float* o, float* z) {
     passB_tile<256, 32, ZM>(lds, r, slot, 1, 256, logN, tw2, o, z);
 }
-template <bool ZM>
+template <bool ZM, bool INL = false>   // INL (tuning): the item bodies inlined (spills 37 VGPRs)
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fft_vfo_persist_kernel(
     const float2* __restrict__ in, float* __restrict__ out, float* __restrict__ zoom, const float* __restrict__ win, int nz,
     int logN, const float2* __restrict__ tw1, const float2* __restrict__ tw2, const float2* __restrict__ tfull,
@@ -1022,7 +1022,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
         if (k < 12) {
             const int j = st, f = 8 * j + x;
             if (k < 4) {
-                persist_quarter(w.v, f, k);
+                if constexpr (INL) vfo_quarter_block(w.v, f, k);
+                else persist_quarter(w.v, f, k);
                 continue;
             }
             float2* slot = ring + (long long)(x * kPersistRing + j % kPersistRing) * N;
@@ -1030,7 +1031,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
                 if (tid == 0) (void)persist_wait(&w.bDone[f - 8 * kPersistRing], 8, w.err);
                 __syncthreads();
             }
-            persist_tile_a(lds, k - 4, in + (long long)f * N, N, win, nz, logN, tw1, tfull, slot);
+            if constexpr (INL) passA_tile<256, 32, 0>(lds, k - 4, in + (long long)f * N, N, 1, win, nz, 256, logN, tw1, tfull, slot);
+            else persist_tile_a(lds, k - 4, in + (long long)f * N, N, win, nz, logN, tw1, tfull, slot);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's intermediate stores are in L2
             __syncthreads();
             if (tid == 0) __hip_atomic_fetch_add(&w.aDone[f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1040,7 +1042,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
             if (tid == 0) (void)persist_wait(&w.aDone[f], 8, w.err);
             __syncthreads();
             asm volatile("buffer_inv sc0" ::: "memory");   // no stale L1 lines of the slot's previous frame
-            persist_tile_b<ZM>(lds, k - 12, slot, logN, tw2, out + (long long)f * N, ZM ? zoom + (long long)f * (N / 32) : nullptr);
+            if constexpr (INL)
+                passB_tile<256, 32, ZM>(lds, k - 12, slot, 1, 256, logN, tw2, out + (long long)f * N,
+                                        ZM ? zoom + (long long)f * (N / 32) : nullptr);
+            else persist_tile_b<ZM>(lds, k - 12, slot, logN, tw2, out + (long long)f * N, ZM ? zoom + (long long)f * (N / 32) : nullptr);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (its slot reads are done before the slot is freed)
             __syncthreads();
             if (tid == 0) __hip_atomic_fetch_add(&w.bDone[f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1870,7 +1875,8 @@ static int fft_execute_vfo_persist(FftPlan& p, const float2* x, int frames, floa
     int* c = p.persistCtl.as<int>();
     SDRGPU_HIP(hipMemsetAsync(c, 0, ctl, s));
     PersistWork w{VfoWork{st.a, 0, 0}, frames, p.persistLag, c, c + 8, c + 8 + frames, c + 8 + 2 * frames};
-    auto k = zoom ? fft_vfo_persist_kernel<true> : fft_vfo_persist_kernel<false>;
+    auto k = p.vfoPersist == 2 ? (zoom ? fft_vfo_persist_kernel<true, true> : fft_vfo_persist_kernel<false, true>)
+                               : (zoom ? fft_vfo_persist_kernel<true> : fft_vfo_persist_kernel<false>);
     const size_t lds = sizeof(float2) * (32 * Lds<256>::LS + 256 + 256);
     SDRGPU_CHECK(set_lds(k, lds));
     if (!p.gridP) {
