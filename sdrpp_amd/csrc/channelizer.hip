@@ -95,7 +95,7 @@ __global__ __launch_bounds__(L) void chan_kernel(const float2* __restrict__ hist
         __syncthreads();
         float2 v[16];
 #pragma unroll
-        for (int i = 0; i < 16; i++) v[i] = lds[sF * LS + pad16(tF + i * T)];
+        for (int i = 0; i < 16; i++) v[i] = lds[sF * LS + pad16s<T>(tF, i)];
         __syncthreads();
         stage_first<L>(lds + sF * LS, v, tF);
         __syncthreads();
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(L / 2) void chan2_kernel(const float2* __restrict__
             const int sF = tid / T + 8 * half, tF = tid % T;
             float2 v[16];
 #pragma unroll
-            for (int i = 0; i < 16; i++) v[i] = lds[sF * LS + pad16(tF + i * T)];
+            for (int i = 0; i < 16; i++) v[i] = lds[sF * LS + pad16s<T>(tF, i)];
             __syncthreads();
             stage_first<L>(lds + sF * LS, v, tF);
             __syncthreads();

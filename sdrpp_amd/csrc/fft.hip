@@ -206,7 +206,7 @@ __device__ __forceinline__ void passA_tile(
         stage_first<L>(seq, v, t);
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < 16; r++) v[r] = seq[pad16(t + 16 * r)];
+        for (int r = 0; r < 16; r++) v[r] = seq[pad16s<16>(t, r)];
 #pragma unroll
         for (int r = 1; r < 16; r++) v[r] = cmul(v[r], tw16[16 * r + t]);
         dft16(v);
@@ -281,7 +281,7 @@ __device__ __forceinline__ void stage_lds_v(float2* seq0, const float2* twl, int
         for (int b = 0; b < BPT; b++) {
             const int j = t + b * T, jm = j % NS;
 #pragma unroll
-            for (int r = 0; r < R; r++) v[q][b][r] = seq0[q * LS + pad16(j + r * (L / R))];
+            for (int r = 0; r < R; r++) v[q][b][r] = seq0[q * LS + pad16s<L / R>(j, r)];
             if constexpr (T16 && R == 16 && NS == 16) {   // conflict-free layout (stage_lds, fft_stages.h)
 #pragma unroll
                 for (int r = 1; r < R; r++) v[q][b][r] = cmul(v[q][b][r], tw16[16 * r + jm]);
@@ -298,7 +298,7 @@ __device__ __forceinline__ void stage_lds_v(float2* seq0, const float2* twl, int
         for (int b = 0; b < BPT; b++) {
             const int j = t + b * T, idxD = (j / NS) * NS * R + (j % NS);
 #pragma unroll
-            for (int r = 0; r < R; r++) seq0[q * LS + pad16(idxD + r * NS)] = v[q][b][r];
+            for (int r = 0; r < R; r++) seq0[q * LS + pad16s<NS>(idxD, r)] = v[q][b][r];
         }
     __syncthreads();
 }
@@ -313,7 +313,7 @@ __device__ __forceinline__ void stage_last_v(const float2* seq0, const float2* t
         for (int b = 0; b < BPT; b++) {
             const int j = t + b * T, jm = j % NS;
 #pragma unroll
-            for (int r = 0; r < R; r++) v[q][b][r] = seq0[q * LS + pad16(j + r * (L / R))];
+            for (int r = 0; r < R; r++) v[q][b][r] = seq0[q * LS + pad16s<L / R>(j, r)];
 #pragma unroll
             for (int r = 1; r < R; r++) v[q][b][r] = cmul(v[q][b][r], twl[r * jm * (L / (NS * R))]);
             dft<R>(v[q][b]);
@@ -390,8 +390,8 @@ __device__ __forceinline__ void passA2_tile(
     float2* seq0 = lds + 2 * cp * LS;
 #pragma unroll
     for (int r = 0; r < 16; r++) {
-        seq0[pad16(t * 16 + r)] = v0[r];
-        seq0[LS + pad16(t * 16 + r)] = v1[r];
+        seq0[pad16lo(t, r)] = v0[r];
+        seq0[LS + pad16lo(t, r)] = v1[r];
     }
     __syncthreads();
     float2* dst = scratch + (f << logN);
@@ -446,7 +446,7 @@ __device__ __forceinline__ void mid16_read(const float2* seq, const float2* tw16
     constexpr int L = 1024;
     const int jm = t % 16;
 #pragma unroll
-    for (int r = 0; r < 16; r++) v[r] = seq[pad16(t + r * (L / 16))];
+    for (int r = 0; r < 16; r++) v[r] = seq[pad16s<L / 16>(t, r)];
 #pragma unroll
     for (int r = 1; r < 16; r++) v[r] = cmul(v[r], tw16[16 * r + jm]);   // (stage_lds's tw16 layout)
     dft16(v);
@@ -454,7 +454,7 @@ __device__ __forceinline__ void mid16_read(const float2* seq, const float2* tw16
 __device__ __forceinline__ void mid16_write(float2* seq, int t, const float2 (&v)[16]) {
     const int idxD = (t / 16) * 256 + (t % 16);
 #pragma unroll
-    for (int r = 0; r < 16; r++) seq[pad16(idxD + r * 16)] = v[r];
+    for (int r = 0; r < 16; r++) seq[pad16s<16>(idxD, r)] = v[r];
 }
 
 // tile -> (frame, block) of the persistent 1M passes. G (the grid, a multiple of 8 G8 and of 8) > 1
@@ -634,8 +634,8 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_
         __syncthreads();   // the previous tile's last LDS reads are done (and twl is staged)
 #pragma unroll
         for (int r = 0; r < 16; r++) {
-            seq0[pad16(t2 * 16 + r)] = v0[r];
-            seq0[LS + pad16(t2 * 16 + r)] = v1[r];
+            seq0[pad16lo(t2, r)] = v0[r];
+            seq0[LS + pad16lo(t2, r)] = v1[r];
         }
         __syncthreads();
         // middle stage (radix 16, NS = 16). MIDCOL: one column at a time, 16 values live instead
@@ -682,7 +682,7 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_
                     const int j = t2 + b4 * T;
                     float2 u[4];
 #pragma unroll
-                    for (int r = 0; r < 4; r++) u[r] = seq0[qq * LS + pad16(j + r * (L / 4))];
+                    for (int r = 0; r < 4; r++) u[r] = seq0[qq * LS + pad16s<L / 4>(j, r)];
 #pragma unroll
                     for (int r = 1; r < 4; r++) u[r] = cmul(u[r], twl[r * j]);
                     dft4v(u);

@@ -116,6 +116,25 @@ template <> __device__ __forceinline__ void dft<8>(float2* v) { dft8(v); }
 template <> __device__ __forceinline__ void dft<16>(float2* v) { dft16(v); }
 
 __device__ __forceinline__ int pad16(int i) { return i + (i >> 4); }
+// pad16(j + r S) for j >= 0: when S is a multiple of 16 the image moves by r (S + S / 16), a constant
+// the unrolled loop folds into the LDS instruction's offset. (Written as pad16(j + r S) the compiler
+// recomputed the shift per element: ~4 VALU per LDS access in the 1M pass A.)
+// (SDRGPU_PAD16_PLAIN: the round-3 per-element form, an A/B build)
+template <int S>
+__device__ __forceinline__ int pad16s(int j, int r) {
+#ifndef SDRGPU_PAD16_PLAIN
+    if constexpr (S % 16 == 0) return pad16(j) + r * (S + S / 16);
+#endif
+    return pad16(j + r * S);
+}
+// pad16(16 t + r) for r < 16: 17 t + r
+__device__ __forceinline__ int pad16lo(int t, int r) {
+#ifndef SDRGPU_PAD16_PLAIN
+    return 17 * t + r;
+#else
+    return pad16(t * 16 + r);
+#endif
+}
 template <int L> struct Lds { static constexpr int LS = L + L / 16 + 1; };   // sequence stride (odd)
 
 // tw16[16 r + jm] = tw[r jm (L / 256)] (r, jm < 16) for the T16 stages below; the caller's next
@@ -141,7 +160,7 @@ __device__ __forceinline__ void stage_lds(float2* seq, const float2* __restrict_
     for (int b = 0; b < BPT; b++) {
         const int j = t + b * T;
 #pragma unroll
-        for (int r = 0; r < R; r++) v[b][r] = seq[pad16(j + r * (L / R))];
+        for (int r = 0; r < R; r++) v[b][r] = seq[pad16s<L / R>(j, r)];
         const int jm = j % NS;
         if constexpr (T16 && R == 16 && NS == 16) {
 #pragma unroll
@@ -158,7 +177,7 @@ __device__ __forceinline__ void stage_lds(float2* seq, const float2* __restrict_
         const int j = t + b * T;
         const int idxD = (j / NS) * NS * R + (j % NS);
 #pragma unroll
-        for (int r = 0; r < R; r++) seq[pad16(idxD + r * NS)] = v[b][r];
+        for (int r = 0; r < R; r++) seq[pad16s<NS>(idxD, r)] = v[b][r];
     }
     __syncthreads();
 }
@@ -174,7 +193,7 @@ __device__ __forceinline__ void stage_last(const float2* seq, const float2* __re
     for (int b = 0; b < BPT; b++) {
         const int j = t + b * T;
 #pragma unroll
-        for (int r = 0; r < R; r++) v[b][r] = seq[pad16(j + r * (L / R))];
+        for (int r = 0; r < R; r++) v[b][r] = seq[pad16s<L / R>(j, r)];
         const int jm = j % NS;
         if constexpr (T16 && R == 16 && NS == 16) {   // (stage_lds's conflict-free layout)
 #pragma unroll
@@ -205,7 +224,7 @@ template <int L>
 __device__ __forceinline__ void stage_first(float2* seq, float2 (&v)[16], int t) {
     dft16(v);
 #pragma unroll
-    for (int r = 0; r < 16; r++) seq[pad16(t * 16 + r)] = v[r];
+    for (int r = 0; r < 16; r++) seq[pad16lo(t, r)] = v[r];
 }
 
 // Stages after the first: LDS -> ... -> store functor. Expects stage_first's LDS writes
