@@ -1524,6 +1524,10 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         // resident in the Infinity Cache: 128 MB of intermediate per chunk (64 and 192-256 MB
         // measured 2-5% slower for 64k with merged launches; 1M: 2.32 vs 2.39 ms at 64 MB)
         long long chunkMB = 128;
+        // the 1M plan (N1 = N2 = 1024): 64 MB = 8 frames, two persistent pass-A tiles per workgroup:
+        // C2 1.770 -> 1.724 ms (r4u), 64 / 96 / 128 / 256 MB 1.742 / 1.802 / 1.77 / 2.10 (r4v, r4u; 3
+        // and 2 interleaved runs); tile counts that are not a multiple of the grid (4 / 6 frames) are slower
+        if (p.N1 == 1024 && p.N2 == 1024) chunkMB = 64;
         if (const char* e = tuning_env("SDRGPU_FFT_CHUNK_MB")) chunkMB = std::max(1, atoi(e));
         // 64k (256 x 256): 32 columns / 32 rows per workgroup (256-B pass-A row segments, 128-B
         // pass-B dB segments, 512 threads, 2 workgroups per CU): the merged spectrum launches
