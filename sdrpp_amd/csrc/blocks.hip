@@ -1274,7 +1274,11 @@ struct ChainBlock : Block {
     int tailBigOut = 512;   // big calls: last-stage outputs per workgroup to start from (SDRGPU_TAIL_OUT, tuning)
     // big calls: the workgroup count and image size depend only on (n0, the stages' offsets), which
     // repeat call after call; the per-workgroup geometry scan is kept for the last key
-    struct TailKey { int n0 = -1; int off[TAIL_MAXS] = {}, H[TAIL_MAXS] = {}, Q[TAIL_MAXS] = {}; int G = 0, maxEl = 0; } tailCache;
+    struct TailKey {
+        int n0 = -1, S = 0;
+        int off[TAIL_MAXS] = {}, H[TAIL_MAXS] = {}, Q[TAIL_MAXS] = {}, D[TAIL_MAXS] = {};
+        int G = 0, maxEl = 0;
+    } tailCache;
     int tailVar = 0;                             // SDRGPU_TAIL_VAR (tuning, timing only): 1 no stage loops, 2 no image loads
     // The tail launch's arguments for kids[1..] on n0 samples of kid 0's output: 1 (t, f, lds
     // filled), 0 (not applicable: the per-kid path runs).
@@ -1317,9 +1321,12 @@ struct ChainBlock : Block {
         // load batch (TAIL_PF per thread); big calls start from ~512 per workgroup
         int maxEl = 0;
         TailGeom g[TAIL_MAXS];
-        bool cached = big && tailCache.n0 == n0;
+        // (the geometry depends on exactly these: every stage's offset, history, padded taps per phase
+        // and decimation, and the stage count)
+        bool cached = big && tailCache.n0 == n0 && tailCache.S == S;
         for (int i = 0; cached && i < S; i++)
-            cached = tailCache.off[i] == t.st[i].off && tailCache.H[i] == t.st[i].H && tailCache.Q[i] == t.st[i].Q;
+            cached = tailCache.off[i] == t.st[i].off && tailCache.H[i] == t.st[i].H && tailCache.Q[i] == t.st[i].Q &&
+                     tailCache.D[i] == t.st[i].D;
         if (cached) {
             t.G = tailCache.G;
             maxEl = tailCache.maxEl;
@@ -1336,10 +1343,12 @@ struct ChainBlock : Block {
             }
             if (big) {
                 tailCache.n0 = n0;
+                tailCache.S = S;
                 for (int i = 0; i < S; i++) {
                     tailCache.off[i] = t.st[i].off;
                     tailCache.H[i] = t.st[i].H;
                     tailCache.Q[i] = t.st[i].Q;
+                    tailCache.D[i] = t.st[i].D;
                 }
                 tailCache.G = t.G;
                 tailCache.maxEl = maxEl;
