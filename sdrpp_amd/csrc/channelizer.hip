@@ -26,6 +26,9 @@
 #include <vector>
 #include "sdrgpu_internal.h"
 #include "fft_stages.h"
+#ifndef SDRGPU_CHAN_PF
+#define SDRGPU_CHAN_PF 1   // FFT-form channelizer: next batch's samples loaded during this batch's FFTs (A/B: 0)
+#endif
 #ifndef SDRGPU_CHAN_NT
 #define SDRGPU_CHAN_NT 1   // FFT-form channelizer: streaming output row stores (A/B builds: 0)
 #endif
@@ -252,28 +255,50 @@ __global__ __launch_bounds__(L / 2) void chan2_kernel(const float2* __restrict__
         for (int q = 0; q < 15; q++) xs[h2][q] = fetch(base + (long long)(m0 + q) * L);
         xs[h2][15] = make_float2(0.f, 0.f);
     }
+    // PF (SDRGPU_CHAN_PF build flag, A/B; not with GEMM, whose DFT already holds 236 VGPRs): the next
+    // batch's 16 samples of the first branch are loaded while this batch's FFTs run (both branches: 72
+    // VGPRs spilled)
+    constexpr bool PFK = SDRGPU_CHAN_PF && !GEMM;
+    float2 pf[1][16];
+    auto load_batch = [&](int mb, int tid, auto& dst, int h0, int h1) {
+        const long long lo = offset0 + (long long)(mb + 15) * L, hi = offset0 + (long long)(mb + 31) * L + L;
+        const bool inner = mb + 16 <= m1 && lo >= H && hi <= (long long)H + count;
+#pragma unroll
+        for (int h2 = h0; h2 < h1; h2++) {
+            const int r = tid + h2 * NT;
+            if (inner) {
+                const float2* __restrict__ src = in + (lo - H);
+#pragma unroll
+                for (int f = 0; f < 16; f++) dst[h2 - h0][f] = src[(long long)f * L + r];
+            } else {
+                const long long base = offset0 + r;
+#pragma unroll
+                for (int f = 0; f < 16; f++)
+                    dst[h2 - h0][f] = (mb + f < m1) ? fetch(base + (long long)(mb + f + 15) * L) : make_float2(0.f, 0.f);
+            }
+        }
+    };
+    if constexpr (PFK) if (m0 < m1) load_batch(m0, threadIdx.x, pf, 0, 1);
     for (int mb = m0; mb < m1; mb += 16) {
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
-        const long long lo = offset0 + (long long)(mb + 15) * L, hi = offset0 + (long long)(mb + 31) * L + L;
-        const bool inner = mb + 16 <= m1 && lo >= H && hi <= (long long)H + count;
+        float2 cur[2][16];
+        if constexpr (PFK) {
+#pragma unroll
+            for (int f = 0; f < 16; f++) cur[0][f] = pf[0][f];
+            float2 (&c1)[1][16] = *reinterpret_cast<float2 (*)[1][16]>(&cur[1]);
+            load_batch(mb, tid, c1, 1, 2);
+        } else {
+            load_batch(mb, tid, cur, 0, 2);
+        }
 #pragma unroll
         for (int h2 = 0; h2 < 2; h2++) {
             const int r = tid + h2 * NT;
             const int c = (rot + r) & (L - 1);
-            float2 nx[16];
             float h[Q];
 #pragma unroll
             for (int q = 0; q < Q; q++) h[q] = taps[q * L + r];
-            if (inner) {
-                const float2* __restrict__ src = in + (lo - H);
-#pragma unroll
-                for (int f = 0; f < 16; f++) nx[f] = src[(long long)f * L + r];
-            } else {
-                const long long base = offset0 + r;
-#pragma unroll
-                for (int f = 0; f < 16; f++) nx[f] = (mb + f < m1) ? fetch(base + (long long)(mb + f + 15) * L) : make_float2(0.f, 0.f);
-            }
+            const float2 (&nx)[16] = cur[h2];
 #pragma unroll
             for (int f = 0; f < 16; f++) {
                 xs[h2][(f + 15) & 15] = nx[f];
@@ -288,6 +313,7 @@ __global__ __launch_bounds__(L / 2) void chan2_kernel(const float2* __restrict__
             }
         }
         __syncthreads();
+        if constexpr (PFK) if (mb + 16 < m1) load_batch(mb + 16, tid, pf, 0, 1);
         if constexpr (GEMM) {
             chan_dft_gemm<L>(lds, twl, tid, mb, m1, out);
             __syncthreads();
