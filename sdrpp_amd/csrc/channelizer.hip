@@ -29,6 +29,9 @@
 #ifndef SDRGPU_CHAN_PF
 #define SDRGPU_CHAN_PF 1   // FFT-form channelizer: next batch's samples loaded during this batch's FFTs (A/B: 0)
 #endif
+#ifndef SDRGPU_CHAN_PF2
+#define SDRGPU_CHAN_PF2 0
+#endif
 #ifndef SDRGPU_CHAN_NT
 #define SDRGPU_CHAN_NT 1   // FFT-form channelizer: streaming output row stores (A/B builds: 0)
 #endif
@@ -278,7 +281,26 @@ __global__ __launch_bounds__(L / 2) void chan2_kernel(const float2* __restrict__
             }
         }
     };
-    if constexpr (PFK) if (m0 < m1) load_batch(m0, threadIdx.x, pf, 0, 1);
+    // (SDRGPU_CHAN_PF2, A/B: the second branch's first PF2 frames prefetched as well)
+    constexpr int PF2 = PFK ? SDRGPU_CHAN_PF2 : 0;
+    float2 pf2[PF2 > 0 ? PF2 : 1];
+    auto load2 = [&](int mb, int tid) {   // branch 1, frames < PF2
+        if constexpr (PF2 > 0) {
+            const long long lo = offset0 + (long long)(mb + 15) * L, hi = offset0 + (long long)(mb + 31) * L + L;
+            const bool inner = mb + 16 <= m1 && lo >= H && hi <= (long long)H + count;
+            const int r = tid + NT;
+            if (inner) {
+                const float2* __restrict__ src = in + (lo - H);
+#pragma unroll
+                for (int f = 0; f < PF2; f++) pf2[f] = src[(long long)f * L + r];
+            } else {
+                const long long base = offset0 + r;
+#pragma unroll
+                for (int f = 0; f < PF2; f++) pf2[f] = (mb + f < m1) ? fetch(base + (long long)(mb + f + 15) * L) : make_float2(0.f, 0.f);
+            }
+        }
+    };
+    if constexpr (PFK) if (m0 < m1) { load_batch(m0, threadIdx.x, pf, 0, 1); load2(m0, threadIdx.x); }
     for (int mb = m0; mb < m1; mb += 16) {
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
@@ -288,6 +310,10 @@ __global__ __launch_bounds__(L / 2) void chan2_kernel(const float2* __restrict__
             for (int f = 0; f < 16; f++) cur[0][f] = pf[0][f];
             float2 (&c1)[1][16] = *reinterpret_cast<float2 (*)[1][16]>(&cur[1]);
             load_batch(mb, tid, c1, 1, 2);
+            if constexpr (PF2 > 0) {
+#pragma unroll
+                for (int f = 0; f < PF2; f++) cur[1][f] = pf2[f];
+            }
         } else {
             load_batch(mb, tid, cur, 0, 2);
         }
@@ -313,7 +339,7 @@ __global__ __launch_bounds__(L / 2) void chan2_kernel(const float2* __restrict__
             }
         }
         __syncthreads();
-        if constexpr (PFK) if (mb + 16 < m1) load_batch(mb + 16, tid, pf, 0, 1);
+        if constexpr (PFK) if (mb + 16 < m1) { load_batch(mb + 16, tid, pf, 0, 1); load2(mb + 16, tid); }
         if constexpr (GEMM) {
             chan_dft_gemm<L>(lds, twl, tid, mb, m1, out);
             __syncthreads();
