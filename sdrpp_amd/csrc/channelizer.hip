@@ -30,7 +30,9 @@
 #define SDRGPU_CHAN_PF 1   // FFT-form channelizer: next batch's samples loaded during this batch's FFTs (A/B: 0)
 #endif
 #ifndef SDRGPU_CHAN_PF2
-#define SDRGPU_CHAN_PF2 0
+// the second branch's first 8 frames prefetched as well (204 VGPRs; all 16: 82 spilled): C4 1.158 (no
+// prefetch) -> 1.074 (first branch) -> 1.064 ms (+ 8 frames), 3 interleaved runs, r4z
+#define SDRGPU_CHAN_PF2 8
 #endif
 #ifndef SDRGPU_CHAN_NT
 #define SDRGPU_CHAN_NT 1   // FFT-form channelizer: streaming output row stores (A/B builds: 0)
