@@ -940,6 +940,213 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     else passA_tile<256, 32, CP>(lds, g * 8 + r, in, frameStride, framesA, win, nz, 256, logN, tw1, tfull, scratchA);
 }
 
+// ---- one-pass 64k spectrum (round 4): no intermediate leaves the CU ---------------------------
+// N = 65536 as four 16,384-point transforms (one radix-4 decimation-in-frequency step). Workgroup
+// (f, r) computes the bins 4 m + r of frame f:
+//   X[4 m + r] = sum_{n < M} W_M^(n m) y_r[n],   y_r[n] = W_N^(n r) sum_{j < 4} W_4^(j r) w[n + M j] x[n + M j],
+// M = 16384. The 16k transform is M = 32 x 32 x 16 on one CU:
+//   stage 1 (registers): thread t holds y_r[t + 512 i], i < 32, straight from its loads (the four
+//     quarters combined as they arrive); a radix-32 DFT over i and the twiddle W_M^(t k2) W_N^(t r)
+//     = W_N^(t (4 k2 + r)) (one exact fp64-built table value) give A[t][k2];
+//   stage 2 (LDS): per (k2, t0), a radix-32 DFT over t1 of A[t0 + 16 t1][k2], twiddle W_512^(t0 q1);
+//   stage 3 (LDS): per (k2, q1), a radix-16 DFT over t0 -> Y[k2 + 32 q1 + 1024 q2], dB, store.
+// The four workgroups of a frame are consecutive on one XCD (round-robin dispatch: workgroup b runs
+// on XCD b mod 8), so the frame is fetched from HBM once and read by the other three from that XCD's
+// L2. Fabric traffic per sample is then the input (8 B) and the dB row (4 B): the two-pass transform's
+// 16 B of intermediate are gone. With a VFO (VFO = true) each workgroup first runs quarter r of the
+// VFO stage 1 (vfo_quarter_block: the same segments as fir_rows_kernel, so bit-identical), which is
+// the frame's first reader. Zoom (ZM): each workgroup writes the max of its 8 bins of every 32-bin
+// zoom column to zpart[f][r][o]; fft_1p_zoom_kernel folds the four.
+// LDS image: 32 rows k2 of 544 used float2 (stage 1: column pad16(t); stage 2: column 17 q1 +
+// (t0 ^ ((k2 >> 1) & 15))), row stride 560 (= 16 mod 32): every stage-2/3 access of a half-wave hits
+// 32 distinct 8-byte bank pairs.
+namespace op1 {
+constexpr int M = 16384;
+constexpr int RS = 560;                 // LDS row stride (float2)
+constexpr int TW512 = 32 * RS;          // W_512^(t0 q1) at [q1][t0]
+constexpr int W128 = TW512 + 512;       // W_128^(r i), i < 32
+constexpr int LDS_BYTES = (W128 + 32) * 8;
+constexpr int TAB = 4 * M + 512 + 128;  // device table: [r][k2][t] W_N^(t (4 k2 + r)), [q1][t0], [r][i]
+}
+
+// 32-point DFT as 2 x 16 (even / odd halves), natural order in and out
+__device__ __forceinline__ void dft32(float2* v) {
+    constexpr float C[16] = {1.0f, 0.98078528040323044913f, 0.92387953251128675613f, 0.83146961230254523708f,
+                             0.70710678118654752440f, 0.55557023301960222474f, 0.38268343236508977173f,
+                             0.19509032201612826785f, 0.0f, -0.19509032201612826785f, -0.38268343236508977173f,
+                             -0.55557023301960222474f, -0.70710678118654752440f, -0.83146961230254523708f,
+                             -0.92387953251128675613f, -0.98078528040323044913f};
+    float2 e[16], o[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        e[i] = v[2 * i];
+        o[i] = v[2 * i + 1];
+    }
+    dft16(e);
+    dft16(o);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        float2 t = o[k];
+        if (k == 8) t = mul_negi(t);
+        else if (k) t = cmul(t, make_float2(C[k], -C[(k + 8) & 15] * (k < 8 ? -1.0f : 1.0f)));   // W_32^k
+        v[k] = cadd(e[k], t);
+        v[k + 16] = csub(e[k], t);
+    }
+}
+
+// stage-1 twiddles W_N^(t (4 k2 + r)): 0 = one exact table value each (128 KB per workgroup from L2);
+// 1 = an fp64 recurrence W_N^(t r) (W_N^(4 t))^k2 from two values of an fp64 table, rounded once
+#ifndef SDRGPU_1P_TW
+#define SDRGPU_1P_TW 0
+#endif
+template <bool ZM, bool VFO>
+__global__ __launch_bounds__(512) void fft_1p_kernel(const float2* __restrict__ in, long long frameStride, int frames,
+                                                     const float* __restrict__ win, int nz, const float2* __restrict__ tab,
+                                                     const double2* __restrict__ tab64, float* __restrict__ out,
+                                                     float* __restrict__ zpart, VfoWork v) {
+    using namespace op1;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    if constexpr (VFO) {
+        if (v.hist && blockIdx.x == gridDim.x - 1) {   // the stage's history carry (fir.h:80)
+            (void)fir_hist_block<float2, true, false>(v.a);
+            return;
+        }
+    }
+    const int b = blockIdx.x, k = b >> 3;
+    const int f = 8 * (k >> 2) + (b & 7), r = k & 3;
+    if (f >= frames) return;
+    if constexpr (VFO) vfo_quarter_block(v, f, r);
+    const int t = threadIdx.x;
+    float2* tw512 = lds + TW512;
+    float2* w128 = lds + W128;
+    tw512[t] = tab[4 * M + t];
+    if (t < 32) w128[t] = tab[4 * M + 512 + 32 * r + t];
+    // stage 1: y_r[t + 512 i] from the four quarters. W_4^(j r): (u0 + s u2) + W_4^r (u1 + s u3), s = (-1)^r
+    const float s = (r & 1) ? -1.0f : 1.0f;
+    const float fx = r == 0 ? 1.0f : (r == 2 ? -1.0f : 0.0f), fy = r == 1 ? -1.0f : (r == 3 ? 1.0f : 0.0f);
+    const float2* xf = in + (long long)f * frameStride;
+    float2 z[32];
+    auto combine = [&](int i, const float2 (&xv)[4], const float (&wv)[4]) {
+        float2 u[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) u[j] = make_float2(xv[j].x * wv[j], xv[j].y * wv[j]);
+        const float2 a = make_float2(fmaf(s, u[2].x, u[0].x), fmaf(s, u[2].y, u[0].y));
+        const float2 q = make_float2(fmaf(s, u[3].x, u[1].x), fmaf(s, u[3].y, u[1].y));
+        // W_4^r q with W_4^r in {1, -i, -1, i}: one of fx, fy is 0, the other +-1 (exact products)
+        z[i] = make_float2(a.x + (fx * q.x - fy * q.y), a.y + (fx * q.y + fy * q.x));
+    };
+#ifndef SDRGPU_1P_DBG
+#define SDRGPU_1P_DBG 0
+#endif
+    if ((SDRGPU_1P_DBG & 1) || nz >= 65536) {   // no zero padding (workgroup-uniform): the quarter / row step rides in soffset
+        const __amdgpu_buffer_rsrc_t rx = brsrc(xf, 65536u * 8u), rw = brsrc(win, 65536u * 4u);
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            float2 xv[8][4];
+            float wv[8][4];
+#pragma unroll
+            for (int ii = 0; ii < 8; ii++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int n0 = 512 * (8 * bb + ii) + M * j;
+                    xv[ii][j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, t * 8, n0 * 8, 0));
+                    wv[ii][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, t * 4, n0 * 4, 0));
+                }
+#pragma unroll
+            for (int ii = 0; ii < 8; ii++) combine(8 * bb + ii, xv[ii], wv[ii]);
+            __builtin_amdgcn_sched_barrier(0);   // one batch of loads in flight (hoisted, they spill)
+        }
+    } else {             // zero-padded frame: range-checked loads (the offset in the per-lane part)
+        const __amdgpu_buffer_rsrc_t rx = brsrc(xf, (unsigned)nz * 8u), rw = brsrc(win, (unsigned)nz * 4u);
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            float2 xv[8][4];
+            float wv[8][4];
+#pragma unroll
+            for (int ii = 0; ii < 8; ii++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int n = t + 512 * (8 * bb + ii) + M * j;   // (past nz: both loads return 0)
+                    xv[ii][j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, n * 8, 0, 0));
+                    wv[ii][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, n * 4, 0, 0));
+                }
+#pragma unroll
+            for (int ii = 0; ii < 8; ii++) combine(8 * bb + ii, xv[ii], wv[ii]);
+            __builtin_amdgcn_sched_barrier(0);   // one batch of loads in flight (hoisted, they spill)
+        }
+    }
+    __syncthreads();   // (w128, tw512)
+#pragma unroll
+    for (int i = 1; i < 32; i++) z[i] = cmul(z[i], w128[i]);   // W_128^(r i) = W_N^(512 r i)
+    dft32(z);
+    if constexpr (SDRGPU_1P_TW == 1) {
+        double2 c = tab64[t * r];
+        const double2 st = tab64[4 * t];
+#pragma unroll
+        for (int k2 = 0; k2 < 32; k2++) {
+            lds[k2 * RS + pad16(t)] = cmul(z[k2], make_float2((float)c.x, (float)c.y));
+            if (k2 < 31) c = zmul(c, st);
+        }
+    } else {
+#pragma unroll
+        for (int k2 = 0; k2 < 32; k2++) lds[k2 * RS + pad16(t)] = cmul(z[k2], tab[(32 * r + k2) * 512 + t]);   // W_N^(t (4 k2 + r))
+    }
+    __syncthreads();
+    if (SDRGPU_1P_DBG & 2) return;
+    // stage 2: (k2, t0) = (t >> 4, t & 15)
+    {
+        const int k2 = t >> 4, t0 = t & 15;
+        float2 a[32];
+#pragma unroll
+        for (int t1 = 0; t1 < 32; t1++) a[t1] = lds[k2 * RS + t0 + 17 * t1];
+        dft32(a);
+#pragma unroll
+        for (int q1 = 1; q1 < 32; q1++) a[q1] = cmul(a[q1], tw512[16 * q1 + t0]);
+        __syncthreads();
+        const int sw = t0 ^ ((k2 >> 1) & 15);
+#pragma unroll
+        for (int q1 = 0; q1 < 32; q1++) lds[k2 * RS + 17 * q1 + sw] = a[q1];
+    }
+    __syncthreads();
+    if (SDRGPU_1P_DBG & 4) return;
+    // stage 3: (k2, q1) = (p & 31, p >> 5), p = t, t + 512
+    float* of = out + ((long long)f << 16);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int p = t + 512 * h, k2 = p & 31, q1 = p >> 5, sw = (k2 >> 1) & 15;
+        float2 c[16];
+#pragma unroll
+        for (int t0 = 0; t0 < 16; t0++) c[t0] = lds[k2 * RS + 17 * q1 + (t0 ^ sw)];
+        dft16(c);
+        float dv[16];
+#pragma unroll
+        for (int q2 = 0; q2 < 16; q2++) {
+            dv[q2] = db_of(c[q2]);
+            of[4 * (k2 + 32 * q1 + 1024 * q2) + r] = dv[q2];
+        }
+        if constexpr (ZM) {   // max over the 8 lanes k2 & 7 (zoom column (k2 >> 3) + 4 q1 + 128 q2)
+            const int lane = t & 63;
+            tr_step<1, 8>(dv, lane);
+            tr_step<2, 4>(dv, lane);
+            tr_step<4, 2>(dv, lane);
+            // lane bits (b0 b1 b2) now select q2 = 8 b0 + 4 b1 + 2 b2 + i in dv[i], i < 2
+            const int q2 = ((lane & 1) << 3) | ((lane & 2) << 1) | (lane & 4) >> 1;
+            float* zp = zpart + ((long long)(4 * f + r) << 11) + (k2 >> 3) + 4 * q1 + 128 * q2;
+            zp[0] = dv[0];
+            zp[128] = dv[1];
+        }
+    }
+}
+
+// zoom[f][o] = max over the four workgroups' partial maxima (fft_1p_kernel's ZM)
+__global__ __launch_bounds__(256) void fft_1p_zoom_kernel(const float* __restrict__ zpart, int frames, float* __restrict__ zoom) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long long)frames * 2048) return;
+    const long long f = i >> 11, o = i & 2047;
+    const float* p = zpart + (f << 13) + o;
+    zoom[i] = fmaxf(fmaxf(p[0], p[2048]), fmaxf(p[4096], p[6144]));
+}
+
 // ---- the C5 launch group as ONE persistent launch with per-frame dataflow (round 4, tuning:
 // SDRGPU_FFT_VFO_PERSIST). Each workgroup reads its XCD id (HW_REG_XCC_ID) and takes items from that
 // XCD's queue: frame f = 8 j + x belongs to XCD x; its 12 first-pass items (4 stage-1 quarters, 8
@@ -1168,6 +1375,9 @@ struct FftPlan {
     // 1 XCD-grouped (group 1.732 -> 1.694 ms, r4d); 2 + passes interleaved (1.684 -> 1.679, noise, r4f);
     // 3 XCD-grouped with quarter-frame stage-1 workgroups (1.743 -> 1.696 ms, r4g), the default
     int vfoXcd = 3;
+    // the 64k plan: one-pass spectrum launches (fft_1p_kernel), SDRGPU_FFT_1P (tuning)
+    int onepass = 0;
+    DevBuf tab1p, tab1p64, zpart;
 };
 // the plan's side stream and its events (the two-stream pipeline; the fused VFO's later stages)
 static int ensure_side(FftPlan& p) {
@@ -1555,6 +1765,33 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         if (const char* e = tuning_env("SDRGPU_FFT_VFO_SIDE")) p.vfoSide = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_VFO_PERSIST")) p.vfoPersist = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_PERSIST_LAG")) p.persistLag = std::max(1, atoi(e));
+        if (const char* e = tuning_env("SDRGPU_FFT_1P")) p.onepass = atoi(e);
+        if (rc >= 0 && fftSize == 65536) {   // fft_1p_kernel's exact twiddles (op1::TAB)
+            std::vector<float2> t(op1::TAB);
+            auto w = [&](long long m) {
+                const double a = -2.0 * M_PI * (double)(m % fftSize) / (double)fftSize;
+                return make_float2((float)std::cos(a), (float)std::sin(a));
+            };
+            for (int r = 0; r < 4; r++)
+                for (int k2 = 0; k2 < 32; k2++)
+                    for (int tt = 0; tt < 512; tt++) t[(size_t)(32 * r + k2) * 512 + tt] = w((long long)tt * (4 * k2 + r));
+            for (int q1 = 0; q1 < 32; q1++)
+                for (int t0 = 0; t0 < 16; t0++) t[4 * op1::M + 16 * q1 + t0] = w(128LL * t0 * q1);
+            for (int r = 0; r < 4; r++)
+                for (int i = 0; i < 32; i++) t[4 * op1::M + 512 + 32 * r + i] = w(512LL * r * i);
+            std::vector<double2> t64(2048);   // W_N^m, m < 2048, fp64 (SDRGPU_1P_TW 1)
+            for (int m = 0; m < 2048; m++) {
+                const double a = -2.0 * M_PI * (double)m / (double)fftSize;
+                t64[m] = make_double2(std::cos(a), std::sin(a));
+            }
+            rc = p.tab1p.ensure(sizeof(float2) * t.size());
+            if (rc >= 0) rc = p.tab1p64.ensure(sizeof(double2) * t64.size());
+            if (rc >= 0 && (hipMemcpy(p.tab1p.p, t.data(), sizeof(float2) * t.size(), hipMemcpyHostToDevice) != hipSuccess ||
+                            hipMemcpy(p.tab1p64.p, t64.data(), sizeof(double2) * t64.size(), hipMemcpyHostToDevice) != hipSuccess)) {
+                set_error("fft: twiddle upload failed");
+                rc = SDRGPU_EHIP;
+            }
+        }
         if (rc >= 0 && p.N1 == 1024 && p.N2 == 1024) {   // fp64 W_N^(256 j), W_N^j for the 1M pass A
             std::vector<double2> t(512);
             for (int j = 0; j < 256; j++) {
@@ -1631,6 +1868,27 @@ static bool zoom_fusable(const FftPlan& p, int zoomSize) {
     return p.N1 == 256 && p.N2 == 256 && p.sa == 32 && p.sb == 32 && zoomSize * 32 == p.N;
 }
 
+// the one-pass 64k launch (+ the zoom fold): 4 workgroups per frame, XCD-grouped in blocks of 8 frames
+template <bool ZM, bool VFO>
+static int launch_1p(FftPlan& p, const float2* in, long long stride, int frames, float* out, float* zoom, VfoWork v,
+                     hipStream_t s) {
+    auto k = fft_1p_kernel<ZM, VFO>;
+    SDRGPU_CHECK(set_lds(k, op1::LDS_BYTES));
+    if (ZM) SDRGPU_CHECK(p.zpart.ensure(sizeof(float) * 4 * 2048 * (size_t)frames));
+    const int g = 32 * ((frames + 7) / 8) + (VFO && v.hist ? 1 : 0);
+    hipLaunchKernelGGL(k, dim3(g), dim3(512), op1::LDS_BYTES, s, in, stride, frames, p.win.as<float>(), p.nz,
+                       p.tab1p.as<float2>(), p.tab1p64.as<double2>(), out, ZM ? p.zpart.as<float>() : nullptr, v);
+    SDRGPU_HIP(hipGetLastError());
+    if (ZM) {
+        const long long n = (long long)frames * 2048;
+        hipLaunchKernelGGL(fft_1p_zoom_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p.zpart.as<float>(),
+                           frames, zoom);
+        SDRGPU_HIP(hipGetLastError());
+    }
+    return SDRGPU_OK;
+}
+static bool onepass_ok(const FftPlan& p) { return p.onepass && p.N == 65536 && p.tab1p.p && !p.f64; }
+
 // frames -> dB rows (and, with zoom != nullptr on a zoom_fusable plan, the full-span zoom rows)
 static int fft_execute_body(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, float* zoom,
                             hipStream_t s);
@@ -1649,6 +1907,12 @@ static int fft_execute_body(sdrgpu_fft* h, const void* in, long long frameStride
     if (p.f64) return fft64_execute(p.f64, x, frameStride, frames, p.win.as<float>(), p.nz, out, s);   // (zoom: unfused)
     if (p.N1 == 0) {
         SDRGPU_CHECK(dispatch_single(p, x, frameStride, frames, out, s));
+        return frames;
+    }
+    if (onepass_ok(p)) {
+        const int rc = zoom ? launch_1p<true, false>(p, x, frameStride, frames, out, zoom, VfoWork{}, s)
+                            : launch_1p<false, false>(p, x, frameStride, frames, out, nullptr, VfoWork{}, s);
+        if (rc < 0) return rc;
         return frames;
     }
     const long long zw = p.N / 32;   // zoom row width when fused
@@ -1913,6 +2177,15 @@ static int fft_execute_vfo(FftPlan& p, const float2* x, int frames, float* out, 
             SDRGPU_CHECK(fft_execute_vfo_persist(p, x, frames, out, zoom, st, s));
             return vfo_stage1_finish(vfo, st, vfoOut, s);
         }
+    }
+    if (onepass_ok(p)) {
+        VfoWork v{st.a, 0, 1};
+        SDRGPU_CHECK(time_mark(p, 0, s));
+        const int rc = zoom ? launch_1p<true, true>(p, x, p.N, frames, out, zoom, v, s)
+                            : launch_1p<false, true>(p, x, p.N, frames, out, nullptr, v, s);
+        if (rc < 0) return rc;
+        SDRGPU_CHECK(time_mark(p, 1, s));
+        return vfo_stage1_finish(vfo, st, vfoOut, s);
     }
     const int cf = p.chunkFrames;
     const int nchunks = (frames + cf - 1) / cf;

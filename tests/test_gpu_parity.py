@@ -1004,6 +1004,51 @@ def test_spectrum_vfo_persistent(frames_list, pre, rng, monkeypatch):
     _fused_vs_separate(frames_list, pre, rng, zoom=True)
 
 
+# ------------------------------------------------- the one-pass 64k spectrum (fft_1p_kernel)
+@pytest.mark.parametrize("nz,skip,frames", [(65536, 0, 9), (40000, 123, 3), (65535, 7, 2)])
+def test_spectrum_onepass_rows_and_zoom(nz, skip, frames, rng, monkeypatch):
+    """The one-pass 64k transform (four 16k sub-transforms per frame on four CUs, radix-4 decimation in
+    frequency; SDRGPU_FFT_1P): every row meets the spectrum parity bar against the fp64 truth and
+    pocketfft on the same frame, zero-padded frames (nz < N) and reshaper strides included; the zoom
+    rows (four partial maxima folded) equal fft_scaler's doZoom of the row bit for bit; and the rows
+    agree with the two-pass kernels to the last bits near the peak."""
+    import torch
+    monkeypatch.setenv("SDRGPU_TUNING", "1")
+    N, zw = 65536, 2048
+    stride = nz + skip
+    x = iq(rng, stride * (frames - 1) + nz)
+    d_x = torch.from_numpy(x.view(np.float32)).cuda()
+    out = torch.empty(frames * N, device="cuda")
+    z = torch.empty(frames * zw, device="cuda")
+    ref = torch.empty(frames * N, device="cuda")
+    monkeypatch.setenv("SDRGPU_FFT_1P", "1")
+    f = dsp.FFTSpectrum(N, nz, 6)
+    assert f.execute_zoom_dev(d_x.data_ptr(), stride, frames, out.data_ptr(), z.data_ptr(), zw) == frames
+    monkeypatch.setenv("SDRGPU_FFT_1P", "0")
+    dsp.FFTSpectrum(N, nz, 6).execute_dev(d_x.data_ptr(), stride, frames, ref.data_ptr())
+    torch.cuda.synchronize()
+    rows = out.cpu().numpy().reshape(frames, N)
+    d = np.abs(rows - ref.cpu().numpy().reshape(frames, N))
+    assert d.max() <= 0.05 and np.all(d[rows >= rows.max(axis=1, keepdims=True) - 60] <= 1e-3), d.max()
+    w = oracle.create_window(6, nz)
+    zr = z.cpu().numpy().reshape(frames, zw)
+    for j in range(frames):
+        xs = x[j * stride:j * stride + nz]
+        db_check(rows[j], oracle.fft_truth_power(xs, nz, N, w), N, ref32_fft_db(xs, nz, N, w))
+        np.testing.assert_array_equal(zr[j], oracle.zoom(rows[j], 0.0, 1.0, 1.0, zw))
+
+
+@pytest.mark.parametrize("frames_list,pre", [([13], 1000), ([3, 8], 0)])
+def test_spectrum_onepass_vfo(frames_list, pre, rng, monkeypatch):
+    """The C5 group as ONE launch (SDRGPU_FFT_1P): each of a frame's four workgroups runs a quarter of
+    the VFO's first stage, then its 16k sub-transform. Rows and zoom rows bit-identical to the one-pass
+    spectrum without the VFO, the VFO output bit-identical to RxVFO.process_dev and within the oracle
+    bar (_fused_vs_separate)."""
+    monkeypatch.setenv("SDRGPU_TUNING", "1")
+    monkeypatch.setenv("SDRGPU_FFT_1P", "1")
+    _fused_vs_separate(frames_list, pre, rng, zoom=True)
+
+
 # ------------------------------------------------- waterfall zoom fused into the spectrum
 @pytest.mark.parametrize("frames,chunk_mb,zsize", [(3, None, 2048), (9, 1, 2048), (4, None, 1800), (5, 1, 4096)])
 def test_spectrum_zoom_rows(frames, chunk_mb, zsize, rng, monkeypatch):
