@@ -996,15 +996,26 @@ __device__ __forceinline__ void dft32(float2* v) {
 
 // stage-1 twiddles W_N^(t (4 k2 + r)): 0 = one exact table value each (128 KB per workgroup from L2);
 // 1 = an fp64 recurrence W_N^(t r) (W_N^(4 t))^k2 from two values of an fp64 table, rounded once
+// (group 1.942 -> 1.893 ms, r41pb; the 1p tests pass with both)
 #ifndef SDRGPU_1P_TW
-#define SDRGPU_1P_TW 0
+#define SDRGPU_1P_TW 1
 #endif
-template <bool ZM, bool VFO>
-__global__ __launch_bounds__(512) void fft_1p_kernel(const float2* __restrict__ in, long long frameStride, int frames,
-                                                     const float* __restrict__ win, int nz, const float2* __restrict__ tab,
-                                                     const double2* __restrict__ tab64, float* __restrict__ out,
-                                                     float* __restrict__ zpart, VfoWork v) {
-    using namespace op1;
+#ifndef SDRGPU_1P_PB
+#define SDRGPU_1P_PB 4   // sample rows per load batch
+#endif
+#ifndef SDRGPU_1P_PB2
+#define SDRGPU_1P_PB2 2   // (HALF) sample rows per load batch at the 128-VGPR budget
+#endif
+// HALF (SDRGPU_FFT_1P=2): the LDS image holds 16 rows k2 at a time (76 KB: two workgroups per CU, 128
+// VGPRs): stage 1's 32 outputs stay in registers, and rows 0-15, then 16-31, go through stages 2 and 3
+template <bool ZM, bool VFO, bool HALF = false>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 1))) void fft_1p_kernel(
+    const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz,
+    const float2* __restrict__ tab, const double2* __restrict__ tab64, float* __restrict__ out, float* __restrict__ zpart,
+    VfoWork v) {
+    using op1::M;
+    using op1::RS;
+    constexpr int TW512 = (HALF ? 16 : 32) * RS, W128 = TW512 + 512;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     if constexpr (VFO) {
         if (v.hist && blockIdx.x == gridDim.x - 1) {   // the stage's history carry (fir.h:80)
@@ -1035,53 +1046,109 @@ __global__ __launch_bounds__(512) void fft_1p_kernel(const float2* __restrict__ 
         // W_4^r q with W_4^r in {1, -i, -1, i}: one of fx, fy is 0, the other +-1 (exact products)
         z[i] = make_float2(a.x + (fx * q.x - fy * q.y), a.y + (fx * q.y + fy * q.x));
     };
-#ifndef SDRGPU_1P_DBG
-#define SDRGPU_1P_DBG 0
-#endif
-    if ((SDRGPU_1P_DBG & 1) || nz >= 65536) {   // no zero padding (workgroup-uniform): the quarter / row step rides in soffset
+    double2 c0, st;   // (SDRGPU_1P_TW 1) W_N^(t r), W_N^(4 t): loaded first, used after the loads
+    if constexpr (SDRGPU_1P_TW == 1 && !HALF) {
+        c0 = tab64[t * r];
+        st = tab64[4 * t];
+    }
+    // batches of PB sample rows (4 PB loads of x and of w each), the next batch's loads in flight while
+    // this one is combined (two batches of registers; issued all at once, the loads spill)
+    constexpr int PB = HALF ? SDRGPU_1P_PB2 : SDRGPU_1P_PB, NB = 32 / PB;
+    auto pipeline = [&](auto&& ld) {
+        float2 xv[2][PB][4];
+        float wv[2][PB][4];
+        auto issue = [&](int bb, float2 (&xb)[PB][4], float (&wb)[PB][4]) {
+#pragma unroll
+            for (int ii = 0; ii < PB; ii++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) ld(512 * (PB * bb + ii) + M * j, xb[ii][j], wb[ii][j]);
+        };
+        issue(0, xv[0], wv[0]);
+#pragma unroll
+        for (int bb = 0; bb < NB; bb++) {
+            if (bb + 1 < NB) issue(bb + 1, xv[(bb + 1) & 1], wv[(bb + 1) & 1]);
+#pragma unroll
+            for (int ii = 0; ii < PB; ii++) combine(PB * bb + ii, xv[bb & 1][ii], wv[bb & 1][ii]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    if (nz >= 65536) {   // no zero padding (workgroup-uniform): the row offset rides in soffset
         const __amdgpu_buffer_rsrc_t rx = brsrc(xf, 65536u * 8u), rw = brsrc(win, 65536u * 4u);
-#pragma unroll
-        for (int bb = 0; bb < 4; bb++) {
-            float2 xv[8][4];
-            float wv[8][4];
-#pragma unroll
-            for (int ii = 0; ii < 8; ii++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int n0 = 512 * (8 * bb + ii) + M * j;
-                    xv[ii][j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, t * 8, n0 * 8, 0));
-                    wv[ii][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, t * 4, n0 * 4, 0));
-                }
-#pragma unroll
-            for (int ii = 0; ii < 8; ii++) combine(8 * bb + ii, xv[ii], wv[ii]);
-            __builtin_amdgcn_sched_barrier(0);   // one batch of loads in flight (hoisted, they spill)
-        }
-    } else {             // zero-padded frame: range-checked loads (the offset in the per-lane part)
+        pipeline([&](int n0, float2& xo, float& wo) {
+            xo = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, t * 8, n0 * 8, 0));
+            wo = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, t * 4, n0 * 4, 0));
+        });
+    } else {             // zero-padded frame: range-checked loads, the offset in the per-lane part (past nz: 0)
         const __amdgpu_buffer_rsrc_t rx = brsrc(xf, (unsigned)nz * 8u), rw = brsrc(win, (unsigned)nz * 4u);
-#pragma unroll
-        for (int bb = 0; bb < 4; bb++) {
-            float2 xv[8][4];
-            float wv[8][4];
-#pragma unroll
-            for (int ii = 0; ii < 8; ii++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int n = t + 512 * (8 * bb + ii) + M * j;   // (past nz: both loads return 0)
-                    xv[ii][j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, n * 8, 0, 0));
-                    wv[ii][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, n * 4, 0, 0));
-                }
-#pragma unroll
-            for (int ii = 0; ii < 8; ii++) combine(8 * bb + ii, xv[ii], wv[ii]);
-            __builtin_amdgcn_sched_barrier(0);   // one batch of loads in flight (hoisted, they spill)
-        }
+        pipeline([&](int n0, float2& xo, float& wo) {
+            xo = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, (t + n0) * 8, 0, 0));
+            wo = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, (t + n0) * 4, 0, 0));
+        });
     }
     __syncthreads();   // (w128, tw512)
 #pragma unroll
     for (int i = 1; i < 32; i++) z[i] = cmul(z[i], w128[i]);   // W_128^(r i) = W_N^(512 r i)
     dft32(z);
+    float* of = out + ((long long)f << 16);
+    if constexpr (HALF) {
+        static_assert(SDRGPU_1P_TW == 1, "HALF: fp64-recurrence twiddles");
+        double2 c = tab64[t * r];   // (loaded here: at 128 VGPRs they do not stay live through the loads)
+        st = tab64[4 * t];
+#pragma unroll
+        for (int k2 = 0; k2 < 32; k2++) {
+            z[k2] = cmul(z[k2], make_float2((float)c.x, (float)c.y));
+            if (k2 < 31) c = zmul(c, st);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+#pragma unroll
+            for (int kl = 0; kl < 16; kl++) lds[kl * RS + pad16(t)] = z[16 * h + kl];
+            __syncthreads();
+            // stage 2 on rows k2 = 16 h + kl: (kl, t0) = (t >> 4, t & 15), the first 256 threads
+            const int kl2 = (t >> 4) & 15, t0 = t & 15, k22 = 16 * h + kl2;
+            float2 a[32];
+            if (t < 256) {
+#pragma unroll
+                for (int t1 = 0; t1 < 32; t1++) a[t1] = lds[kl2 * RS + t0 + 17 * t1];
+                dft32(a);
+#pragma unroll
+                for (int q1 = 1; q1 < 32; q1++) a[q1] = cmul(a[q1], lds[TW512 + 16 * q1 + t0]);
+            }
+            __syncthreads();
+            if (t < 256) {
+                const int sw = t0 ^ ((k22 >> 1) & 15);
+#pragma unroll
+                for (int q1 = 0; q1 < 32; q1++) lds[kl2 * RS + 17 * q1 + sw] = a[q1];
+            }
+            __syncthreads();
+            // stage 3: (kl, q1) = (t & 15, t >> 4)
+            const int kl = t & 15, q1 = t >> 4, k2 = 16 * h + kl, sw = (k2 >> 1) & 15;
+            float2 c3[16];
+#pragma unroll
+            for (int t0 = 0; t0 < 16; t0++) c3[t0] = lds[kl * RS + 17 * q1 + (t0 ^ sw)];
+            dft16(c3);
+            float dv[16];
+#pragma unroll
+            for (int q2 = 0; q2 < 16; q2++) {
+                dv[q2] = db_of(c3[q2]);
+                of[4 * (k2 + 32 * q1 + 1024 * q2) + r] = dv[q2];
+            }
+            if constexpr (ZM) {   // max over the 8 lanes kl & 7 (zoom column (k2 >> 3) + 4 q1 + 128 q2)
+                const int lane = t & 63;
+                tr_step<1, 8>(dv, lane);
+                tr_step<2, 4>(dv, lane);
+                tr_step<4, 2>(dv, lane);
+                const int q2 = ((lane & 1) << 3) | ((lane & 2) << 1) | (lane & 4) >> 1;
+                float* zp = zpart + ((long long)(4 * f + r) << 11) + (k2 >> 3) + 4 * q1 + 128 * q2;
+                zp[0] = dv[0];
+                zp[128] = dv[1];
+            }
+            if (h == 0) __syncthreads();   // (stage 3's reads before the next rows land)
+        }
+        return;
+    }
     if constexpr (SDRGPU_1P_TW == 1) {
-        double2 c = tab64[t * r];
-        const double2 st = tab64[4 * t];
+        double2 c = c0;
 #pragma unroll
         for (int k2 = 0; k2 < 32; k2++) {
             lds[k2 * RS + pad16(t)] = cmul(z[k2], make_float2((float)c.x, (float)c.y));
@@ -1092,7 +1159,6 @@ __global__ __launch_bounds__(512) void fft_1p_kernel(const float2* __restrict__ 
         for (int k2 = 0; k2 < 32; k2++) lds[k2 * RS + pad16(t)] = cmul(z[k2], tab[(32 * r + k2) * 512 + t]);   // W_N^(t (4 k2 + r))
     }
     __syncthreads();
-    if (SDRGPU_1P_DBG & 2) return;
     // stage 2: (k2, t0) = (t >> 4, t & 15)
     {
         const int k2 = t >> 4, t0 = t & 15;
@@ -1108,9 +1174,7 @@ __global__ __launch_bounds__(512) void fft_1p_kernel(const float2* __restrict__ 
         for (int q1 = 0; q1 < 32; q1++) lds[k2 * RS + 17 * q1 + sw] = a[q1];
     }
     __syncthreads();
-    if (SDRGPU_1P_DBG & 4) return;
     // stage 3: (k2, q1) = (p & 31, p >> 5), p = t, t + 512
-    float* of = out + ((long long)f << 16);
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const int p = t + 512 * h, k2 = p & 31, q1 = p >> 5, sw = (k2 >> 1) & 15;
@@ -1872,11 +1936,13 @@ static bool zoom_fusable(const FftPlan& p, int zoomSize) {
 template <bool ZM, bool VFO>
 static int launch_1p(FftPlan& p, const float2* in, long long stride, int frames, float* out, float* zoom, VfoWork v,
                      hipStream_t s) {
-    auto k = fft_1p_kernel<ZM, VFO>;
-    SDRGPU_CHECK(set_lds(k, op1::LDS_BYTES));
+    const bool half = p.onepass == 2;
+    auto k = half ? fft_1p_kernel<ZM, VFO, true> : fft_1p_kernel<ZM, VFO, false>;
+    const int ldsB = half ? (16 * op1::RS + 512 + 32) * 8 : op1::LDS_BYTES;
+    SDRGPU_CHECK(set_lds(k, ldsB));
     if (ZM) SDRGPU_CHECK(p.zpart.ensure(sizeof(float) * 4 * 2048 * (size_t)frames));
     const int g = 32 * ((frames + 7) / 8) + (VFO && v.hist ? 1 : 0);
-    hipLaunchKernelGGL(k, dim3(g), dim3(512), op1::LDS_BYTES, s, in, stride, frames, p.win.as<float>(), p.nz,
+    hipLaunchKernelGGL(k, dim3(g), dim3(512), ldsB, s, in, stride, frames, p.win.as<float>(), p.nz,
                        p.tab1p.as<float2>(), p.tab1p64.as<double2>(), out, ZM ? p.zpart.as<float>() : nullptr, v);
     SDRGPU_HIP(hipGetLastError());
     if (ZM) {
