@@ -1003,6 +1003,9 @@ __device__ __forceinline__ void dft32(float2* v) {
 #ifndef SDRGPU_1P_PB
 #define SDRGPU_1P_PB 4   // sample rows per load batch
 #endif
+#ifndef SDRGPU_1P_VFO_LAST
+#define SDRGPU_1P_VFO_LAST 0   // (A/B) the VFO quarter after the transform instead of before it
+#endif
 #ifndef SDRGPU_1P_PB2
 #define SDRGPU_1P_PB2 2   // (HALF) sample rows per load batch at the 128-VGPR budget
 #endif
@@ -1026,7 +1029,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
     const int b = blockIdx.x, k = b >> 3;
     const int f = 8 * (k >> 2) + (b & 7), r = k & 3;
     if (f >= frames) return;
-    if constexpr (VFO) vfo_quarter_block(v, f, r);
+    if constexpr (VFO && !SDRGPU_1P_VFO_LAST) vfo_quarter_block(v, f, r);
     const int t = threadIdx.x;
     float2* tw512 = lds + TW512;
     float2* w128 = lds + W128;
@@ -1145,6 +1148,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
             }
             if (h == 0) __syncthreads();   // (stage 3's reads before the next rows land)
         }
+        if constexpr (VFO && SDRGPU_1P_VFO_LAST) vfo_quarter_block(v, f, r);
         return;
     }
     if constexpr (SDRGPU_1P_TW == 1) {
@@ -1200,6 +1204,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
             zp[128] = dv[1];
         }
     }
+    if constexpr (VFO && SDRGPU_1P_VFO_LAST) vfo_quarter_block(v, f, r);
 }
 
 // zoom[f][o] = max over the four workgroups' partial maxima (fft_1p_kernel's ZM)
