@@ -1003,6 +1003,9 @@ __device__ __forceinline__ void dft32(float2* v) {
 #ifndef SDRGPU_1P_PB
 #define SDRGPU_1P_PB 4   // sample rows per load batch
 #endif
+#ifndef SDRGPU_1P_WIDE
+#define SDRGPU_1P_WIDE 0
+#endif
 #ifndef SDRGPU_1P_VFO_LAST
 #define SDRGPU_1P_VFO_LAST 0   // (A/B) the VFO quarter after the transform instead of before it
 #endif
@@ -1075,7 +1078,55 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
             __builtin_amdgcn_sched_barrier(0);
         }
     };
-    if (nz >= 65536) {   // no zero padding (workgroup-uniform): the row offset rides in soffset
+    // SDRGPU_1P_WIDE: half the load instructions (the vmcnt cap of 63 per wave bounds the bytes in
+    // flight): lanes 2u and 2u + 1 load rows i and i + 1 of the adjacent sample pair (t, t + 1) as one
+    // 16-B load each (8-B for the window) and swap the halves the other lane needs (DPP)
+    auto pipeline2 = [&](auto&& ld2) {
+        constexpr int PP = PB / 2;
+        const int lane = t & 63;
+        const bool odd = (t & 1) != 0;
+        float4 xr[2][PP][4];
+        float2 wr[2][PP][4];
+        auto issue = [&](int bb, float4 (&xb)[PP][4], float2 (&wb)[PP][4]) {
+#pragma unroll
+            for (int pp = 0; pp < PP; pp++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) ld2(512 * (PB * bb + 2 * pp) + M * j, xb[pp][j], wb[pp][j]);
+        };
+        issue(0, xr[0], wr[0]);
+#pragma unroll
+        for (int bb = 0; bb < NB; bb++) {
+            if (bb + 1 < NB) issue(bb + 1, xr[(bb + 1) & 1], wr[(bb + 1) & 1]);
+#pragma unroll
+            for (int pp = 0; pp < PP; pp++) {
+                float2 x0[4], x1[4];
+                float w0[4], w1[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    // even lane: (x(t, i), x(t + 1, i)); odd lane: (x(t - 1, i + 1), x(t, i + 1))
+                    const float4 X = xr[bb & 1][pp][j];
+                    const float2 Wv = wr[bb & 1][pp][j];
+                    const float r0 = xchg<1>(odd ? X.x : X.z, lane), r1 = xchg<1>(odd ? X.y : X.w, lane);
+                    x0[j] = odd ? make_float2(r0, r1) : make_float2(X.x, X.y);
+                    x1[j] = odd ? make_float2(X.z, X.w) : make_float2(r0, r1);
+                    const float rw = xchg<1>(odd ? Wv.x : Wv.y, lane);
+                    w0[j] = odd ? rw : Wv.x;
+                    w1[j] = odd ? Wv.y : rw;
+                }
+                combine(PB * bb + 2 * pp, x0, w0);
+                combine(PB * bb + 2 * pp + 1, x1, w1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    if (SDRGPU_1P_WIDE && nz >= 65536 && ((uintptr_t)xf & 15) == 0) {
+        const __amdgpu_buffer_rsrc_t rx = brsrc(xf, 65536u * 8u), rw = brsrc(win, 65536u * 4u);
+        const int o = t + 511 * (t & 1);   // the pair's first sample, in row i (even lane) or i + 1 (odd lane)
+        pipeline2([&](int n0, float4& xo, float2& wo) {
+            xo = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, o * 8, n0 * 8, 0));
+            wo = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rw, o * 4, n0 * 4, 0));
+        });
+    } else if (nz >= 65536) {   // no zero padding (workgroup-uniform): the row offset rides in soffset
         const __amdgpu_buffer_rsrc_t rx = brsrc(xf, 65536u * 8u), rw = brsrc(win, 65536u * 4u);
         pipeline([&](int n0, float2& xo, float& wo) {
             xo = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, t * 8, n0 * 8, 0));
