@@ -1003,6 +1003,12 @@ __device__ __forceinline__ void dft32(float2* v) {
 #ifndef SDRGPU_1P_PB
 #define SDRGPU_1P_PB 4   // sample rows per load batch
 #endif
+#ifdef SDRGPU_1P_TIMING   // (measurement builds) per-workgroup phase timestamps, wave 0
+__device__ unsigned long long g_1p_t[16384 * 8];
+#define T1P(k) do { if (threadIdx.x == 0 && blockIdx.x < 16384) g_1p_t[blockIdx.x * 8 + (k)] = clock64(); } while (0)
+#else
+#define T1P(k) do {} while (0)
+#endif
 #ifndef SDRGPU_1P_WIDE
 #define SDRGPU_1P_WIDE 0
 #endif
@@ -1032,7 +1038,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
     const int b = blockIdx.x, k = b >> 3;
     const int f = 8 * (k >> 2) + (b & 7), r = k & 3;
     if (f >= frames) return;
+    T1P(0);
     if constexpr (VFO && !SDRGPU_1P_VFO_LAST) vfo_quarter_block(v, f, r);
+    T1P(1);
     const int t = threadIdx.x;
     float2* tw512 = lds + TW512;
     float2* w128 = lds + W128;
@@ -1139,6 +1147,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
             wo = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, (t + n0) * 4, 0, 0));
         });
     }
+    T1P(2);
     __syncthreads();   // (w128, tw512)
 #pragma unroll
     for (int i = 1; i < 32; i++) z[i] = cmul(z[i], w128[i]);   // W_128^(r i) = W_N^(512 r i)
@@ -1214,6 +1223,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
         for (int k2 = 0; k2 < 32; k2++) lds[k2 * RS + pad16(t)] = cmul(z[k2], tab[(32 * r + k2) * 512 + t]);   // W_N^(t (4 k2 + r))
     }
     __syncthreads();
+    T1P(3);
     // stage 2: (k2, t0) = (t >> 4, t & 15)
     {
         const int k2 = t >> 4, t0 = t & 15;
@@ -1229,6 +1239,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
         for (int q1 = 0; q1 < 32; q1++) lds[k2 * RS + 17 * q1 + sw] = a[q1];
     }
     __syncthreads();
+    T1P(4);
     // stage 3: (k2, q1) = (p & 31, p >> 5), p = t, t + 512
 #pragma unroll
     for (int h = 0; h < 2; h++) {
@@ -1255,8 +1266,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
             zp[128] = dv[1];
         }
     }
+    T1P(5);
     if constexpr (VFO && SDRGPU_1P_VFO_LAST) vfo_quarter_block(v, f, r);
 }
+#ifdef SDRGPU_1P_TIMING
+extern "C" int sdrgpu_debug_1p_times(unsigned long long* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_1p_t), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // zoom[f][o] = max over the four workgroups' partial maxima (fft_1p_kernel's ZM)
 __global__ __launch_bounds__(256) void fft_1p_zoom_kernel(const float* __restrict__ zpart, int frames, float* __restrict__ zoom) {
