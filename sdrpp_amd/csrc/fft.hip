@@ -1009,6 +1009,9 @@ __device__ unsigned long long g_1p_t[16384 * 8];
 #else
 #define T1P(k) do {} while (0)
 #endif
+#ifndef SDRGPU_1P_VFO_UNROLL
+#define SDRGPU_1P_VFO_UNROLL 0   // (A/B) fft_1p256_kernel's two stage-1 segments per lane group unrolled
+#endif
 #ifndef SDRGPU_1P_WIDE
 #define SDRGPU_1P_WIDE 0
 #endif
@@ -1154,7 +1157,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
     dft32(z);
     float* of = out + ((long long)f << 16);
     if constexpr (HALF) {
-        static_assert(SDRGPU_1P_TW == 1, "HALF: fp64-recurrence twiddles");
         double2 c = tab64[t * r];   // (loaded here: at 128 VGPRs they do not stay live through the loads)
         st = tab64[4 * t];
 #pragma unroll
@@ -1274,6 +1276,162 @@ extern "C" int sdrgpu_debug_1p_times(unsigned long long* host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_1p_t), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : -1;
 }
 #endif
+
+// SDRGPU_FFT_1P=3: the half-image transform with 256-thread workgroups (2 per CU at 76 KB of LDS and up
+// to 256 VGPRs each: one workgroup's loads wait while the other one computes). Thread t takes the stage-1
+// columns t and t + 256; stages 2 and 3 as in the HALF mode (the 256 threads are stage 2's butterflies).
+// SV (SDRGPU_FFT_1P=4): the VFO quarters as workgroups of their own, a frame's 4 quarters dispatched
+// before its 4 transform workgroups on the same XCD (they fetch the frame; the transforms read it from L2)
+template <bool ZM, bool VFO, bool SV = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void fft_1p256_kernel(const float2* __restrict__ in, long long frameStride, int frames,
+                                                        const float* __restrict__ win, int nz, const float2* __restrict__ tab,
+                                                        const double2* __restrict__ tab64, float* __restrict__ out,
+                                                        float* __restrict__ zpart, VfoWork v) {
+    using op1::M;
+    using op1::RS;
+    constexpr int TW512 = 16 * RS, W128 = TW512 + 512;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    if constexpr (VFO) {
+        if (v.hist && blockIdx.x == gridDim.x - 1) {   // the stage's history carry (fir.h:80)
+            (void)fir_hist_block<float2, true, false>(v.a);
+            return;
+        }
+    }
+    const int b = blockIdx.x, k = b >> 3;
+    const int kq = SV ? (k & 7) : (k & 3) + 4;
+    const int f = 8 * (SV ? k >> 3 : k >> 2) + (b & 7), r = kq & 3;
+    if (f >= frames) return;
+    const int t = threadIdx.x;
+    if constexpr (VFO) {   // quarter r of the stage: 16 segments, 8 per pass of the 4 waves
+      if (!SV || kq < 4) {
+        const int lane = t & 63, wave = t >> 6;
+#if SDRGPU_1P_VFO_UNROLL
+#pragma unroll
+#else
+#pragma unroll 1
+#endif
+        for (int sub = 0; sub < 2; sub++)
+            fir_rows_segment<32, 5, true, false, 32, 32, true>(
+                v.a, (long long)(v.frame0 + f) * 64 + r * 16 + sub * 8 + wave * 2 + (lane >> 5), lane);
+        if (SV) return;
+      }
+    }
+    lds[TW512 + t] = tab[4 * M + t];
+    lds[TW512 + 256 + t] = tab[4 * M + 256 + t];
+    if (t < 32) lds[W128 + t] = tab[4 * M + 512 + 32 * r + t];
+    const float s = (r & 1) ? -1.0f : 1.0f;
+    const float fx = r == 0 ? 1.0f : (r == 2 ? -1.0f : 0.0f), fy = r == 1 ? -1.0f : (r == 3 ? 1.0f : 0.0f);
+    const float2* xf = in + (long long)f * frameStride;
+    float2 z[2][32];
+    auto combine = [&](int u, int i, const float2 (&xv)[4], const float (&wv)[4]) {
+        float2 uu[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) uu[j] = make_float2(xv[j].x * wv[j], xv[j].y * wv[j]);
+        const float2 a = make_float2(fmaf(s, uu[2].x, uu[0].x), fmaf(s, uu[2].y, uu[0].y));
+        const float2 q = make_float2(fmaf(s, uu[3].x, uu[1].x), fmaf(s, uu[3].y, uu[1].y));
+        z[u][i] = make_float2(a.x + (fx * q.x - fy * q.y), a.y + (fx * q.y + fy * q.x));
+    };
+    constexpr int NB = 32;   // one sample row (both columns, four quarters) per batch
+    auto pipeline = [&](auto&& ld) {
+        float2 xv[2][2][4];
+        float wv[2][2][4];
+        auto issue = [&](int i, float2 (&xb)[2][4], float (&wb)[2][4]) {
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) ld(256 * u + 512 * i + M * j, xb[u][j], wb[u][j]);
+        };
+        issue(0, xv[0], wv[0]);
+#pragma unroll
+        for (int i = 0; i < NB; i++) {
+            if (i + 1 < NB) issue(i + 1, xv[(i + 1) & 1], wv[(i + 1) & 1]);
+#pragma unroll
+            for (int u = 0; u < 2; u++) combine(u, i, xv[i & 1][u], wv[i & 1][u]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    if (nz >= 65536) {
+        const __amdgpu_buffer_rsrc_t rx = brsrc(xf, 65536u * 8u), rw = brsrc(win, 65536u * 4u);
+        pipeline([&](int n0, float2& xo, float& wo) {
+            xo = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, t * 8, n0 * 8, 0));
+            wo = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, t * 4, n0 * 4, 0));
+        });
+    } else {
+        const __amdgpu_buffer_rsrc_t rx = brsrc(xf, (unsigned)nz * 8u), rw = brsrc(win, (unsigned)nz * 4u);
+        pipeline([&](int n0, float2& xo, float& wo) {
+            xo = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, (t + n0) * 8, 0, 0));
+            wo = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, (t + n0) * 4, 0, 0));
+        });
+    }
+    __syncthreads();   // (the LDS tables)
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        const int tu = t + 256 * u;
+#pragma unroll
+        for (int i = 1; i < 32; i++) z[u][i] = cmul(z[u][i], lds[W128 + i]);
+        dft32(z[u]);
+        if constexpr (SDRGPU_1P_TW == 1) {
+            double2 c = tab64[tu * r];
+            const double2 st = tab64[4 * tu];
+#pragma unroll
+            for (int k2 = 0; k2 < 32; k2++) {
+                z[u][k2] = cmul(z[u][k2], make_float2((float)c.x, (float)c.y));
+                if (k2 < 31) c = zmul(c, st);
+            }
+        } else {
+#pragma unroll
+            for (int k2 = 0; k2 < 32; k2++) z[u][k2] = cmul(z[u][k2], tab[(32 * r + k2) * 512 + tu]);
+        }
+    }
+    float* of = out + ((long long)f << 16);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int kl = 0; kl < 16; kl++) lds[kl * RS + pad16(t + 256 * u)] = z[u][16 * h + kl];
+        __syncthreads();
+        {   // stage 2: (kl, t0) = (t >> 4, t & 15)
+            const int kl = t >> 4, t0 = t & 15, k2 = 16 * h + kl;
+            float2 a[32];
+#pragma unroll
+            for (int t1 = 0; t1 < 32; t1++) a[t1] = lds[kl * RS + t0 + 17 * t1];
+            dft32(a);
+#pragma unroll
+            for (int q1 = 1; q1 < 32; q1++) a[q1] = cmul(a[q1], lds[TW512 + 16 * q1 + t0]);
+            __syncthreads();
+            const int sw = t0 ^ ((k2 >> 1) & 15);
+#pragma unroll
+            for (int q1 = 0; q1 < 32; q1++) lds[kl * RS + 17 * q1 + sw] = a[q1];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 2; e++) {   // stage 3: (kl, q1) = (p & 15, p >> 4), p = t, t + 256
+            const int p = t + 256 * e, kl = p & 15, q1 = p >> 4, k2 = 16 * h + kl, sw = (k2 >> 1) & 15;
+            float2 c3[16];
+#pragma unroll
+            for (int t0 = 0; t0 < 16; t0++) c3[t0] = lds[kl * RS + 17 * q1 + (t0 ^ sw)];
+            dft16(c3);
+            float dv[16];
+#pragma unroll
+            for (int q2 = 0; q2 < 16; q2++) {
+                dv[q2] = db_of(c3[q2]);
+                of[4 * (k2 + 32 * q1 + 1024 * q2) + r] = dv[q2];
+            }
+            if constexpr (ZM) {
+                const int lane = t & 63;
+                tr_step<1, 8>(dv, lane);
+                tr_step<2, 4>(dv, lane);
+                tr_step<4, 2>(dv, lane);
+                const int q2 = ((lane & 1) << 3) | ((lane & 2) << 1) | (lane & 4) >> 1;
+                float* zp = zpart + ((long long)(4 * f + r) << 11) + (k2 >> 3) + 4 * q1 + 128 * q2;
+                zp[0] = dv[0];
+                zp[128] = dv[1];
+            }
+        }
+        if (h == 0) __syncthreads();
+    }
+}
 
 // zoom[f][o] = max over the four workgroups' partial maxima (fft_1p_kernel's ZM)
 __global__ __launch_bounds__(256) void fft_1p_zoom_kernel(const float* __restrict__ zpart, int frames, float* __restrict__ zoom) {
@@ -2009,13 +2167,14 @@ static bool zoom_fusable(const FftPlan& p, int zoomSize) {
 template <bool ZM, bool VFO>
 static int launch_1p(FftPlan& p, const float2* in, long long stride, int frames, float* out, float* zoom, VfoWork v,
                      hipStream_t s) {
-    const bool half = p.onepass == 2;
-    auto k = half ? fft_1p_kernel<ZM, VFO, true> : fft_1p_kernel<ZM, VFO, false>;
+    const bool half = p.onepass >= 2, w256 = p.onepass >= 3, sv = VFO && p.onepass == 4;
+    auto k = sv ? fft_1p256_kernel<ZM, VFO, true> : w256 ? fft_1p256_kernel<ZM, VFO> : half ? fft_1p_kernel<ZM, VFO, true>
+                                                                                             : fft_1p_kernel<ZM, VFO, false>;
     const int ldsB = half ? (16 * op1::RS + 512 + 32) * 8 : op1::LDS_BYTES;
     SDRGPU_CHECK(set_lds(k, ldsB));
     if (ZM) SDRGPU_CHECK(p.zpart.ensure(sizeof(float) * 4 * 2048 * (size_t)frames));
-    const int g = 32 * ((frames + 7) / 8) + (VFO && v.hist ? 1 : 0);
-    hipLaunchKernelGGL(k, dim3(g), dim3(512), ldsB, s, in, stride, frames, p.win.as<float>(), p.nz,
+    const int g = (sv ? 64 : 32) * ((frames + 7) / 8) + (VFO && v.hist ? 1 : 0);
+    hipLaunchKernelGGL(k, dim3(g), dim3(w256 ? 256 : 512), ldsB, s, in, stride, frames, p.win.as<float>(), p.nz,
                        p.tab1p.as<float2>(), p.tab1p64.as<double2>(), out, ZM ? p.zpart.as<float>() : nullptr, v);
     SDRGPU_HIP(hipGetLastError());
     if (ZM) {
