@@ -1012,6 +1012,9 @@ __device__ unsigned long long g_1p_t[16384 * 8];
 #ifndef SDRGPU_1P_VFO_UNROLL
 #define SDRGPU_1P_VFO_UNROLL 0   // (A/B) fft_1p256_kernel's two stage-1 segments per lane group unrolled
 #endif
+#ifndef SDRGPU_1P_NT
+#define SDRGPU_1P_NT 0   // (A/B) fft_1p256_kernel's dB rows as streaming stores
+#endif
 #ifndef SDRGPU_1P_WIDE
 #define SDRGPU_1P_WIDE 0
 #endif
@@ -1416,7 +1419,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
 #pragma unroll
             for (int q2 = 0; q2 < 16; q2++) {
                 dv[q2] = db_of(c3[q2]);
-                of[4 * (k2 + 32 * q1 + 1024 * q2) + r] = dv[q2];
+                if constexpr (SDRGPU_1P_NT) __builtin_nontemporal_store(dv[q2], &of[4 * (k2 + 32 * q1 + 1024 * q2) + r]);
+                else of[4 * (k2 + 32 * q1 + 1024 * q2) + r] = dv[q2];
             }
             if constexpr (ZM) {
                 const int lane = t & 63;
