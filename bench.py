@@ -116,8 +116,9 @@ class C5:
         (sdrgpu_fft_group_times), or None when the group is timed by the bench's events."""
         if not self.fuse:
             return None
-        t = self.fft.group_times(steps)
-        return float(np.mean(t)) if len(t) == steps else None
+        n = min(steps, 256)   # the library keeps the last 256 calls' events (all of them timed steps here)
+        t = self.fft.group_times(n)
+        return float(np.mean(t)) if len(t) == n else None
 
 
 class C2:
@@ -448,6 +449,8 @@ def run_config(config, a, shard, dev, stream, rt=None, workloads=None):
     kern_ms = sum(sum(e0.elapsed_time(e1) for e0, e1 in evs) for evs in ev) / max(len(ev), 1)
     if hasattr(wl, "group_ms") and wl.group_ms(a.steps) is not None:
         kern_ms = wl.group_ms(a.steps)
+    if not kern_ms > 0:
+        raise RuntimeError(f"{config}: no kernel time recorded for the dominant group (steps {a.steps})")
     elapsed, kern_ms = shard.max_over_ranks([elapsed, kern_ms], device=rt.reduce_device)
     if pipe is not None:
         # the first multi-GPU run proves the gather: rank 0's received rows of the last step carry
@@ -668,4 +671,13 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except sdrpp_amd.SdrGpuError as e:
+        # a peer rank that died or stalled (gather deadline, communicator aborted: sdrgpu_gather_*)
+        # or any other library failure: report it and leave at once with a non-zero status, without
+        # the interpreter's teardown (process-group destroy, device synchronise), which could block
+        # on the peer that is gone
+        rank = os.environ.get("RANK", "0")
+        print(f"bench.py rank {rank}: {e}", file=sys.stderr, flush=True)
+        os._exit(3)

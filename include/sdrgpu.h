@@ -45,7 +45,8 @@ enum {
     SDRGPU_EHIP = -2,     /* HIP runtime error (name in sdrgpu_last_error) */
     SDRGPU_ENOMEM = -3,
     SDRGPU_ESTATE = -4,   /* wrong handle kind / not initialised */
-    SDRGPU_ENODEV = -5
+    SDRGPU_ENODEV = -5,
+    SDRGPU_ETIMEOUT = -6  /* a peer rank did not answer within the deadline (gather: communicator aborted) */
 };
 
 /* element types (dsp::complex_t is {float re, im}, dsp/types.h:6; stereo_t {float l, r}) */
@@ -114,10 +115,6 @@ int sdrgpu_fft_execute_zoom_vfo_dev(sdrgpu_fft* h, const void* in, int frames, f
  * min(n, calls, 256) group times in ms, oldest first, waiting for them */
 int sdrgpu_fft_set_timing(sdrgpu_fft* h, int on);
 int sdrgpu_fft_group_times(sdrgpu_fft* h, float* ms, int n);
-/* Diagnostics of the persistent spectrum + VFO launch (tuning SDRGPU_FFT_VFO_PERSIST): the number
- * of bounded dependency waits that timed out in the last call of `frames` frames (0 = every
- * dependency was met). Synchronises the device. */
-int sdrgpu_fft_persist_errors(sdrgpu_fft* h, int frames);
 /* drop-in for IQFrontEnd::handler: in = host complex_t[nz]; out = host float[N] or NULL
  * (acquireFFTBuffer may return NULL; the spectrum is then computed but not written). */
 int sdrgpu_fft_logmag(sdrgpu_fft* h, const void* in, float* out);
@@ -262,8 +259,15 @@ int sdrgpu_frontend_release(sdrgpu_frontend* f, int ticket);
 #define SDRGPU_GATHER_ID_BYTES 128
 typedef struct sdrgpu_gather sdrgpu_gather;
 int sdrgpu_gather_get_id(void* id /* SDRGPU_GATHER_ID_BYTES */);
+/* Every wait on the peers has a deadline (SDRGPU_GATHER_TIMEOUT_S, default 120 s; set_timeout per
+ * handle): create and rows poll the non-blocking communicator, wait polls `stream`; on expiry the
+ * communicator is aborted and the call returns SDRGPU_ETIMEOUT naming the rank (the reference never
+ * blocks forever on a stopped peer either: utils/threading.h:53-62, dsp/stream.h:94-116). After a
+ * failure the handle accepts only destroy. create's device < 0: the thread's current device. */
 int sdrgpu_gather_create(sdrgpu_gather** g, int device, int rank, int world, const void* id);
+int sdrgpu_gather_set_timeout(sdrgpu_gather* g, double seconds);
 int sdrgpu_gather_rows(sdrgpu_gather* g, const float* rows, long long count, float* out, void* stream);
+int sdrgpu_gather_wait(sdrgpu_gather* g, void* stream, double timeoutS /* <= 0: the handle's */);
 int sdrgpu_gather_destroy(sdrgpu_gather* g);
 
 /* ---------------------------------------------- spectrum/IQ consumers ---- */

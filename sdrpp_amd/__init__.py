@@ -69,7 +69,6 @@ def _load():
         "sdrgpu_fft_execute_zoom_vfo_dev": (i, [vp, vp, i, vp, vp, i, vp, vp, vp]),
         "sdrgpu_fft_set_timing": (i, [vp, i]),
         "sdrgpu_fft_group_times": (i, [vp, fp, i]),
-        "sdrgpu_fft_persist_errors": (i, [vp, i]),
         "sdrgpu_fft_execute_zoom_dev": (i, [vp, vp, ll, i, vp, vp, i, vp]),
         "sdrgpu_fft_logmag": (i, [vp, vp, vp]),
         "sdrgpu_fft_size": (i, [vp]),
@@ -92,6 +91,8 @@ def _load():
         "sdrgpu_gather_get_id": (i, [vp]),
         "sdrgpu_gather_create": (i, [pp, i, i, i, vp]),
         "sdrgpu_gather_rows": (i, [vp, vp, ll, vp, vp]),
+        "sdrgpu_gather_set_timeout": (i, [vp, d]),
+        "sdrgpu_gather_wait": (i, [vp, vp, d]),
         "sdrgpu_gather_destroy": (i, [vp]),
         "sdrgpu_ddc_fm_create": (i, [pp, i, d, fp, i, i, d]),
         "sdrgpu_fm_create": (i, [pp, i, d, d, i, i]),

@@ -1279,14 +1279,12 @@ struct ChainBlock : Block {
         int off[TAIL_MAXS] = {}, H[TAIL_MAXS] = {}, Q[TAIL_MAXS] = {}, D[TAIL_MAXS] = {};
         int G = 0, maxEl = 0;
     } tailCache;
-    int tailVar = 0;                             // SDRGPU_TAIL_VAR (tuning, timing only): 1 no stage loops, 2 no image loads
     // The tail launch's arguments for kids[1..] on n0 samples of kid 0's output: 1 (t, f, lds
     // filled), 0 (not applicable: the per-kid path runs).
     int tail_plan(int n0, TailArgs& t, FirBlock** f, size_t& lds) {
         if (tailMode < 0) {
             const char* e = tuning_env("SDRGPU_VFO_TAIL");
             tailMode = e ? atoi(e) : 2;
-            if (const char* v = tuning_env("SDRGPU_TAIL_VAR")) tailVar = atoi(v);
             if (const char* v = tuning_env("SDRGPU_TAIL_OUT")) tailBigOut = std::max(8, atoi(v));
         }
         const int S = (int)kids.size() - 1;
@@ -1365,7 +1363,6 @@ struct ChainBlock : Block {
         if (tapF > 2 * TAIL_NT) return 0;                 // two tap loads per thread
         lds = sizeof(float2) * (size_t)maxEl + sizeof(float) * (size_t)tapF;
         if (lds > 64 * 1024) return 0;
-        t.var = tailVar;
         return 1;
     }
     // the tail launch over kid 0's output s1 (n0 samples) into out, and the kids' state update
@@ -1588,13 +1585,15 @@ int vfo_tail_prepare(sdrgpu_block* vfo, const VfoStage1& st, void* out, TailArgs
     FirBlock* f[TAIL_MAXS];
     const int ok = c->tail_plan(st.M, *t, f, *lds);
     if (ok <= 0) return ok;
-    dynamic_cast<FirBlock*>(c->kids[0].get())->rows_commit(st.count, st.M);
     t->in = reinterpret_cast<const float2*>(st.out);
     t->out = reinterpret_cast<float2*>(out);
     return 1;
 }
-int vfo_tail_commit(sdrgpu_block* vfo, const TailArgs& t) {
+// called once the launches that carry stage 1 and the tail are in: only then does any stage's state
+// move on (a failed launch leaves the VFO as it was, as the header promises)
+int vfo_tail_commit(sdrgpu_block* vfo, const VfoStage1& st, const TailArgs& t) {
     auto* c = dynamic_cast<ChainBlock*>(vfo->impl);
+    dynamic_cast<FirBlock*>(c->kids[0].get())->rows_commit(st.count, st.M);
     for (int i = 0; i < t.S; i++) {   // FirBlock::run's state update (as launch_tail)
         auto* f = dynamic_cast<FirBlock*>(c->kids[i + 1].get());
         f->cur ^= 1;

@@ -411,85 +411,46 @@ __global__ __launch_bounds__(S / 2 * L / 16) void fft_passA2_kernel(
     passA2_tile<L, S>(lds, blockIdx.x, in, frameStride, frames, win, nz, N2, logN, tw, tfull, scratch);
 }
 
-// ---- 1M pass A, persistent and software-pipelined (N1 = 1024, paired columns) --------------
-// The 1M column FFT needs S x 1024 x 8 B of LDS per tile (139 KB at S = 16), so one workgroup per
-// CU: in the one-shot kernel above each CU alternates "load the tile" and "transform + store it",
-// and HBM idles during the transform. Here a CU's workgroup walks tiles blockIdx.x, +gridDim.x, ...
-// and issues the next tile's input + window loads (96 VGPRs) before it transforms the current one,
-// so the loads fly during the LDS stages and the stores. The stage twiddles are staged in LDS once
-// per workgroup, and the four-step twiddle W_N^(c k1) is generated in fp64 and rounded once
-// (the same single rounding as the table it replaces): for column c and this thread's outputs
-// k1 = t + 64 m, W^(c t) and W^(64 c) come from two 256-entry fp64 tables (W_N^(256 j), W_N^j;
-// c t, 64 c < 2^16) and W^(c (t + 64 m)) = W^(c t) (W^(64 c))^m by an fp64 recurrence over m
-// (15 products: relative error ~1e-15, far below the fp32 rounding). That removes the 8 MB
-// [k1][n2] table read (8 B per sample of L2 / Infinity-Cache traffic).
-typedef float nt_f4 __attribute__((ext_vector_type(4)));
-typedef float nt_f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float4 nt_load4(const float2* p) {   // streaming (non-temporal) 16-B load
-    const nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ float2 nt_load2(const float2* p) {
-    const nt_f2 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f2*>(p));
-    return make_float2(v.x, v.y);
-}
+// ---- 1M passes (N1 = N2 = 1024), persistent and software-pipelined ----------------------------
+// The 1M column FFT needs 16 x 1024 x 8 B of LDS per tile (139 KB), so one workgroup per CU: in a
+// one-shot kernel each CU alternates "load the tile" and "transform + store it", and HBM idles during
+// the transform. Here each CU's workgroup walks tiles blockIdx.x, +gridDim.x, ... and issues the next
+// tile's input + window loads (96 VGPRs) before it transforms the current one, so the loads fly
+// during the LDS stages and the stores. The stage twiddles are staged in LDS once per workgroup, and
+// the four-step twiddle W_N^(c k1) is generated in fp64 and rounded once (the same single rounding as
+// a table): for column c and this thread's outputs k1 = t + 64 m, W^(c t) and W^(64 c) come from two
+// 256-entry fp64 tables (W_N^(256 j), W_N^j; c t, 64 c < 2^16) and W^(c (t + 64 m)) = W^(c t)
+// (W^(64 c))^m by an fp64 recurrence over m (15 products: relative error ~1e-15, far below the fp32
+// rounding). That removes the 8 MB [k1][n2] table read (8 B per sample of L2 / Infinity-Cache
+// traffic). Measured alternatives (rounds 2-4; kept in git history, not here): 8-column
+// tiles (2.24-2.70 ms), spill-free laundered offsets (same time), the merged pass-B(c-1) + pass-A(c)
+// launches (1.80 vs 1.73 ms), two workgroups per CU (2.16 ms).
 __device__ __forceinline__ double2 zmul(double2 a, double2 b) {
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
-typedef unsigned bu2 __attribute__((ext_vector_type(2)));
 typedef unsigned bu4 __attribute__((ext_vector_type(4)));
 
-// the radix-16 middle stage (NS = 16) of the 1M pass A for one column, thread t: read + twiddle +
-// DFT into v, then (after the caller's barrier) the in-place write
-__device__ __forceinline__ void mid16_read(const float2* seq, const float2* tw16, int t, float2 (&v)[16]) {
-    constexpr int L = 1024;
-    const int jm = t % 16;
-#pragma unroll
-    for (int r = 0; r < 16; r++) v[r] = seq[pad16s<L / 16>(t, r)];
-#pragma unroll
-    for (int r = 1; r < 16; r++) v[r] = cmul(v[r], tw16[16 * r + jm]);   // (stage_lds's tw16 layout)
-    dft16(v);
-}
-__device__ __forceinline__ void mid16_write(float2* seq, int t, const float2 (&v)[16]) {
-    const int idxD = (t / 16) * 256 + (t % 16);
-#pragma unroll
-    for (int r = 0; r < 16; r++) seq[pad16s<16>(idxD, r)] = v[r];
-}
-
-// tile -> (frame, block) of the persistent 1M passes. G (the grid, a multiple of 8 G8 and of 8) > 1
-// groups G8 adjacent blocks on one XCD at once: workgroups x, x + 8, ... (same XCD, same round)
-// take blocks b, b + 1, ..., whose row / dB segments share 128-B lines (64-B pass-A segments at 8
-// columns, 32-B dB segments at 8 rows), so a line is filled / written whole in one L2.
+// tile -> (frame, block) of the 1M pass B: G8 adjacent row blocks on one XCD at once. Workgroups x,
+// x + 8, ... (same XCD, same round) take blocks b, b + 1, ..., whose 32-B dB segments share 128-B
+// lines, so a line is written whole in one L2.
 template <int G8>
 __device__ __forceinline__ void tile_fb(int T, int nb, int& b, long long& f) {
-    if constexpr (G8 <= 1) {
-        b = T % nb;
-        f = T / nb;
-    } else {
-        const int g = T / (8 * G8), w = T % (8 * G8);
-        const int P = g * 8 + (w & 7), h = w >> 3;
-        const int npf = nb / G8;
-        f = P / npf;
-        b = G8 * (P % npf) + h;
-    }
+    const int g = T / (8 * G8), w = T % (8 * G8);
+    const int P = g * 8 + (w & 7), h = w >> 3;
+    const int npf = nb / G8;
+    f = P / npf;
+    b = G8 * (P % npf) + h;
 }
 
-// VAR (tuning, SDRGPU_FFT_1M_VAR): bit 0 middle stage one column at a time, bit 3 row offsets
-// advanced through opaque registers (together: no spills, same time as the default, r3 A/B),
-// bit 6 XCD-grouped column blocks (S = 8); bits 4 / 5 measurement only (below). Measured and
-// removed (r3, C2 step, 3 interleaved runs, one box): the last stage + 8-B stores one column at a
-// time (2.22 vs 1.95 ms), the four-step fp64 tables staged in LDS (2.17 vs 1.95 ms).
-// ---- 1M pass B, persistent and software-pipelined (N2 = 1024) -------------------------------
-// Same transform as fft_passB_kernel<1024, S>, each workgroup walking tiles with the next tile's
-// 16 row values per thread loaded while the current tile is transformed and stored.
-template <int S, int CP, int VAR = 0>   // VAR (measurement only): 16 loads tile 0 only, 32 stores dropped
-__device__ __forceinline__ void passB_1m_body(int tile0, int step, const float2* __restrict__ scratch, int frames,
-                                              int N1, int logN, const float2* __restrict__ tw, float* __restrict__ out) {
-    constexpr int L = 1024, T = L / 16;
+// ---- 1M pass B: 8 rows of 1024 per tile (two workgroups per CU), each workgroup walking tiles with
+// the next tile's 16 row values per thread loaded while the current tile is transformed and stored.
+// The intermediate is pass A's tile-major layout [block][k1][16 columns]: a row piece of 16 columns is
+// 128 contiguous bytes. Row blocks XCD-grouped by 4 (1.93 vs 1.97 ms per C2 step; ungrouped 2.06).
+__global__ __launch_bounds__(512) void fft_passB_1m_kernel(const float2* __restrict__ scratch, int frames, int N1, int logN,
+                                                           const float2* __restrict__ tw, float* __restrict__ out) {
+    constexpr int L = 1024, T = L / 16, S = 8, XG = 4;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    constexpr int XG = (VAR & 64) ? 32 / S : 1;   // XCD grouping of row blocks (bit 6): 128-B dB lines
-    constexpr bool TMAJ = VAR & 128;              // bit 7: the tile-major intermediate of pass A at 16 columns
     float2* twl = lds + S * Lds<L>::LS;   // stage twiddles, staged once per workgroup
     float2* tw16 = twl + L;                // the middle stage's, bank-conflict-free (stage_lds)
     const int tid = threadIdx.x;
@@ -499,25 +460,22 @@ __device__ __forceinline__ void passB_1m_body(int tile0, int step, const float2*
     const int nb = N1 / S;
     const int ntiles = nb * frames;
     float2 fr[16];
-#define SDRGPU_PB1M_ISSUE(TILE)                                                                                       \
-    do {                                                                                                              \
-        int b_;                                                                                                       \
-        long long f_;                                                                                                 \
-        tile_fb<XG>((TILE), nb, b_, f_);                                                                              \
-        if (VAR & 16) { b_ = 0; f_ = 0; }                                                                             \
-        const __amdgpu_buffer_rsrc_t rs_ = brsrc(scratch + (f_ << logN), 0x7fffffffu);                                \
-        const unsigned o_ = TMAJ ? (unsigned)((tF / 16) * L * 16 + (b_ * S + sF) * 16 + tF % 16) * 8u                 \
-                                 : (unsigned)((b_ * S + sF) * L + tF) * 8u;                                            \
-        _Pragma("unroll") for (int r = 0; r < 16; r++)                                                               \
-            fr[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs_, o_, r * (TMAJ ? 4 * L * 16 * 8 : T * 8), CP)); \
-    } while (0)
-    int tile = tile0;
-    if (tile < ntiles) SDRGPU_PB1M_ISSUE(tile);
-    for (; tile < ntiles; tile += step) {
+    auto issue = [&](int tile) {
+        int b;
+        long long f;
+        tile_fb<XG>(tile, nb, b, f);
+        const __amdgpu_buffer_rsrc_t rs = brsrc(scratch + (f << logN), 0x7fffffffu);
+        const unsigned o = (unsigned)((tF / 16) * L * 16 + (b * S + sF) * 16 + tF % 16) * 8u;
+#pragma unroll
+        for (int r = 0; r < 16; r++) fr[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs, o, r * 4 * L * 16 * 8, 0));
+    };
+    int tile = blockIdx.x;
+    if (tile < ntiles) issue(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
         float2 v[16];
 #pragma unroll
         for (int r = 0; r < 16; r++) v[r] = fr[r];
-        if (tile + step < ntiles) SDRGPU_PB1M_ISSUE(tile + step);
+        if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);
         // the LDS addresses below are loop-invariant; recomputing them per tile (laundered thread
         // index) keeps ~40 hoisted address registers from spilling the prefetched tile
         int tv = tid;
@@ -529,49 +487,23 @@ __device__ __forceinline__ void passB_1m_body(int tile0, int step, const float2*
         int b;
         long long f;
         tile_fb<XG>(tile, nb, b, f);
-        const __amdgpu_buffer_rsrc_t ro = brsrc(out + (f << logN) + b * S, (VAR & 32) ? 0u : 0x7fffffffu);
+        const __amdgpu_buffer_rsrc_t ro = brsrc(out + (f << logN) + b * S, 0x7fffffffu);
         stages_rest<L, true>(lds, twl, sL2, tL2, [&](int k2, float2 y) {
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, db_of(y)), ro, (unsigned)(sL2 + N1 * k2) * 4u, 0, CP);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, db_of(y)), ro, (unsigned)(sL2 + N1 * k2) * 4u, 0, 0);
         }, tw16);
     }
 }
-#undef SDRGPU_PB1M_ISSUE
 
-template <int S, int CP, int VAR = 0>
-__global__ __launch_bounds__(S * 1024 / 16) void fft_passB_1m_kernel(const float2* __restrict__ scratch, int frames, int N1,
-                                                                    int logN, const float2* __restrict__ tw,
-                                                                    float* __restrict__ out) {
-    passB_1m_body<S, CP, VAR>(blockIdx.x, gridDim.x, scratch, frames, N1, logN, tw, out);
-}
-
-// MERGED (round 4, fft_merged_1m launches): the workgroup first runs its share of the previous
-// chunk's pass-B tiles (mb), then this pass A. Both walk tiles blockIdx.x + k gridDim.x; they share
-// nothing (pass A writes the other scratch buffer). Pass B's twiddles sit inside pass A's data
-// region: pass A's first barrier orders its first LDS write after every pass-B read. (The pass-A
-// code stays in the kernel body: moved into a device function, the compiler's allocation changed
-// and the kernel spilled 24 VGPRs.)
-struct MergeB {
-    const float2* scratch;
-    int frames, N1;
-    float* out;
-    const float2* tw;
-};
-template <int S, int CP, int VAR, bool MERGED = false>   // CP: cache-policy bits of the streaming accesses (0, or 2 = nt; tuning)
-__global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_eu(S < 16 ? 2 : 1))) void fft_passA_1m_kernel(
+// ---- 1M pass A: 16 paired columns x 1024 rows per tile, one workgroup per CU -----------------------
+// The input rows are read once: streaming (slc) loads, so they do not push the 4 MB window out of L2
+// (PMC fetch 18.15 -> 17.50 B/sample, C2 1.848 -> 1.798 ms). Each tile's 128 KB of output is written
+// contiguously in the tile-major layout [block][k1][16] (1 KB per store instruction instead of eight
+// 128-B row pieces: 1.89 vs 1.94 ms).
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void fft_passA_1m_kernel(
     const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz, int N2,
-    int logN, const float2* __restrict__ tw, const double2* __restrict__ wt, float2* __restrict__ scratch, MergeB mb) {
-    if constexpr (MERGED) {
-        if (mb.frames) passB_1m_body<8, 0, 64 | 128>(blockIdx.x, gridDim.x, mb.scratch, mb.frames, mb.N1, logN, mb.tw, mb.out);
-        if (!frames) return;
-    }
-    constexpr int L = 1024, P = S / 2, T = L / 16, NT = P * T, LS = Lds<L>::LS;
+    int logN, const float2* __restrict__ tw, const double2* __restrict__ wt, float2* __restrict__ scratch) {
+    constexpr int L = 1024, S = 16, P = S / 2, T = L / 16, NT = P * T, LS = Lds<L>::LS, CP = 2;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    constexpr bool MIDCOL = VAR & 1, LAUNDER = VAR & 8;
-    constexpr bool NOLOAD = VAR & 16, NOSTORE = VAR & 32;   // (measurement only: wrong results)
-    constexpr int XG = ((VAR & 64) && S < 16) ? 16 / S : 1;   // XCD grouping of column blocks (bit 6): 128-B row lines
-    // bit 7: tile-major intermediate [b][k1][c] (each tile's 128 KB written contiguously; pass B
-    // then reads 128-B pieces of 16 columns) instead of row-major [k1][n2]
-    constexpr bool TMAJ = VAR & 128;
     float2* twl = lds + S * LS;
     float2* tw16 = twl + L;   // the middle stage's twiddles, bank-conflict-free (stage_lds)
     const int tid = threadIdx.x;
@@ -590,33 +522,19 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_
     const int rowB = T * N2 * 8;   // bytes between rows t + 64 r and t + 64 (r + 1)
     float4 q[16];
     float2 w[16];
-    // LAUNDER: the 16 row offsets are advanced through opaque registers; left to itself the
-    // compiler may precompute all 32 and spill them, and every reload from scratch then waits
-    // (vmcnt, in order) for the prefetch loads issued before it
-#define SDRGPU_PA1M_ISSUE(TILE)                                                                                         \
-    do {                                                                                                                \
-        int b_;                                                                                                         \
-        long long f_;                                                                                                   \
-        tile_fb<XG>((TILE), nb, b_, f_);                                                                                \
-        if (NOLOAD) { b_ = 0; f_ = 0; }                                                                                 \
-        const unsigned o_ = (unsigned)(t * N2 + b_ * S + 2 * cp);                                                       \
-        const __amdgpu_buffer_rsrc_t rx_ = brsrc(in + f_ * frameStride, (unsigned)nz * 8u);                            \
-        unsigned vq_ = o_ * 8, vw_ = o_ * 4;                                                                            \
-        _Pragma("unroll") for (int r = 0; r < 16; r++) {                                                                \
-            if constexpr (LAUNDER) {                                                                                    \
-                q[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx_, vq_, 0, CP));              \
-                w[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rw, vw_, 0, 0));                 \
-                vq_ += (unsigned)rowB;                                                                                  \
-                vw_ += (unsigned)rowB / 2;                                                                              \
-                asm volatile("" : "+v"(vq_), "+v"(vw_));                                                                \
-            } else {                                                                                                    \
-                q[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx_, o_ * 8 + r * rowB, 0, CP)); \
-                w[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rw, o_ * 4 + r * rowB / 2, 0, 0)); \
-            }                                                                                                           \
-        }                                                                                                               \
-    } while (0)
+    auto issue = [&](int tile) {
+        const int b = tile % nb;
+        const long long f = tile / nb;
+        const unsigned o = (unsigned)(t * N2 + b * S + 2 * cp);
+        const __amdgpu_buffer_rsrc_t rx = brsrc(in + f * frameStride, (unsigned)nz * 8u);
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            q[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, o * 8 + r * rowB, 0, CP));
+            w[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rw, o * 4 + r * rowB / 2, 0, 0));
+        }
+    };
     int tile = blockIdx.x;
-    if (tile < ntiles) SDRGPU_PA1M_ISSUE(tile);
+    if (tile < ntiles) issue(tile);
     for (; tile < ntiles; tile += gridDim.x) {
         float2 v0[16], v1[16];
 #pragma unroll
@@ -624,7 +542,7 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_
             v0[r] = make_float2(q[r].x * w[r].x, q[r].y * w[r].x);
             v1[r] = make_float2(q[r].z * w[r].y, q[r].w * w[r].y);
         }
-        if (tile + (int)gridDim.x < ntiles) SDRGPU_PA1M_ISSUE(tile + (int)gridDim.x);   // next tile's loads fly now
+        if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);   // next tile's loads fly now
         dft16(v0);
         dft16(v1);
         int tv = tid;   // laundered thread index: the LDS addresses are recomputed per tile, not hoisted
@@ -638,75 +556,56 @@ __global__ __launch_bounds__(S / 2 * 1024 / 16) __attribute__((amdgpu_waves_per_
             seq0[LS + pad16lo(t2, r)] = v1[r];
         }
         __syncthreads();
-        // middle stage (radix 16, NS = 16). MIDCOL: one column at a time, 16 values live instead
-        // of 32. Column 1's region is disjoint from column 0's, so its read needs no barrier of its
-        // own.
-        float2 m16[16];
-        if constexpr (MIDCOL) {
-            mid16_read(seq0, tw16, t2, m16);
-            __syncthreads();   // every column-0 read is done
-            mid16_write(seq0, t2, m16);
-            mid16_read(seq0 + LS, tw16, t2, m16);
-            __syncthreads();   // every column-1 read done
-            mid16_write(seq0 + LS, t2, m16);
-            __syncthreads();
-        } else {
-            stage_lds_v<L, 16, 16, 2, true>(seq0, twl, t2, tw16);   // (two barriers inside)
-        }
-        int b;
-        long long f;
-        tile_fb<XG>(tile, nb, b, f);
+        stage_lds_v<L, 16, 16, 2, true>(seq0, twl, t2, tw16);   // middle stage, radix 16 (two barriers inside)
+        const int b = tile % nb;
+        const long long f = tile / nb;
         const int col = b * S + 2 * cp;
-        const __amdgpu_buffer_rsrc_t rs = brsrc(scratch + (f << logN), NOSTORE ? 0u : 0x7fffffffu);
+        const __amdgpu_buffer_rsrc_t rs = brsrc(scratch + (f << logN), 0x7fffffffu);
         // Stores carry the row step in the per-lane offset and a ZERO soffset. A >64-bit buffer
         // store with an SGPR soffset gets no wait state before the next VALU write of its data
         // VGPRs (hipcc's hazard check skips that form, and two 8-B stores get merged into it): it
         // wrote already-overwritten data, rows of some lanes changing from run to run (DESIGN.md
         // §3). The offset is advanced through an opaque register so the 16 row offsets are not all
         // precomputed (register pressure).
-        {
-            double2 cur[2], step[2];
+        double2 cur[2], step[2];
 #pragma unroll
-            for (int qq = 0; qq < 2; qq++) {
-                const int c = col + qq;
-                const int e0 = c * t2, d = 64 * c;   // < 2^16
-                cur[qq] = zmul(wt[e0 >> 8], wt[256 + (e0 & 255)]);
-                step[qq] = zmul(wt[d >> 8], wt[256 + (d & 255)]);
+        for (int qq = 0; qq < 2; qq++) {
+            const int c = col + qq;
+            const int e0 = c * t2, d = 64 * c;   // < 2^16
+            cur[qq] = zmul(wt[e0 >> 8], wt[256 + (e0 & 255)]);
+            step[qq] = zmul(wt[d >> 8], wt[256 + (d & 255)]);
+        }
+        // last stage (radix 4, NS = 256): outputs k1 = t + 64 m, m = b4 + 4 r, kept in registers
+        float2 y[2][16];
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++)
+#pragma unroll
+            for (int b4 = 0; b4 < 4; b4++) {
+                const int j = t2 + b4 * T;
+                float2 u[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) u[r] = seq0[qq * LS + pad16s<L / 4>(j, r)];
+#pragma unroll
+                for (int r = 1; r < 4; r++) u[r] = cmul(u[r], twl[r * j]);
+                dft4v(u);
+#pragma unroll
+                for (int r = 0; r < 4; r++) y[qq][b4 + 4 * r] = u[r];
             }
-            // last stage (radix 4, NS = 256): outputs k1 = t + 64 m, m = b4 + 4 r, kept in registers
-            float2 y[2][16];
+        unsigned vo = (unsigned)(b * L * S + t * S + 2 * cp) * 8u;
 #pragma unroll
-            for (int qq = 0; qq < 2; qq++)
-#pragma unroll
-                for (int b4 = 0; b4 < 4; b4++) {
-                    const int j = t2 + b4 * T;
-                    float2 u[4];
-#pragma unroll
-                    for (int r = 0; r < 4; r++) u[r] = seq0[qq * LS + pad16s<L / 4>(j, r)];
-#pragma unroll
-                    for (int r = 1; r < 4; r++) u[r] = cmul(u[r], twl[r * j]);
-                    dft4v(u);
-#pragma unroll
-                    for (int r = 0; r < 4; r++) y[qq][b4 + 4 * r] = u[r];
-                }
-            unsigned vo = TMAJ ? (unsigned)(b * L * S + t * S + 2 * cp) * 8u : (unsigned)(t * N2 + col) * 8u;
-            const unsigned mstep = TMAJ ? (unsigned)(T * S * 8) : (unsigned)rowB;
-#pragma unroll
-            for (int m = 0; m < 16; m++) {
-                const float2 a = cmul(y[0][m], make_float2((float)cur[0].x, (float)cur[0].y));
-                const float2 c = cmul(y[1][m], make_float2((float)cur[1].x, (float)cur[1].y));
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bu4, make_float4(a.x, a.y, c.x, c.y)), rs, vo, 0, 0);
-                vo += mstep;
-                asm volatile("" : "+v"(vo));
-                if (m < 15) {
-                    cur[0] = zmul(cur[0], step[0]);
-                    cur[1] = zmul(cur[1], step[1]);
-                }
+        for (int m = 0; m < 16; m++) {
+            const float2 a = cmul(y[0][m], make_float2((float)cur[0].x, (float)cur[0].y));
+            const float2 c = cmul(y[1][m], make_float2((float)cur[1].x, (float)cur[1].y));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bu4, make_float4(a.x, a.y, c.x, c.y)), rs, vo, 0, 0);
+            vo += (unsigned)(T * S * 8);
+            asm volatile("" : "+v"(vo));
+            if (m < 15) {
+                cur[0] = zmul(cur[0], step[0]);
+                cur[1] = zmul(cur[1], step[1]);
             }
         }
     }
 }
-#undef SDRGPU_PA1M_ISSUE
 
 // ---- pass B: S rows of length N2 per tile, dB out, transposed store -----------------
 // Stage 1 maps threads row-contiguous (coalesced row reads); the last stage maps the row
@@ -855,36 +754,24 @@ struct VfoWork {
 
 // The segments are those fir_rows_kernel runs (32 outputs, launch_rows): a segment's xlator phasors
 // are nco(segment start) x e^{i w D r}, so the segment boundaries are part of the arithmetic, and equal
-// boundaries give equal bits. (XG 0-2) one workgroup per frame: 64 segments, 4 per D-lane group.
-__device__ __forceinline__ void vfo_frame_block(const VfoWork& v, int g) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;   // 8 waves x 2 groups
-    for (int k = 0; k < 4; k++) {
-        const long long seg = (long long)(v.frame0 + g) * 64 + k * 16 + wave * 2 + (lane >> 5);
-        fir_rows_segment<32, 5, true, false, 32, 32, true>(v.a, seg, lane);
-    }
-}
-// (XG 3, the default) quarter q of frame g's stage-1 outputs: 16 segments of 32 outputs, one per D-lane
-// group, one row batch each -- a workgroup that lives one load round, like the column tiles beside it
+// boundaries give equal bits. Quarter q of frame g's stage-1 outputs: 16 segments of 32 outputs, one
+// per D-lane group, one row batch each -- a workgroup that lives one load round, like the column
+// tiles beside it.
 __device__ __forceinline__ void vfo_quarter_block(const VfoWork& v, int g, int q) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const long long seg = (long long)(v.frame0 + g) * 64 + q * 16 + wave * 2 + (lane >> 5);
     fir_rows_segment<32, 5, true, false, 32, 32, true>(v.a, seg, lane);
 }
 
-// XG: XCD-grouped frames. Workgroups x, x + 8, x + 16, ... run on one XCD (round-robin dispatch), so
-// workgroup 8 k + x takes item k % 9 of frame 8 (k / 9) + x: a frame's stage-1 workgroup (item 0,
-// dispatched first) and its 8 column tiles share one XCD's L2, and the second reader of each IQ line
-// finds it there instead of crossing the fabric to the Infinity Cache. Ungrouped, a frame's 9
-// consecutive workgroups land on all eight XCDs.
-// XG 3 (the default): a frame's stage 1 as 4 quarter workgroups of 16 one-row-batch segments: they
-// live one load round, as the 8 column tiles beside them do, so all 12 read the frame's lines at the
-// same time and the second read is served by the XCD's L2. C5 PMC 36.7 -> 30.4 B/sample (fetch 23.5
-// -> 17.1), group 1.743 -> 1.696 ms (3 interleaved runs, r4g).
-// XG 2 (tuning): also interleaves the two passes -- XCD x's workgroups take, per group of 17, one
-// frame's 8 pass-B row tiles and then one frame's 9 pass-A items, instead of every pass-B tile of
-// the launch first (the Infinity-Cache reads of pass B beside the HBM reads of pass A all launch
-// long, rather than one phase after the other).
-template <bool ZM, int CP, int XG = 0>
+// XCD-grouped frames. Workgroups x, x + 8, x + 16, ... run on one XCD (round-robin dispatch, speed
+// only), so after the nB pass-B tiles workgroup nB + 8 k + x takes item k % 12 of frame 8 (k / 12) + x:
+// a frame's 4 stage-1 quarter workgroups (items 0-3, dispatched first) and its 8 column tiles share
+// one XCD's L2 and live the same load round, so the second reader of each IQ line finds it in that
+// L2 instead of crossing the fabric. C5 PMC 36.7 -> 30.4 B/sample (fetch 23.5 -> 17.1), group 1.743
+// -> 1.696 ms (r4g). Measured and removed: a frame's 9 workgroups consecutive over all
+// XCDs (fetch 26.1 B), one whole-frame stage-1 workgroup per frame (L2 turned over), the passes
+// interleaved per XCD (noise), streaming pass-A input loads (the quarters' L2 hits need the lines).
+template <bool ZM>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fft_vfo_kernel(
     int nB, const float2* __restrict__ scratchB, int framesB, float* __restrict__ outB, float* __restrict__ zoomB,
     const float2* __restrict__ in, long long frameStride, int framesA, const float* __restrict__ win, int nz,
@@ -895,49 +782,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
         (void)fir_hist_block<float2, true, false>(v.a);
         return;
     }
-    int g, r;                        // pass-A frame g: 8 column tiles (r < 8), its VFO block (r = 8)
-    if constexpr (XG == 3) {
-        if ((int)blockIdx.x < nB) {
-            passB_tile<256, 32, ZM>(lds, blockIdx.x, scratchB, framesB, 256, logN, tw2, outB, zoomB);
-            return;
-        }
-        const int i = blockIdx.x - nB, k = i >> 3, kk = k % 12;
-        g = 8 * (k / 12) + (i & 7);
-        if (g >= framesA) return;
-        if (kk < 4) {
-            vfo_quarter_block(v, g, kk);
-            return;
-        }
-        passA_tile<256, 32, CP>(lds, g * 8 + kk - 4, in, frameStride, framesA, win, nz, 256, logN, tw1, tfull, scratchA);
-        return;
-    } else if constexpr (XG == 2) {
-        const int i = blockIdx.x, k = i >> 3, kk = k % 17;
-        const int gs = 8 * (k / 17) + (i & 7);   // frame slot of this XCD lane
-        if (kk < 8) {
-            if (gs < framesB) passB_tile<256, 32, ZM>(lds, gs * 8 + kk, scratchB, framesB, 256, logN, tw2, outB, zoomB);
-            return;
-        }
-        g = gs;
-        r = kk == 8 ? 8 : kk - 9;
-        if (g >= framesA) return;
-    } else {
     if ((int)blockIdx.x < nB) {
         passB_tile<256, 32, ZM>(lds, blockIdx.x, scratchB, framesB, 256, logN, tw2, outB, zoomB);
         return;
     }
-    const int i = blockIdx.x - nB;   // (nB = 8 x pass-B frames: XCD lane of i = that of blockIdx.x)
-    if constexpr (XG == 1) {
-        const int k = i >> 3, kk = k % 9;
-        g = 8 * (k / 9) + (i & 7);
-        r = kk == 0 ? 8 : kk - 1;
-        if (g >= framesA) return;    // (padding of the last group of 8 frames)
-    } else {
-        g = i / 9;
-        r = i % 9;
+    const int i = blockIdx.x - nB, k = i >> 3, kk = k % 12;
+    const int g = 8 * (k / 12) + (i & 7);
+    if (g >= framesA) return;   // (padding of the last group of 8 frames)
+    if (kk < 4) {
+        vfo_quarter_block(v, g, kk);
+        return;
     }
-    }
-    if (r == 8) vfo_frame_block(v, g);
-    else passA_tile<256, 32, CP>(lds, g * 8 + r, in, frameStride, framesA, win, nz, 256, logN, tw1, tfull, scratchA);
+    passA_tile<256, 32, 0>(lds, g * 8 + kk - 4, in, frameStride, framesA, win, nz, 256, logN, tw1, tfull, scratchA);
 }
 
 // ---- one-pass 64k spectrum (round 4): no intermediate leaves the CU ---------------------------
@@ -994,46 +850,19 @@ __device__ __forceinline__ void dft32(float2* v) {
     }
 }
 
-// stage-1 twiddles W_N^(t (4 k2 + r)): 0 = one exact table value each (128 KB per workgroup from L2);
-// 1 = an fp64 recurrence W_N^(t r) (W_N^(4 t))^k2 from two values of an fp64 table, rounded once
-// (group 1.942 -> 1.893 ms, r41pb; the 1p tests pass with both)
-#ifndef SDRGPU_1P_TW
-#define SDRGPU_1P_TW 1
-#endif
-#ifndef SDRGPU_1P_PB
-#define SDRGPU_1P_PB 4   // sample rows per load batch
-#endif
-#ifdef SDRGPU_1P_TIMING   // (measurement builds) per-workgroup phase timestamps, wave 0
-__device__ unsigned long long g_1p_t[16384 * 8];
-#define T1P(k) do { if (threadIdx.x == 0 && blockIdx.x < 16384) g_1p_t[blockIdx.x * 8 + (k)] = clock64(); } while (0)
-#else
-#define T1P(k) do {} while (0)
-#endif
-#ifndef SDRGPU_1P_VFO_UNROLL
-#define SDRGPU_1P_VFO_UNROLL 0   // (A/B) fft_1p256_kernel's two stage-1 segments per lane group unrolled
-#endif
-#ifndef SDRGPU_1P_NT
-#define SDRGPU_1P_NT 0   // (A/B) fft_1p256_kernel's dB rows as streaming stores
-#endif
-#ifndef SDRGPU_1P_WIDE
-#define SDRGPU_1P_WIDE 0
-#endif
-#ifndef SDRGPU_1P_VFO_LAST
-#define SDRGPU_1P_VFO_LAST 0   // (A/B) the VFO quarter after the transform instead of before it
-#endif
-#ifndef SDRGPU_1P_PB2
-#define SDRGPU_1P_PB2 2   // (HALF) sample rows per load batch at the 128-VGPR budget
-#endif
-// HALF (SDRGPU_FFT_1P=2): the LDS image holds 16 rows k2 at a time (76 KB: two workgroups per CU, 128
-// VGPRs): stage 1's 32 outputs stay in registers, and rows 0-15, then 16-31, go through stages 2 and 3
-template <bool ZM, bool VFO, bool HALF = false>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 1))) void fft_1p_kernel(
+// Stage-1 twiddles W_N^(t (4 k2 + r)) by an fp64 recurrence W_N^(t r) (W_N^(4 t))^k2 from two values of
+// an fp64 table, rounded once (against one exact table value each, 128 KB per workgroup from L2: group
+// 1.942 -> 1.893 ms, r41pb).
+constexpr int k1pPB = 4;   // sample rows per load batch
+template <bool ZM, bool VFO>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void fft_1p_kernel(
     const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz,
     const float2* __restrict__ tab, const double2* __restrict__ tab64, float* __restrict__ out, float* __restrict__ zpart,
     VfoWork v) {
     using op1::M;
     using op1::RS;
-    constexpr int TW512 = (HALF ? 16 : 32) * RS, W128 = TW512 + 512;
+    using op1::TW512;
+    using op1::W128;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     if constexpr (VFO) {
         if (v.hist && blockIdx.x == gridDim.x - 1) {   // the stage's history carry (fir.h:80)
@@ -1044,9 +873,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
     const int b = blockIdx.x, k = b >> 3;
     const int f = 8 * (k >> 2) + (b & 7), r = k & 3;
     if (f >= frames) return;
-    T1P(0);
-    if constexpr (VFO && !SDRGPU_1P_VFO_LAST) vfo_quarter_block(v, f, r);
-    T1P(1);
+    if constexpr (VFO) vfo_quarter_block(v, f, r);
     const int t = threadIdx.x;
     float2* tw512 = lds + TW512;
     float2* w128 = lds + W128;
@@ -1066,14 +893,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
         // W_4^r q with W_4^r in {1, -i, -1, i}: one of fx, fy is 0, the other +-1 (exact products)
         z[i] = make_float2(a.x + (fx * q.x - fy * q.y), a.y + (fx * q.y + fy * q.x));
     };
-    double2 c0, st;   // (SDRGPU_1P_TW 1) W_N^(t r), W_N^(4 t): loaded first, used after the loads
-    if constexpr (SDRGPU_1P_TW == 1 && !HALF) {
-        c0 = tab64[t * r];
-        st = tab64[4 * t];
-    }
+    const double2 c0 = tab64[t * r], st = tab64[4 * t];   // W_N^(t r), W_N^(4 t): loaded first, used after the loads
     // batches of PB sample rows (4 PB loads of x and of w each), the next batch's loads in flight while
     // this one is combined (two batches of registers; issued all at once, the loads spill)
-    constexpr int PB = HALF ? SDRGPU_1P_PB2 : SDRGPU_1P_PB, NB = 32 / PB;
+    constexpr int PB = k1pPB, NB = 32 / PB;
     auto pipeline = [&](auto&& ld) {
         float2 xv[2][PB][4];
         float wv[2][PB][4];
@@ -1092,55 +915,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
             __builtin_amdgcn_sched_barrier(0);
         }
     };
-    // SDRGPU_1P_WIDE: half the load instructions (the vmcnt cap of 63 per wave bounds the bytes in
-    // flight): lanes 2u and 2u + 1 load rows i and i + 1 of the adjacent sample pair (t, t + 1) as one
-    // 16-B load each (8-B for the window) and swap the halves the other lane needs (DPP)
-    auto pipeline2 = [&](auto&& ld2) {
-        constexpr int PP = PB / 2;
-        const int lane = t & 63;
-        const bool odd = (t & 1) != 0;
-        float4 xr[2][PP][4];
-        float2 wr[2][PP][4];
-        auto issue = [&](int bb, float4 (&xb)[PP][4], float2 (&wb)[PP][4]) {
-#pragma unroll
-            for (int pp = 0; pp < PP; pp++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) ld2(512 * (PB * bb + 2 * pp) + M * j, xb[pp][j], wb[pp][j]);
-        };
-        issue(0, xr[0], wr[0]);
-#pragma unroll
-        for (int bb = 0; bb < NB; bb++) {
-            if (bb + 1 < NB) issue(bb + 1, xr[(bb + 1) & 1], wr[(bb + 1) & 1]);
-#pragma unroll
-            for (int pp = 0; pp < PP; pp++) {
-                float2 x0[4], x1[4];
-                float w0[4], w1[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    // even lane: (x(t, i), x(t + 1, i)); odd lane: (x(t - 1, i + 1), x(t, i + 1))
-                    const float4 X = xr[bb & 1][pp][j];
-                    const float2 Wv = wr[bb & 1][pp][j];
-                    const float r0 = xchg<1>(odd ? X.x : X.z, lane), r1 = xchg<1>(odd ? X.y : X.w, lane);
-                    x0[j] = odd ? make_float2(r0, r1) : make_float2(X.x, X.y);
-                    x1[j] = odd ? make_float2(X.z, X.w) : make_float2(r0, r1);
-                    const float rw = xchg<1>(odd ? Wv.x : Wv.y, lane);
-                    w0[j] = odd ? rw : Wv.x;
-                    w1[j] = odd ? Wv.y : rw;
-                }
-                combine(PB * bb + 2 * pp, x0, w0);
-                combine(PB * bb + 2 * pp + 1, x1, w1);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-    if (SDRGPU_1P_WIDE && nz >= 65536 && ((uintptr_t)xf & 15) == 0) {
-        const __amdgpu_buffer_rsrc_t rx = brsrc(xf, 65536u * 8u), rw = brsrc(win, 65536u * 4u);
-        const int o = t + 511 * (t & 1);   // the pair's first sample, in row i (even lane) or i + 1 (odd lane)
-        pipeline2([&](int n0, float4& xo, float2& wo) {
-            xo = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, o * 8, n0 * 8, 0));
-            wo = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rw, o * 4, n0 * 4, 0));
-        });
-    } else if (nz >= 65536) {   // no zero padding (workgroup-uniform): the row offset rides in soffset
+    if (nz >= 65536) {   // no zero padding (workgroup-uniform): the row offset rides in soffset
         const __amdgpu_buffer_rsrc_t rx = brsrc(xf, 65536u * 8u), rw = brsrc(win, 65536u * 4u);
         pipeline([&](int n0, float2& xo, float& wo) {
             xo = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, t * 8, n0 * 8, 0));
@@ -1153,82 +928,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
             wo = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, (t + n0) * 4, 0, 0));
         });
     }
-    T1P(2);
     __syncthreads();   // (w128, tw512)
 #pragma unroll
     for (int i = 1; i < 32; i++) z[i] = cmul(z[i], w128[i]);   // W_128^(r i) = W_N^(512 r i)
     dft32(z);
     float* of = out + ((long long)f << 16);
-    if constexpr (HALF) {
-        double2 c = tab64[t * r];   // (loaded here: at 128 VGPRs they do not stay live through the loads)
-        st = tab64[4 * t];
-#pragma unroll
-        for (int k2 = 0; k2 < 32; k2++) {
-            z[k2] = cmul(z[k2], make_float2((float)c.x, (float)c.y));
-            if (k2 < 31) c = zmul(c, st);
-        }
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-#pragma unroll
-            for (int kl = 0; kl < 16; kl++) lds[kl * RS + pad16(t)] = z[16 * h + kl];
-            __syncthreads();
-            // stage 2 on rows k2 = 16 h + kl: (kl, t0) = (t >> 4, t & 15), the first 256 threads
-            const int kl2 = (t >> 4) & 15, t0 = t & 15, k22 = 16 * h + kl2;
-            float2 a[32];
-            if (t < 256) {
-#pragma unroll
-                for (int t1 = 0; t1 < 32; t1++) a[t1] = lds[kl2 * RS + t0 + 17 * t1];
-                dft32(a);
-#pragma unroll
-                for (int q1 = 1; q1 < 32; q1++) a[q1] = cmul(a[q1], lds[TW512 + 16 * q1 + t0]);
-            }
-            __syncthreads();
-            if (t < 256) {
-                const int sw = t0 ^ ((k22 >> 1) & 15);
-#pragma unroll
-                for (int q1 = 0; q1 < 32; q1++) lds[kl2 * RS + 17 * q1 + sw] = a[q1];
-            }
-            __syncthreads();
-            // stage 3: (kl, q1) = (t & 15, t >> 4)
-            const int kl = t & 15, q1 = t >> 4, k2 = 16 * h + kl, sw = (k2 >> 1) & 15;
-            float2 c3[16];
-#pragma unroll
-            for (int t0 = 0; t0 < 16; t0++) c3[t0] = lds[kl * RS + 17 * q1 + (t0 ^ sw)];
-            dft16(c3);
-            float dv[16];
-#pragma unroll
-            for (int q2 = 0; q2 < 16; q2++) {
-                dv[q2] = db_of(c3[q2]);
-                of[4 * (k2 + 32 * q1 + 1024 * q2) + r] = dv[q2];
-            }
-            if constexpr (ZM) {   // max over the 8 lanes kl & 7 (zoom column (k2 >> 3) + 4 q1 + 128 q2)
-                const int lane = t & 63;
-                tr_step<1, 8>(dv, lane);
-                tr_step<2, 4>(dv, lane);
-                tr_step<4, 2>(dv, lane);
-                const int q2 = ((lane & 1) << 3) | ((lane & 2) << 1) | (lane & 4) >> 1;
-                float* zp = zpart + ((long long)(4 * f + r) << 11) + (k2 >> 3) + 4 * q1 + 128 * q2;
-                zp[0] = dv[0];
-                zp[128] = dv[1];
-            }
-            if (h == 0) __syncthreads();   // (stage 3's reads before the next rows land)
-        }
-        if constexpr (VFO && SDRGPU_1P_VFO_LAST) vfo_quarter_block(v, f, r);
-        return;
-    }
-    if constexpr (SDRGPU_1P_TW == 1) {
+    {
         double2 c = c0;
 #pragma unroll
         for (int k2 = 0; k2 < 32; k2++) {
             lds[k2 * RS + pad16(t)] = cmul(z[k2], make_float2((float)c.x, (float)c.y));
             if (k2 < 31) c = zmul(c, st);
         }
-    } else {
-#pragma unroll
-        for (int k2 = 0; k2 < 32; k2++) lds[k2 * RS + pad16(t)] = cmul(z[k2], tab[(32 * r + k2) * 512 + t]);   // W_N^(t (4 k2 + r))
     }
     __syncthreads();
-    T1P(3);
     // stage 2: (k2, t0) = (t >> 4, t & 15)
     {
         const int k2 = t >> 4, t0 = t & 15;
@@ -1244,7 +957,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
         for (int q1 = 0; q1 < 32; q1++) lds[k2 * RS + 17 * q1 + sw] = a[q1];
     }
     __syncthreads();
-    T1P(4);
     // stage 3: (k2, q1) = (p & 31, p >> 5), p = t, t + 512
 #pragma unroll
     for (int h = 0; h < 2; h++) {
@@ -1271,170 +983,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HALF ? 4 : 
             zp[128] = dv[1];
         }
     }
-    T1P(5);
-    if constexpr (VFO && SDRGPU_1P_VFO_LAST) vfo_quarter_block(v, f, r);
-}
-#ifdef SDRGPU_1P_TIMING
-extern "C" int sdrgpu_debug_1p_times(unsigned long long* host, int n) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_1p_t), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : -1;
-}
-#endif
-
-// SDRGPU_FFT_1P=3: the half-image transform with 256-thread workgroups (2 per CU at 76 KB of LDS and up
-// to 256 VGPRs each: one workgroup's loads wait while the other one computes). Thread t takes the stage-1
-// columns t and t + 256; stages 2 and 3 as in the HALF mode (the 256 threads are stage 2's butterflies).
-// SV (SDRGPU_FFT_1P=4): the VFO quarters as workgroups of their own, a frame's 4 quarters dispatched
-// before its 4 transform workgroups on the same XCD (they fetch the frame; the transforms read it from L2)
-template <bool ZM, bool VFO, bool SV = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void fft_1p256_kernel(const float2* __restrict__ in, long long frameStride, int frames,
-                                                        const float* __restrict__ win, int nz, const float2* __restrict__ tab,
-                                                        const double2* __restrict__ tab64, float* __restrict__ out,
-                                                        float* __restrict__ zpart, VfoWork v) {
-    using op1::M;
-    using op1::RS;
-    constexpr int TW512 = 16 * RS, W128 = TW512 + 512;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    if constexpr (VFO) {
-        if (v.hist && blockIdx.x == gridDim.x - 1) {   // the stage's history carry (fir.h:80)
-            (void)fir_hist_block<float2, true, false>(v.a);
-            return;
-        }
-    }
-    const int b = blockIdx.x, k = b >> 3;
-    const int kq = SV ? (k & 7) : (k & 3) + 4;
-    const int f = 8 * (SV ? k >> 3 : k >> 2) + (b & 7), r = kq & 3;
-    if (f >= frames) return;
-    const int t = threadIdx.x;
-    if constexpr (VFO) {   // quarter r of the stage: 16 segments, 8 per pass of the 4 waves
-      if (!SV || kq < 4) {
-        const int lane = t & 63, wave = t >> 6;
-#if SDRGPU_1P_VFO_UNROLL
-#pragma unroll
-#else
-#pragma unroll 1
-#endif
-        for (int sub = 0; sub < 2; sub++)
-            fir_rows_segment<32, 5, true, false, 32, 32, true>(
-                v.a, (long long)(v.frame0 + f) * 64 + r * 16 + sub * 8 + wave * 2 + (lane >> 5), lane);
-        if (SV) return;
-      }
-    }
-    lds[TW512 + t] = tab[4 * M + t];
-    lds[TW512 + 256 + t] = tab[4 * M + 256 + t];
-    if (t < 32) lds[W128 + t] = tab[4 * M + 512 + 32 * r + t];
-    const float s = (r & 1) ? -1.0f : 1.0f;
-    const float fx = r == 0 ? 1.0f : (r == 2 ? -1.0f : 0.0f), fy = r == 1 ? -1.0f : (r == 3 ? 1.0f : 0.0f);
-    const float2* xf = in + (long long)f * frameStride;
-    float2 z[2][32];
-    auto combine = [&](int u, int i, const float2 (&xv)[4], const float (&wv)[4]) {
-        float2 uu[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) uu[j] = make_float2(xv[j].x * wv[j], xv[j].y * wv[j]);
-        const float2 a = make_float2(fmaf(s, uu[2].x, uu[0].x), fmaf(s, uu[2].y, uu[0].y));
-        const float2 q = make_float2(fmaf(s, uu[3].x, uu[1].x), fmaf(s, uu[3].y, uu[1].y));
-        z[u][i] = make_float2(a.x + (fx * q.x - fy * q.y), a.y + (fx * q.y + fy * q.x));
-    };
-    constexpr int NB = 32;   // one sample row (both columns, four quarters) per batch
-    auto pipeline = [&](auto&& ld) {
-        float2 xv[2][2][4];
-        float wv[2][2][4];
-        auto issue = [&](int i, float2 (&xb)[2][4], float (&wb)[2][4]) {
-#pragma unroll
-            for (int u = 0; u < 2; u++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) ld(256 * u + 512 * i + M * j, xb[u][j], wb[u][j]);
-        };
-        issue(0, xv[0], wv[0]);
-#pragma unroll
-        for (int i = 0; i < NB; i++) {
-            if (i + 1 < NB) issue(i + 1, xv[(i + 1) & 1], wv[(i + 1) & 1]);
-#pragma unroll
-            for (int u = 0; u < 2; u++) combine(u, i, xv[i & 1][u], wv[i & 1][u]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-    if (nz >= 65536) {
-        const __amdgpu_buffer_rsrc_t rx = brsrc(xf, 65536u * 8u), rw = brsrc(win, 65536u * 4u);
-        pipeline([&](int n0, float2& xo, float& wo) {
-            xo = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, t * 8, n0 * 8, 0));
-            wo = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, t * 4, n0 * 4, 0));
-        });
-    } else {
-        const __amdgpu_buffer_rsrc_t rx = brsrc(xf, (unsigned)nz * 8u), rw = brsrc(win, (unsigned)nz * 4u);
-        pipeline([&](int n0, float2& xo, float& wo) {
-            xo = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, (t + n0) * 8, 0, 0));
-            wo = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, (t + n0) * 4, 0, 0));
-        });
-    }
-    __syncthreads();   // (the LDS tables)
-#pragma unroll
-    for (int u = 0; u < 2; u++) {
-        const int tu = t + 256 * u;
-#pragma unroll
-        for (int i = 1; i < 32; i++) z[u][i] = cmul(z[u][i], lds[W128 + i]);
-        dft32(z[u]);
-        if constexpr (SDRGPU_1P_TW == 1) {
-            double2 c = tab64[tu * r];
-            const double2 st = tab64[4 * tu];
-#pragma unroll
-            for (int k2 = 0; k2 < 32; k2++) {
-                z[u][k2] = cmul(z[u][k2], make_float2((float)c.x, (float)c.y));
-                if (k2 < 31) c = zmul(c, st);
-            }
-        } else {
-#pragma unroll
-            for (int k2 = 0; k2 < 32; k2++) z[u][k2] = cmul(z[u][k2], tab[(32 * r + k2) * 512 + tu]);
-        }
-    }
-    float* of = out + ((long long)f << 16);
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-#pragma unroll
-        for (int u = 0; u < 2; u++)
-#pragma unroll
-            for (int kl = 0; kl < 16; kl++) lds[kl * RS + pad16(t + 256 * u)] = z[u][16 * h + kl];
-        __syncthreads();
-        {   // stage 2: (kl, t0) = (t >> 4, t & 15)
-            const int kl = t >> 4, t0 = t & 15, k2 = 16 * h + kl;
-            float2 a[32];
-#pragma unroll
-            for (int t1 = 0; t1 < 32; t1++) a[t1] = lds[kl * RS + t0 + 17 * t1];
-            dft32(a);
-#pragma unroll
-            for (int q1 = 1; q1 < 32; q1++) a[q1] = cmul(a[q1], lds[TW512 + 16 * q1 + t0]);
-            __syncthreads();
-            const int sw = t0 ^ ((k2 >> 1) & 15);
-#pragma unroll
-            for (int q1 = 0; q1 < 32; q1++) lds[kl * RS + 17 * q1 + sw] = a[q1];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int e = 0; e < 2; e++) {   // stage 3: (kl, q1) = (p & 15, p >> 4), p = t, t + 256
-            const int p = t + 256 * e, kl = p & 15, q1 = p >> 4, k2 = 16 * h + kl, sw = (k2 >> 1) & 15;
-            float2 c3[16];
-#pragma unroll
-            for (int t0 = 0; t0 < 16; t0++) c3[t0] = lds[kl * RS + 17 * q1 + (t0 ^ sw)];
-            dft16(c3);
-            float dv[16];
-#pragma unroll
-            for (int q2 = 0; q2 < 16; q2++) {
-                dv[q2] = db_of(c3[q2]);
-                if constexpr (SDRGPU_1P_NT) __builtin_nontemporal_store(dv[q2], &of[4 * (k2 + 32 * q1 + 1024 * q2) + r]);
-                else of[4 * (k2 + 32 * q1 + 1024 * q2) + r] = dv[q2];
-            }
-            if constexpr (ZM) {
-                const int lane = t & 63;
-                tr_step<1, 8>(dv, lane);
-                tr_step<2, 4>(dv, lane);
-                tr_step<4, 2>(dv, lane);
-                const int q2 = ((lane & 1) << 3) | ((lane & 2) << 1) | (lane & 4) >> 1;
-                float* zp = zpart + ((long long)(4 * f + r) << 11) + (k2 >> 3) + 4 * q1 + 128 * q2;
-                zp[0] = dv[0];
-                zp[128] = dv[1];
-            }
-        }
-        if (h == 0) __syncthreads();
-    }
 }
 
 // zoom[f][o] = max over the four workgroups' partial maxima (fft_1p_kernel's ZM)
@@ -1444,119 +992,6 @@ __global__ __launch_bounds__(256) void fft_1p_zoom_kernel(const float* __restric
     const long long f = i >> 11, o = i & 2047;
     const float* p = zpart + (f << 13) + o;
     zoom[i] = fmaxf(fmaxf(p[0], p[2048]), fmaxf(p[4096], p[6144]));
-}
-
-// ---- the C5 launch group as ONE persistent launch with per-frame dataflow (round 4, tuning:
-// SDRGPU_FFT_VFO_PERSIST). Each workgroup reads its XCD id (HW_REG_XCC_ID) and takes items from that
-// XCD's queue: frame f = 8 j + x belongs to XCD x; its 12 first-pass items (4 stage-1 quarters, 8
-// column tiles) come at queue step j and its 8 pass-B row tiles at step j + lag, so pass B of a frame
-// runs on the XCD that wrote its intermediate, a few frames later, from that XCD's L2 / the Infinity
-// Cache -- no launch boundaries, no chunk drains, and the intermediate's working set is ~lag frames
-// per XCD instead of a 128-MB chunk. The intermediate lives in a ring of R frame slots per XCD.
-// Dependencies (same XCD, so one L2 is the coherence point; the producer drains its stores before
-// counting, the consumer drops its L1 before reading):
-//   pass-B tile of f   waits for the 8 column tiles of f   (aDone[f] == 8)
-//   column tile of f   waits for the 8 pass-B tiles of f - 8 R, the slot's previous user (bDone == 8)
-// Every wait points at an item dequeued earlier by a running workgroup, so there is no deadlock for
-// any residency; every spin is bounded (on timeout the kernel raises err[0] and goes on).
-constexpr int kPersistRing = 32;   // slots per XCD
-struct PersistWork {
-    VfoWork v;
-    int frames, lag;
-    int* q;          // [8] per-XCD item counters (zeroed per call)
-    int* aDone;      // [frames]
-    int* bDone;      // [frames]
-    int* err;        // [1] spin timeouts
-};
-__device__ __forceinline__ bool persist_wait(const int* c, int target, int* err) {
-    for (int k = 0; k < (1 << 22); k++) {
-        if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
-        __builtin_amdgcn_s_sleep(2);
-    }
-    __hip_atomic_fetch_add(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return false;
-}
-// (the item bodies as separate functions: inlined into one loop their registers add up and the
-// kernel spilled 37 VGPRs at the 128-VGPR budget)
-__device__ __attribute__((noinline)) void persist_quarter(const VfoWork& v, int f, int q) { vfo_quarter_block(v, f, q); }
-__device__ __attribute__((noinline)) void persist_tile_a(float2* lds, int r, const float2* x, long long N, const float* win,
-                                                         int nz, int logN, const float2* tw1, const float2* tfull, float2* slot) {
-    passA_tile<256, 32, 0>(lds, r, x, N, 1, win, nz, 256, logN, tw1, tfull, slot);
-}
-template <bool ZM>
-__device__ __attribute__((noinline)) void persist_tile_b(float2* lds, int r, const float2* slot, int logN, const float2* tw2,
-                                                         float* o, float* z) {
-    passB_tile<256, 32, ZM>(lds, r, slot, 1, 256, logN, tw2, o, z);
-}
-template <bool ZM, bool INL = false>   // INL (tuning): the item bodies inlined (spills 37 VGPRs)
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fft_vfo_persist_kernel(
-    const float2* __restrict__ in, float* __restrict__ out, float* __restrict__ zoom, const float* __restrict__ win, int nz,
-    int logN, const float2* __restrict__ tw1, const float2* __restrict__ tw2, const float2* __restrict__ tfull,
-    float2* __restrict__ ring, PersistWork w) {
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    __shared__ int item;
-    const int tid = threadIdx.x;
-    if (blockIdx.x == 0) (void)fir_hist_copy<float2, true, false>(w.v.a);   // the stage's history carry (fir.h:80)
-    const int x = (int)(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 7);   // HW_REG_XCC_ID[2:0]
-    const int J = (w.frames - x + 7) / 8;   // this XCD's frames: f = 8 j + x, j < J
-    const int L = w.lag;
-    const int a = J < L ? J : L, b = J < L ? L : J, c2 = J < L ? 0 : 20;
-    const int total = 20 * J;
-    const long long N = 1LL << logN;
-    // the next item's index is drawn while the current one runs (an atomic round trip per item would
-    // otherwise serialise with the work)
-    int nxt = 0;
-    if (tid == 0) nxt = __hip_atomic_fetch_add(&w.q[x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (;;) {
-        __syncthreads();   // (the previous item's last LDS reads and its use of `item` are done)
-        if (tid == 0) {
-            item = nxt;
-            if (nxt < total) nxt = __hip_atomic_fetch_add(&w.q[x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        int i = item;
-        if (i >= total) break;
-        int st, k;   // queue step, item within it: k < 12 first pass (0-3 quarters, 4-11 tiles), k >= 12 pass B
-        if (i < 12 * a) {
-            st = i / 12; k = i % 12;
-        } else if ((i -= 12 * a) < c2 * (b - a)) {
-            st = a + i / c2; k = i % c2;
-        } else {
-            i -= c2 * (b - a);
-            st = b + i / 8; k = 12 + i % 8;
-        }
-        if (k < 12) {
-            const int j = st, f = 8 * j + x;
-            if (k < 4) {
-                if constexpr (INL) vfo_quarter_block(w.v, f, k);
-                else persist_quarter(w.v, f, k);
-                continue;
-            }
-            float2* slot = ring + (long long)(x * kPersistRing + j % kPersistRing) * N;
-            if (j >= kPersistRing) {   // the slot's previous frame must be out of pass B
-                if (tid == 0) (void)persist_wait(&w.bDone[f - 8 * kPersistRing], 8, w.err);
-                __syncthreads();
-            }
-            if constexpr (INL) passA_tile<256, 32, 0>(lds, k - 4, in + (long long)f * N, N, 1, win, nz, 256, logN, tw1, tfull, slot);
-            else persist_tile_a(lds, k - 4, in + (long long)f * N, N, win, nz, logN, tw1, tfull, slot);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's intermediate stores are in L2
-            __syncthreads();
-            if (tid == 0) __hip_atomic_fetch_add(&w.aDone[f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            const int j = st - L, f = 8 * j + x;
-            const float2* slot = ring + (long long)(x * kPersistRing + j % kPersistRing) * N;
-            if (tid == 0) (void)persist_wait(&w.aDone[f], 8, w.err);
-            __syncthreads();
-            asm volatile("buffer_inv sc0" ::: "memory");   // no stale L1 lines of the slot's previous frame
-            if constexpr (INL)
-                passB_tile<256, 32, ZM>(lds, k - 12, slot, 1, 256, logN, tw2, out + (long long)f * N,
-                                        ZM ? zoom + (long long)f * (N / 32) : nullptr);
-            else persist_tile_b<ZM>(lds, k - 12, slot, logN, tw2, out + (long long)f * N, ZM ? zoom + (long long)f * (N / 32) : nullptr);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (its slot reads are done before the slot is freed)
-            __syncthreads();
-            if (tid == 0) __hip_atomic_fetch_add(&w.bDone[f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 // ---- the front end's per-block launch: pass A (frame straddling two pushes read in place) + the
@@ -1615,51 +1050,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
 struct FftPlan {
     int device = 0, N = 0, logN = 0, nz = 0;
     int N1 = 0, N2 = 0;               // two-pass split (N1 * N2 = N); N1 = 0 -> single pass
-    DevBuf win, tw1, tw2, tfull, scratch;
+    DevBuf win, tw1, tw2, tfull, scratch, scratch2;
     int chunkFrames = 1;
-    int sa = 16, sb = 32;             // pass-A columns / pass-B rows per workgroup (tuning)
+    int sa = 16, sb = 32;             // pass-A columns / pass-B rows per workgroup (32 / 32 on the 64k plan)
     float2* cur = nullptr;            // scratch buffer of the chunk being launched
     int sa2 = 0;                      // paired pass-A columns per workgroup (0: paired kernel off)
-    int pipe1m = 1;                   // N1 = N2 = 1024: persistent software-pipelined passes (SDRGPU_FFT_1M=0 off)
-    int gridA = 0, gridB = 0, gridM = 0;   // their grids (resident workgroups); gridM: the merged 1M launches
-    int merge1m = 0;                  // SDRGPU_FFT_MERGE_1M (tuning): merged pass-B(c-1) + pass-A(c) launches
-    // pass-A variant (SDRGPU_FFT_1M_VAR, tuning: fft_passA_1m_kernel's VAR). Default 128: the
-    // tile-major intermediate (each pass-A tile's 128 KB written contiguously, 1 KB per store
-    // instruction instead of eight 128-B row pieces; pass B reads 16-column pieces of 128 B):
-    // 1.89 vs 1.94 ms per C2 step (3 interleaved runs, one box)
-    int var1m = 128;
-    int var1mB = 64;                  // pass-B variant (SDRGPU_FFT_1M_VARB, tuning: 64 XCD grouping; 16 / 32 measurement only)
-    // columns / rows per workgroup of the 1M passes (SDRGPU_FFT_1M_SA / SB, tuning). Pass B at 8
-    // rows (2 workgroups per CU) with XCD-grouped row blocks (4 blocks whose 32-B dB segments share
-    // 128-B lines on one XCD): 1.93 vs 1.97 ms per C2 step (3 interleaved runs on each of two boxes);
-    // without the grouping 2.06. Pass A at 8 columns: 2.24 (XCD-grouped) / 2.70 ms.
-    int sA1m = 16, sB1m = 8;
+    int gridA = 0, gridB = 0;         // the persistent 1M passes' grids (resident workgroups)
     DevBuf wt;                        // fp64 W_N^(256 j), W_N^j (j < 256) for the 1M pass A
     hipStream_t own = nullptr;
     PinnedBuf pin_in, pin_out;
     DevBuf dev_in, dev_out;
-    // two-stream chunk pipeline: pass A of chunk i+1 (caller stream) overlaps pass B of chunk
-    // i (second stream), scratch double-buffered. Measured SLOWER (64k: 2.16 vs 1.86 ms, 1M:
-    // 2.98 vs 2.39 ms per step; the concurrent passes evict each other's Infinity-Cache
-    // working set), so it is off unless SDRGPU_FFT_PIPE=1.
-    int pipe = 0;
     // merged pass-B(c) + pass-A(c+1) launches (64k split): one launch boundary per chunk
     // instead of two; 1.87 -> 1.73 ms per 2^28 samples (A/B on one box). SDRGPU_FFT_MERGE=0 off.
     int merge = 1;
     StreamOrder order;                // scratch is per plan: calls on different streams are serialised
     sdrgpu_zoom* zoom = nullptr;      // execute_zoom's unfused zoom (sizes other than N / 32)
     int zoomSize = 0;
-    hipStream_t s2 = nullptr;
-    hipEvent_t evFork = nullptr, evJoin = nullptr, evA[2] = {nullptr, nullptr}, evB[2] = {nullptr, nullptr};
-    // SDRGPU_FFT_VFO_SIDE=1 (tuning): the fused VFO's later stages on the side stream, beside the last
-    // pass-B launch. Measured slower: C5 step 1.725 vs 1.705 ms (3 interleaved runs, r4i; the overlap
-    // stretches the last launch more than it hides), so they run after it on the call's stream
-    int vfoSide = 0;
-    int vfoPersist = 0;   // SDRGPU_FFT_VFO_PERSIST (tuning): the group as one persistent dataflow launch
-    int persistLag = 6;   // SDRGPU_FFT_PERSIST_LAG (tuning): queue steps between a frame's two passes
-    DevBuf persistCtl;    // its counters: q[8], aDone[frames], bDone[frames], err
-    int gridP = 0;
-    DevBuf scratch2;
     Fft64Plan* f64 = nullptr;         // sdrgpu_fft_set_precision(h, 1): the fp64-interior kernels (fft64.hip)
     // sdrgpu_fft_set_timing: HIP events around each call's spectrum launch group (the fused VFO
     // stage included, the VFO's later stages not), a ring of kTimed calls read by sdrgpu_fft_group_times
@@ -1667,29 +1073,10 @@ struct FftPlan {
     bool timing = false;
     hipEvent_t tev[kTimed][2] = {};
     long long tcalls = 0;
-    int vfoCP = 0;                    // fused VFO launches: pass-A input cache policy (SDRGPU_FFT_VFO_CP, tuning)
     int vfoFuse = 1;                  // SDRGPU_FFT_VFO_FUSE=0 (tuning): spectrum and VFO as separate launch groups
-    int fuseTail = 1;                 // SDRGPU_FFT_FUSE_TAIL=0 (tuning): the front end's VFO tail as a launch of its own
-    // fft_vfo_kernel's launch order (SDRGPU_FFT_VFO_XCD, tuning): 0 a frame's 9 workgroups consecutive;
-    // 1 XCD-grouped (group 1.732 -> 1.694 ms, r4d); 2 + passes interleaved (1.684 -> 1.679, noise, r4f);
-    // 3 XCD-grouped with quarter-frame stage-1 workgroups (1.743 -> 1.696 ms, r4g), the default
-    int vfoXcd = 3;
-    // the 64k plan: one-pass spectrum launches (fft_1p_kernel), SDRGPU_FFT_1P (tuning)
-    int onepass = 0;
+    int onepass = 0;                  // the 64k plan's one-pass launches (fft_1p_kernel), SDRGPU_FFT_1P (tuning)
     DevBuf tab1p, tab1p64, zpart;
 };
-// the plan's side stream and its events (the two-stream pipeline; the fused VFO's later stages)
-static int ensure_side(FftPlan& p) {
-    if (p.s2) return SDRGPU_OK;
-    SDRGPU_HIP(hipStreamCreateWithFlags(&p.s2, hipStreamNonBlocking));
-    SDRGPU_HIP(hipEventCreateWithFlags(&p.evFork, hipEventDisableTiming));
-    SDRGPU_HIP(hipEventCreateWithFlags(&p.evJoin, hipEventDisableTiming));
-    for (int k = 0; k < 2; k++) {
-        SDRGPU_HIP(hipEventCreateWithFlags(&p.evA[k], hipEventDisableTiming));
-        SDRGPU_HIP(hipEventCreateWithFlags(&p.evB[k], hipEventDisableTiming));
-    }
-    return SDRGPU_OK;
-}
 static int time_mark(FftPlan& p, int which, hipStream_t s) {
     if (!p.timing) return SDRGPU_OK;
     SDRGPU_HIP(hipEventRecord(p.tev[p.tcalls % FftPlan::kTimed][which], s));
@@ -1775,147 +1162,61 @@ static int launch_passB(const FftPlan& p, int frames, float* out, hipStream_t s,
     return SDRGPU_OK;
 }
 
-template <int LA, int SA, int LB, int SB, bool PAIRED, bool ZM = false>
+// merged pass B (chunk c) + pass A (chunk c+1) launches of the 64k split (256 x 256, 32 columns / 32
+// rows, one-column pass A). The 1M split's merged form (paired pass A, pass B at 8 rows to match its
+// 512 threads) measured 12% SLOWER: pass B loses half its occupancy to pass A's 147 KB of LDS, so the
+// 1M transform keeps separate launches.
+template <bool ZM>
 static int launch_merged(const FftPlan& p, const float2* scratchB, int framesB, float* outB, const float2* in,
                          long long stride, int framesA, float2* scratchA, hipStream_t s, float* zoomB = nullptr) {
-    auto k = fft_merged_kernel<LA, SA, LB, SB, PAIRED, ZM>;
-    size_t lds = sizeof(float2) * std::max(SA * Lds<LA>::LS + ((PAIRED || LA == 256) ? LA : 0) + (LA == 256 && !PAIRED ? 256 : 0),
-                                           SB * Lds<LB>::LS + (LB >= 256 ? 256 : 0));
+    auto k = fft_merged_kernel<256, 32, 256, 32, false, ZM>;
+    const size_t lds = sizeof(float2) * (32 * Lds<256>::LS + 256 + 256);
     SDRGPU_CHECK(set_lds(k, lds));
-    const int nB = (LA / SB) * framesB, nA = (LB / SA) * framesA;
-    hipLaunchKernelGGL(k, dim3(nB + nA), dim3(SB * LB / 16), lds, s, nB, scratchB, framesB, outB, zoomB, in, stride, framesA,
+    const int nB = 8 * framesB, nA = 8 * framesA;
+    hipLaunchKernelGGL(k, dim3(nB + nA), dim3(512), lds, s, nB, scratchB, framesB, outB, zoomB, in, stride, framesA,
                        p.win.as<float>(), p.nz, p.logN, p.tw1.as<float2>(), p.tw2.as<float2>(), p.tfull.as<float2>(),
                        scratchA);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
-
-template <int S, int CP, int VAR>
-static int launch_passA_1m(FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
-    if (p.N2 % S) { set_error("fft: N2 %d not a multiple of %d columns", p.N2, S); return SDRGPU_ESTATE; }
-    auto k = fft_passA_1m_kernel<S, CP, VAR>;
-    size_t lds = sizeof(float2) * (S * Lds<1024>::LS + 1024 + 256);
-    SDRGPU_CHECK(set_lds(k, lds));
-    if (!p.gridA) {
-        int per = 0, cus = 0;
-        SDRGPU_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k, S / 2 * 64, lds));
-        SDRGPU_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p.device));
-        p.gridA = std::max(1, per) * cus;
-    }
-    const int ntiles = (p.N2 / S) * frames;
-    hipLaunchKernelGGL(k, dim3(std::min(p.gridA, ntiles)), dim3(S / 2 * 64), lds, s, in, stride, frames, p.win.as<float>(),
-                       p.nz, p.N2, p.logN, p.tw1.as<float2>(), p.wt.as<double2>(), p.cur, MergeB{});
-    SDRGPU_HIP(hipGetLastError());
-    return SDRGPU_OK;
-}
-
-template <int S, int CP, int VAR = 0>
-static int launch_passB_1m(FftPlan& p, int frames, float* out, hipStream_t s) {
-    auto k = fft_passB_1m_kernel<S, CP, VAR>;
-    size_t lds = sizeof(float2) * (S * Lds<1024>::LS + 1024 + 256);
-    SDRGPU_CHECK(set_lds(k, lds));
-    if (!p.gridB) {
-        int per = 0, cus = 0;
-        SDRGPU_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k, S * 64, lds));
-        SDRGPU_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p.device));
-        p.gridB = std::max(1, per) * cus;
-    }
-    const int ntiles = (p.N1 / S) * frames;
-    hipLaunchKernelGGL(k, dim3(std::min(p.gridB, ntiles)), dim3(S * 64), lds, s, p.cur, frames, p.N1, p.logN,
-                       p.tw2.as<float2>(), out);
-    SDRGPU_HIP(hipGetLastError());
-    return SDRGPU_OK;
-}
-
-// one merged 1M launch (fft_passA_1m_kernel<16, 2, 128, MERGED>): pass B of framesB frames of scratchB
-// (0: none), then pass A of framesA frames into scratchA (0: none)
-static int launch_merged_1m(FftPlan& p, const float2* scratchB, int framesB, float* outB, const float2* in, long long stride,
-                            int framesA, float2* scratchA, hipStream_t s) {
-    auto k = fft_passA_1m_kernel<16, 2, 128, true>;
-    const size_t lds = sizeof(float2) * (16 * Lds<1024>::LS + 1024 + 256);
-    SDRGPU_CHECK(set_lds(k, lds));
-    if (!p.gridM) {
-        int per = 0, cus = 0;
-        SDRGPU_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k, 512, lds));
-        SDRGPU_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p.device));
-        p.gridM = std::max(1, per) * cus;
-    }
-    const int tiles = std::max((p.N1 / 8) * framesB, (p.N2 / 16) * framesA);
-    hipLaunchKernelGGL(k, dim3(std::min(p.gridM, tiles)), dim3(512), lds, s, in, stride, framesA, p.win.as<float>(), p.nz,
-                       p.N2, p.logN, p.tw1.as<float2>(), p.wt.as<double2>(), scratchA,
-                       MergeB{scratchB, framesB, p.N1, outB, p.tw2.as<float2>()});
-    SDRGPU_HIP(hipGetLastError());
-    return SDRGPU_OK;
-}
-
-// the persistent 1M passes for one chunk, with the tuning variants. Pass B reads the layout pass A
-// wrote: tile-major (pass A VAR 128, the default) or row-major (every other variant).
-static int dispatch_1m(FftPlan& p, const float2* xc, long long stride, int nf, float* o, hipStream_t s) {
-    if (p.pipe1m == 2) {   // (tuning) non-temporal streaming accesses, row-major
-        SDRGPU_CHECK((launch_passA_1m<16, 2, 0>(p, xc, stride, nf, s)));
-        return launch_passB_1m<16, 2>(p, nf, o, s);
-    }
-    if (p.pipe1m == 3 || p.pipe1m == 4) {   // (tuning) default layout with cached input loads (3), nt pass B loads (4)
-        if (p.pipe1m == 3) SDRGPU_CHECK((launch_passA_1m<16, 0, 128>(p, xc, stride, nf, s)));
-        else SDRGPU_CHECK((launch_passA_1m<16, 2, 128>(p, xc, stride, nf, s)));
-        return p.pipe1m == 4 ? launch_passB_1m<8, 2, 64 | 128>(p, nf, o, s) : launch_passB_1m<8, 0, 64 | 128>(p, nf, o, s);
-    }
-    bool tm = false;
-    if (p.sA1m == 8) {
-        if (p.var1m == 73) SDRGPU_CHECK((launch_passA_1m<8, 0, 73>(p, xc, stride, nf, s)));
-        else if (p.var1m & 64) SDRGPU_CHECK((launch_passA_1m<8, 0, 64>(p, xc, stride, nf, s)));
-        else SDRGPU_CHECK((launch_passA_1m<8, 0, 0>(p, xc, stride, nf, s)));
-    } else {
-        switch (p.var1m) {
-        // default: the input rows are read once, non-temporal (slc), so they do not push the 4 MB
-        // window out of L2 (PMC fetch 18.15 -> 17.50 B/sample, C2 1.848 -> 1.798 ms, 3 interleaved
-        // runs; non-temporal pass-B loads of the intermediate measured 2.41 ms: it must stay cached)
-        case 128: SDRGPU_CHECK((launch_passA_1m<16, 2, 128>(p, xc, stride, nf, s))); tm = true; break;
-        case 137: SDRGPU_CHECK((launch_passA_1m<16, 0, 137>(p, xc, stride, nf, s))); tm = true; break;
-        case 144: SDRGPU_CHECK((launch_passA_1m<16, 0, 144>(p, xc, stride, nf, s))); tm = true; break;   // (measurement)
-        case 160: SDRGPU_CHECK((launch_passA_1m<16, 0, 160>(p, xc, stride, nf, s))); tm = true; break;
-        case 176: SDRGPU_CHECK((launch_passA_1m<16, 0, 176>(p, xc, stride, nf, s))); tm = true; break;
-        case 9: SDRGPU_CHECK((launch_passA_1m<16, 0, 9>(p, xc, stride, nf, s))); break;
-        case 16: SDRGPU_CHECK((launch_passA_1m<16, 0, 16>(p, xc, stride, nf, s))); break;
-        case 32: SDRGPU_CHECK((launch_passA_1m<16, 0, 32>(p, xc, stride, nf, s))); break;
-        case 48: SDRGPU_CHECK((launch_passA_1m<16, 0, 48>(p, xc, stride, nf, s))); break;
-        default: SDRGPU_CHECK((launch_passA_1m<16, 0, 0>(p, xc, stride, nf, s))); break;
-        }
-    }
-    if (tm) {
-        switch (p.var1mB) {   // (16 / 32 / 48: measurement only)
-        case 16: return launch_passB_1m<8, 0, 64 | 128 | 16>(p, nf, o, s);
-        case 32: return launch_passB_1m<8, 0, 64 | 128 | 32>(p, nf, o, s);
-        case 48: return launch_passB_1m<8, 0, 64 | 128 | 48>(p, nf, o, s);
-        }
-        return p.sB1m == 8 ? launch_passB_1m<8, 0, 64 | 128>(p, nf, o, s) : launch_passB_1m<16, 0, 128>(p, nf, o, s);
-    }
-    if (p.sB1m == 8) return (p.var1mB & 64) ? launch_passB_1m<8, 0, 64>(p, nf, o, s) : launch_passB_1m<8, 0, 0>(p, nf, o, s);
-    switch (p.var1mB) {
-    case 64: return launch_passB_1m<16, 0, 64>(p, nf, o, s);
-    case 16: return launch_passB_1m<16, 0, 16>(p, nf, o, s);
-    case 32: return launch_passB_1m<16, 0, 32>(p, nf, o, s);
-    case 48: return launch_passB_1m<16, 0, 48>(p, nf, o, s);
-    default: return launch_passB_1m<16, 0>(p, nf, o, s);
-    }
-}
-
-static bool pipe1m_ok(const FftPlan& p, bool paired) { return p.pipe1m && paired && p.N1 == 1024 && p.N2 == 1024 && (p.nz % 2) == 0; }
-
-// merged pass B (chunk c) + pass A (chunk c+1) launches: the 64k split (256 x 256, one-column
-// pass A). The 1M split's merged form (paired pass A, pass B at 8 rows to match its 512
-// threads) measured 12% SLOWER (2.68 vs 2.39 ms per 256 frames): pass B loses half its
-// occupancy to pass A's 147 KB of LDS, so the 1M transform keeps separate launches.
-static int dispatch_merged(const FftPlan& p, const float2* scratchB, int framesB, float* outB, const float2* in,
-                           long long stride, int framesA, float2* scratchA, hipStream_t s, float* zoomB = nullptr) {
-    if (zoomB) return launch_merged<256, 32, 256, 32, false, true>(p, scratchB, framesB, outB, in, stride, framesA, scratchA, s, zoomB);
-    if (p.sa == 64) return launch_merged<256, 64, 256, 64, false>(p, scratchB, framesB, outB, in, stride, framesA, scratchA, s);
-    if (p.sa == 32) return launch_merged<256, 32, 256, 32, false>(p, scratchB, framesB, outB, in, stride, framesA, scratchA, s);
-    return launch_merged<256, 16, 256, 16, false>(p, scratchB, framesB, outB, in, stride, framesA, scratchA, s);
-}
 static bool merged_supported(const FftPlan& p, bool paired) {
-    return !paired && p.N1 == 256 && p.N2 == 256 && (p.sa == 16 || ((p.sa == 32 || p.sa == 64) && p.sb == p.sa));
+    return !paired && p.N1 == 256 && p.N2 == 256 && p.sa == 32 && p.sb == 32;
 }
+
+template <typename K>
+static int resident_grid(const FftPlan& p, K k, int threads, size_t lds, int& grid) {
+    if (!grid) {
+        int per = 0, cus = 0;
+        SDRGPU_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k, threads, lds));
+        SDRGPU_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p.device));
+        grid = std::max(1, per) * cus;
+    }
+    return SDRGPU_OK;
+}
+
+// the persistent 1M passes for one chunk (pass B reads pass A's tile-major intermediate)
+static int dispatch_1m(FftPlan& p, const float2* xc, long long stride, int nf, float* o, hipStream_t s) {
+    {
+        auto k = fft_passA_1m_kernel;
+        const size_t lds = sizeof(float2) * (16 * Lds<1024>::LS + 1024 + 256);
+        SDRGPU_CHECK(set_lds(k, lds));
+        SDRGPU_CHECK(resident_grid(p, k, 512, lds, p.gridA));
+        const int ntiles = (p.N2 / 16) * nf;
+        hipLaunchKernelGGL(k, dim3(std::min(p.gridA, ntiles)), dim3(512), lds, s, xc, stride, nf, p.win.as<float>(), p.nz,
+                           p.N2, p.logN, p.tw1.as<float2>(), p.wt.as<double2>(), p.cur);
+        SDRGPU_HIP(hipGetLastError());
+    }
+    auto k = fft_passB_1m_kernel;
+    const size_t lds = sizeof(float2) * (8 * Lds<1024>::LS + 1024 + 256);
+    SDRGPU_CHECK(set_lds(k, lds));
+    SDRGPU_CHECK(resident_grid(p, k, 512, lds, p.gridB));
+    const int ntiles = (p.N1 / 8) * nf;
+    hipLaunchKernelGGL(k, dim3(std::min(p.gridB, ntiles)), dim3(512), lds, s, p.cur, nf, p.N1, p.logN, p.tw2.as<float2>(), o);
+    SDRGPU_HIP(hipGetLastError());
+    return SDRGPU_OK;
+}
+
+static bool pipe1m_ok(const FftPlan& p, bool paired) { return paired && p.N1 == 1024 && p.N2 == 1024 && (p.nz % 2) == 0; }
 
 static int dispatch_single(const FftPlan& p, const float2* in, long long stride, int frames, float* out, hipStream_t s) {
     switch (p.N) {
@@ -1937,33 +1238,23 @@ static int dispatch_passA(const FftPlan& p, const float2* in, long long stride, 
     case 64: return launch_passA<64, 16>(p, in, stride, frames, s);
     case 128: return launch_passA<128, 16>(p, in, stride, frames, s);
     case 256:
-        if (p.sa == 64) return launch_passA<256, 64>(p, in, stride, frames, s);
         if (p.sa == 32) return launch_passA<256, 32>(p, in, stride, frames, s);
         return launch_passA<256, 16>(p, in, stride, frames, s);
     case 512: return launch_passA<512, 8>(p, in, stride, frames, s);
-    case 1024:
-        if (p.sa == 16) return launch_passA<1024, 16>(p, in, stride, frames, s);
-        return launch_passA<1024, 8>(p, in, stride, frames, s);   // (sa 8 only on request)
+    case 1024: return launch_passA<1024, 16>(p, in, stride, frames, s);
     }
     set_error("fft: unsupported N1 %d", p.N1);
     return SDRGPU_EARG;
 }
 
-// paired-column pass A (16-B accesses); used when the input allows 16-B loads
+// paired-column pass A (16-B accesses; +13% on the 1M transform, slower than the one-column kernel
+// at N1 = 256): N1 >= 512, when the input allows 16-B loads
 static int dispatch_passA2(const FftPlan& p, const float2* in, long long stride, int frames, hipStream_t s) {
     switch (p.N1) {
-    case 64: return launch_passA2<64, 32>(p, in, stride, frames, s);
-    case 128: return launch_passA2<128, 32>(p, in, stride, frames, s);
-    case 256:
-        if (p.sa2 == 64) return launch_passA2<256, 64>(p, in, stride, frames, s);
-        if (p.sa2 == 16) return launch_passA2<256, 16>(p, in, stride, frames, s);
-        return launch_passA2<256, 32>(p, in, stride, frames, s);
     case 512: return launch_passA2<512, 16>(p, in, stride, frames, s);
-    case 1024:
-        if (p.sa2 == 8) return launch_passA2<1024, 8>(p, in, stride, frames, s);   // (tuning; 2.68 vs 2.10 ms)
-        return launch_passA2<1024, 16>(p, in, stride, frames, s);
+    case 1024: return launch_passA2<1024, 16>(p, in, stride, frames, s);
     }
-    set_error("fft: unsupported N1 %d", p.N1);
+    set_error("fft: unsupported paired N1 %d", p.N1);
     return SDRGPU_EARG;
 }
 
@@ -1972,14 +1263,9 @@ static int dispatch_passB(const FftPlan& p, int frames, float* out, hipStream_t 
     switch (p.N2) {
     case 64: return launch_passB<64, 32>(p, frames, out, s);
     case 128: return launch_passB<128, 32>(p, frames, out, s);
-    case 256:
-        if (p.sb == 64) return launch_passB<256, 64>(p, frames, out, s);
-        if (p.sb == 16) return launch_passB<256, 16>(p, frames, out, s);
-        return launch_passB<256, 32>(p, frames, out, s);
+    case 256: return launch_passB<256, 32>(p, frames, out, s);
     case 512: return launch_passB<512, 16>(p, frames, out, s);
-    case 1024:
-        if (p.sb == 8) return launch_passB<1024, 8>(p, frames, out, s);   // (tuning; equal time)
-        return launch_passB<1024, 16>(p, frames, out, s);
+    case 1024: return launch_passB<1024, 16>(p, frames, out, s);
     }
     set_error("fft: unsupported N2 %d", p.N2);
     return SDRGPU_EARG;
@@ -2021,10 +1307,6 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         rc = make_twiddles(p.tw1, fftSize);
     } else {
         p.N1 = 1 << ((logN + 1) / 2);   // N1 >= N2, both <= 1024
-        if (const char* e = tuning_env("SDRGPU_FFT_N1")) {   // (tuning) another split, N1, N2 in [64, 1024]
-            const int n1 = atoi(e);
-            if (n1 >= 64 && n1 <= 1024 && (n1 & (n1 - 1)) == 0 && fftSize / n1 >= 64 && fftSize / n1 <= 1024) p.N1 = n1;
-        }
         p.N2 = fftSize / p.N1;
         rc = make_twiddles(p.tw1, p.N1);
         if (rc >= 0) rc = make_twiddles(p.tw2, p.N2);
@@ -2042,28 +1324,13 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         // pass-B dB segments, 512 threads, 2 workgroups per CU): the merged spectrum launches
         // take 1.44 vs 1.58 ms per 2^28 samples with 16 / 16 (A/B on one box)
         if (p.N1 == 256 && p.N2 == 256) p.sa = p.sb = 32;
-        if (const char* e = tuning_env("SDRGPU_FFT_SA")) p.sa = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FFT_SB")) p.sb = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FFT_PIPE")) p.pipe = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_MERGE")) p.merge = atoi(e);
         p.chunkFrames = std::max(1, (int)((chunkMB << 20) / ((long long)fftSize * 8)));
         // paired-column pass A: +13% on the 1M transform (N1 = 1024), but slower than the
         // one-column kernel at N1 = 256 (64k: 2.05-2.10 vs 1.86 ms per 2^28 samples, A/B on
         // one box), so it is the default only for N1 >= 512
         p.sa2 = p.N1 >= 512 ? 16 : 0;
-        if (const char* e = tuning_env("SDRGPU_FFT_SA2")) p.sa2 = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FFT_1M")) p.pipe1m = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FFT_MERGE_1M")) p.merge1m = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FFT_1M_VAR")) p.var1m = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FFT_1M_VARB")) p.var1mB = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FFT_1M_SA")) p.sA1m = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FFT_1M_SB")) p.sB1m = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FFT_VFO_CP")) p.vfoCP = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FFT_VFO_FUSE")) p.vfoFuse = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FFT_VFO_XCD")) p.vfoXcd = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FFT_VFO_SIDE")) p.vfoSide = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FFT_VFO_PERSIST")) p.vfoPersist = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FFT_PERSIST_LAG")) p.persistLag = std::max(1, atoi(e));
         if (const char* e = tuning_env("SDRGPU_FFT_1P")) p.onepass = atoi(e);
         if (rc >= 0 && fftSize == 65536) {   // fft_1p_kernel's exact twiddles (op1::TAB)
             std::vector<float2> t(op1::TAB);
@@ -2078,7 +1345,7 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
                 for (int t0 = 0; t0 < 16; t0++) t[4 * op1::M + 16 * q1 + t0] = w(128LL * t0 * q1);
             for (int r = 0; r < 4; r++)
                 for (int i = 0; i < 32; i++) t[4 * op1::M + 512 + 32 * r + i] = w(512LL * r * i);
-            std::vector<double2> t64(2048);   // W_N^m, m < 2048, fp64 (SDRGPU_1P_TW 1)
+            std::vector<double2> t64(2048);   // W_N^m, m < 2048, fp64 (the stage-1 twiddle recurrence)
             for (int m = 0; m < 2048; m++) {
                 const double a = -2.0 * M_PI * (double)m / (double)fftSize;
                 t64[m] = make_double2(std::cos(a), std::sin(a));
@@ -2120,7 +1387,6 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
             }
         }
     }
-    if (const char* e = tuning_env("SDRGPU_FFT_FUSE_TAIL")) p.fuseTail = atoi(e);
     if (rc >= 0 && hipStreamCreateWithFlags(&p.own, hipStreamNonBlocking) != hipSuccess) {
         set_error("fft_create: hipStreamCreate failed");
         rc = SDRGPU_EHIP;
@@ -2171,14 +1437,11 @@ static bool zoom_fusable(const FftPlan& p, int zoomSize) {
 template <bool ZM, bool VFO>
 static int launch_1p(FftPlan& p, const float2* in, long long stride, int frames, float* out, float* zoom, VfoWork v,
                      hipStream_t s) {
-    const bool half = p.onepass >= 2, w256 = p.onepass >= 3, sv = VFO && p.onepass == 4;
-    auto k = sv ? fft_1p256_kernel<ZM, VFO, true> : w256 ? fft_1p256_kernel<ZM, VFO> : half ? fft_1p_kernel<ZM, VFO, true>
-                                                                                             : fft_1p_kernel<ZM, VFO, false>;
-    const int ldsB = half ? (16 * op1::RS + 512 + 32) * 8 : op1::LDS_BYTES;
-    SDRGPU_CHECK(set_lds(k, ldsB));
+    auto k = fft_1p_kernel<ZM, VFO>;
+    SDRGPU_CHECK(set_lds(k, op1::LDS_BYTES));
     if (ZM) SDRGPU_CHECK(p.zpart.ensure(sizeof(float) * 4 * 2048 * (size_t)frames));
-    const int g = (sv ? 64 : 32) * ((frames + 7) / 8) + (VFO && v.hist ? 1 : 0);
-    hipLaunchKernelGGL(k, dim3(g), dim3(w256 ? 256 : 512), ldsB, s, in, stride, frames, p.win.as<float>(), p.nz,
+    const int g = 32 * ((frames + 7) / 8) + (VFO && v.hist ? 1 : 0);
+    hipLaunchKernelGGL(k, dim3(g), dim3(512), op1::LDS_BYTES, s, in, stride, frames, p.win.as<float>(), p.nz,
                        p.tab1p.as<float2>(), p.tab1p64.as<double2>(), out, ZM ? p.zpart.as<float>() : nullptr, v);
     SDRGPU_HIP(hipGetLastError());
     if (ZM) {
@@ -2229,65 +1492,33 @@ static int fft_execute_body(sdrgpu_fft* h, const void* in, long long frameStride
         SDRGPU_CHECK(p.scratch2.ensure(p.scratch.bytes));
         float2* sc[2] = {p.scratch.as<float2>(), p.scratch2.as<float2>()};
         p.cur = sc[0];
-        if (paired) SDRGPU_CHECK(dispatch_passA2(p, x, frameStride, std::min(p.chunkFrames, frames), s));
-        else SDRGPU_CHECK(dispatch_passA(p, x, frameStride, std::min(p.chunkFrames, frames), s));
+        SDRGPU_CHECK(dispatch_passA(p, x, frameStride, std::min(p.chunkFrames, frames), s));
         for (int c = 1; c < nchunks; c++) {
             const int fB = (c - 1) * p.chunkFrames, nfB = p.chunkFrames;
             const int fA = c * p.chunkFrames, nfA = std::min(p.chunkFrames, frames - fA);
-            SDRGPU_CHECK(dispatch_merged(p, sc[(c - 1) & 1], nfB, out + (long long)fB * p.N,
-                                         x + (long long)fA * frameStride, frameStride, nfA, sc[c & 1], s, zoomAt(fB)));
+            const float2* xa = x + (long long)fA * frameStride;
+            float* ob = out + (long long)fB * p.N;
+            if (zoom) SDRGPU_CHECK(launch_merged<true>(p, sc[(c - 1) & 1], nfB, ob, xa, frameStride, nfA, sc[c & 1], s, zoomAt(fB)));
+            else SDRGPU_CHECK(launch_merged<false>(p, sc[(c - 1) & 1], nfB, ob, xa, frameStride, nfA, sc[c & 1], s));
         }
         const int fL = (nchunks - 1) * p.chunkFrames;
         p.cur = sc[(nchunks - 1) & 1];
         SDRGPU_CHECK(dispatch_passB(p, frames - fL, out + (long long)fL * p.N, s, zoomAt(fL)));
         return frames;
     }
-    const bool pipe = p.pipe && nchunks > 1 && !zoom;
-    if (pipe) {
-        SDRGPU_CHECK(ensure_side(p));
-        SDRGPU_CHECK(p.scratch2.ensure(p.scratch.bytes));
-        SDRGPU_HIP(hipEventRecord(p.evFork, s));
-        SDRGPU_HIP(hipStreamWaitEvent(p.s2, p.evFork, 0));
-    }
-    if (pipe1m_ok(p, paired) && !pipe && !zoom && p.merge1m && nchunks > 1 && p.var1m == 128 && p.sA1m == 16 && p.sB1m == 8 &&
-        p.var1mB == 64) {
-        // A(0); [B(c - 1) + A(c)] for c = 1 ..; B(last): the chunks alternate between two scratch buffers
-        SDRGPU_CHECK(p.scratch2.ensure(p.scratch.bytes));
-        float2* sc[2] = {p.scratch.as<float2>(), p.scratch2.as<float2>()};
-        const int cf = p.chunkFrames;
-        SDRGPU_CHECK(launch_merged_1m(p, nullptr, 0, nullptr, x, frameStride, std::min(cf, frames), sc[0], s));
-        for (int c = 1; c < nchunks; c++) {
-            const int fB = (c - 1) * cf, fA = c * cf;
-            SDRGPU_CHECK(launch_merged_1m(p, sc[(c - 1) & 1], cf, out + (long long)fB * p.N, x + (long long)fA * frameStride,
-                                          frameStride, std::min(cf, frames - fA), sc[c & 1], s));
-        }
-        const int fL = (nchunks - 1) * cf;
-        SDRGPU_CHECK(launch_merged_1m(p, sc[(nchunks - 1) & 1], frames - fL, out + (long long)fL * p.N, nullptr, 0, 0, nullptr, s));
-        return frames;
-    }
+    p.cur = p.scratch.as<float2>();
     for (int c = 0; c < nchunks; c++) {
         const int f0 = c * p.chunkFrames;
         const int nf = std::min(p.chunkFrames, frames - f0);
         const float2* xc = x + (long long)f0 * frameStride;
-        const int b = pipe ? (c & 1) : 0;
-        p.cur = b ? p.scratch2.as<float2>() : p.scratch.as<float2>();
-        if (pipe && c >= 2) SDRGPU_HIP(hipStreamWaitEvent(s, p.evB[b], 0));   // buffer b free again
-        if (pipe1m_ok(p, paired) && !pipe) {
+        if (pipe1m_ok(p, paired)) {
             SDRGPU_CHECK(dispatch_1m(p, xc, frameStride, nf, out + (long long)f0 * p.N, s));
             continue;
         }
         if (paired) SDRGPU_CHECK(dispatch_passA2(p, xc, frameStride, nf, s));
         else SDRGPU_CHECK(dispatch_passA(p, xc, frameStride, nf, s));
-        hipStream_t sb = s;
-        if (pipe) {
-            SDRGPU_HIP(hipEventRecord(p.evA[b], s));
-            SDRGPU_HIP(hipStreamWaitEvent(p.s2, p.evA[b], 0));
-            sb = p.s2;
-        }
-        SDRGPU_CHECK(dispatch_passB(p, nf, out + (long long)f0 * p.N, sb, zoomAt(f0)));
-        if (pipe) SDRGPU_HIP(hipEventRecord(p.evB[b], p.s2));
+        SDRGPU_CHECK(dispatch_passB(p, nf, out + (long long)f0 * p.N, s, zoomAt(f0)));
     }
-    if (pipe) SDRGPU_HIP(hipStreamWaitEvent(s, p.evB[(nchunks - 1) & 1], 0));   // join
     return frames;
 }
 
@@ -2339,7 +1570,7 @@ int sdrgpu::fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const f
     // pass B + the VFO's later stages (one tail launch's workgroups) where the chain has that form
     TailArgs t;
     size_t ldsTail = 0;
-    const int tail = p.fuseTail ? vfo_tail_prepare(vfoBlock, *vfo, vfoOut, &t, &ldsTail) : 0;
+    const int tail = vfo_tail_prepare(vfoBlock, *vfo, vfoOut, &t, &ldsTail);
     if (tail < 0) return tail;
     if (tail) {
         auto k = fft_passB_tail_kernel;
@@ -2347,7 +1578,7 @@ int sdrgpu::fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const f
         SDRGPU_CHECK(set_lds(k, lds));
         hipLaunchKernelGGL(k, dim3(8 * frames + t.G), dim3(512), lds, s, p.cur, frames, p.N1, p.logN, p.tw2.as<float2>(), out, t);
         SDRGPU_HIP(hipGetLastError());
-        *vfoN = vfo_tail_commit(vfoBlock, t);
+        *vfoN = vfo_tail_commit(vfoBlock, *vfo, t);
         SDRGPU_CHECK(time_mark(p, 1, s));
         return frames;
     }
@@ -2395,16 +1626,14 @@ extern "C" int sdrgpu_fft_execute_zoom_dev(sdrgpu_fft* h, const void* in, long l
 
 // The fused launch group (fft_vfo_kernel): A(0)+V(0); [B(c-1) + A(c)+V(c)] for c = 1..; B(last) +
 // the stage's history workgroup. Scratch alternates between two buffers as in fft_execute.
-template <bool ZM, int CP, int XG = 0>
+template <bool ZM>
 static int launch_vfo(FftPlan& p, const float2* scratchB, int framesB, float* outB, float* zoomB, const float2* in,
                       int framesA, float2* scratchA, VfoWork v, hipStream_t s) {
-    auto k = fft_vfo_kernel<ZM, CP, XG>;
+    auto k = fft_vfo_kernel<ZM>;
     const size_t lds = sizeof(float2) * (32 * Lds<256>::LS + 256 + 256);
     SDRGPU_CHECK(set_lds(k, lds));
     const int nB = 8 * framesB;
-    const int g = (XG == 2 ? 136 * ((std::max(framesA, framesB) + 7) / 8)
-                           : nB + (XG == 3 ? 96 * ((framesA + 7) / 8) : XG ? 72 * ((framesA + 7) / 8) : 9 * framesA)) +
-                  (v.hist ? 1 : 0);
+    const int g = nB + 96 * ((framesA + 7) / 8) + (v.hist ? 1 : 0);
     hipLaunchKernelGGL(k, dim3(g), dim3(512), lds, s, nB, scratchB, framesB, outB, zoomB, in, (long long)p.N, framesA,
                        p.win.as<float>(), p.nz, p.logN, p.tw1.as<float2>(), p.tw2.as<float2>(), p.tfull.as<float2>(),
                        scratchA, v);
@@ -2413,73 +1642,18 @@ static int launch_vfo(FftPlan& p, const float2* scratchB, int framesB, float* ou
 }
 static int dispatch_vfo(FftPlan& p, bool zm, const float2* scratchB, int framesB, float* outB, float* zoomB,
                         const float2* in, int framesA, float2* scratchA, const VfoWork& v, hipStream_t s) {
-    if (p.vfoXcd == 3) {
-        if (p.vfoCP == 2)   // (tuning) streaming pass-A input loads: the stage's L2 hits, no Infinity-Cache allocation
-            return zm ? launch_vfo<true, 2, 3>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
-                      : launch_vfo<false, 2, 3>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
-        return zm ? launch_vfo<true, 0, 3>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
-                  : launch_vfo<false, 0, 3>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
-    }
-    if (p.vfoXcd == 2) return zm ? launch_vfo<true, 0, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
-                                 : launch_vfo<false, 0, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
-    if (p.vfoXcd) return zm ? launch_vfo<true, 0, 1>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
-                            : launch_vfo<false, 0, 1>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
-    if (zm) return p.vfoCP == 2 ? launch_vfo<true, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
-                                : launch_vfo<true, 0>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
-    return p.vfoCP == 2 ? launch_vfo<false, 2>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
-                        : launch_vfo<false, 0>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
+    return zm ? launch_vfo<true>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s)
+              : launch_vfo<false>(p, scratchB, framesB, outB, zoomB, in, framesA, scratchA, v, s);
 }
 static bool vfo_fusable(const FftPlan& p, float* zoom, int zoomSize) {
     return p.vfoFuse && !p.f64 && p.N1 == 256 && p.N2 == 256 && p.sa == 32 && p.sb == 32 && p.sa2 == 0 && p.nz == p.N &&
            (zoom == nullptr || zoom_fusable(p, zoomSize));
 }
 // Returns the VFO's output count: its later stages (vfo_stage1_finish) need only the stage-1 outputs,
-// complete once the last pass-A launch is done, so they run on the plan's side stream beside the last
-// launch (pass B of the last chunk + the stage's history), and the call's stream joins them.
-// the group as one fft_vfo_persist_kernel launch (SPX devices: 8 XCDs, read by HW_REG_XCC_ID)
-static int fft_execute_vfo_persist(FftPlan& p, const float2* x, int frames, float* out, float* zoom, const VfoStage1& st,
-                                   hipStream_t s) {
-    SDRGPU_CHECK(p.scratch.ensure((size_t)8 * kPersistRing * p.N * sizeof(float2)));
-    const size_t ctl = sizeof(int) * (8 + 2 * (size_t)frames + 1);
-    SDRGPU_CHECK(p.persistCtl.ensure(ctl));
-    int* c = p.persistCtl.as<int>();
-    SDRGPU_HIP(hipMemsetAsync(c, 0, ctl, s));
-    PersistWork w{VfoWork{st.a, 0, 0}, frames, p.persistLag, c, c + 8, c + 8 + frames, c + 8 + 2 * frames};
-    auto k = p.vfoPersist == 2 ? (zoom ? fft_vfo_persist_kernel<true, true> : fft_vfo_persist_kernel<false, true>)
-                               : (zoom ? fft_vfo_persist_kernel<true> : fft_vfo_persist_kernel<false>);
-    const size_t lds = sizeof(float2) * (32 * Lds<256>::LS + 256 + 256);
-    SDRGPU_CHECK(set_lds(k, lds));
-    if (!p.gridP) {
-        int per = 0, cus = 0;
-        SDRGPU_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k, 512, lds));
-        SDRGPU_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p.device));
-        p.gridP = std::max(1, std::min(per, 2)) * cus;
-    }
-    SDRGPU_CHECK(time_mark(p, 0, s));
-    hipLaunchKernelGGL(k, dim3(p.gridP), dim3(512), lds, s, x, out, zoom, p.win.as<float>(), p.nz, p.logN,
-                       p.tw1.as<float2>(), p.tw2.as<float2>(), p.tfull.as<float2>(), p.scratch.as<float2>(), w);
-    SDRGPU_HIP(hipGetLastError());
-    return time_mark(p, 1, s);
-}
-// spin timeouts of the last persistent launch (synchronises the plan's stream; tests)
-extern "C" int sdrgpu_fft_persist_errors(sdrgpu_fft* h, int frames) {
-    if (!h || !h->p.persistCtl.p) return 0;
-    int e = 0;
-    SDRGPU_HIP(hipDeviceSynchronize());
-    SDRGPU_HIP(hipMemcpy(&e, h->p.persistCtl.as<int>() + 8 + 2 * frames, sizeof(int), hipMemcpyDeviceToHost));
-    return e;
-}
-
+// complete once the last pass-A launch is done; they run after the group on the call's stream (on a
+// side stream beside the last launch they measured slower: 1.725 vs 1.705 ms, r4i).
 static int fft_execute_vfo(FftPlan& p, const float2* x, int frames, float* out, float* zoom, const VfoStage1& st,
                            sdrgpu_block* vfo, void* vfoOut, hipStream_t s) {
-    if (p.vfoPersist) {
-        int cus = 0;
-        SDRGPU_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p.device));
-        if (cus == 256) {
-            SDRGPU_CHECK(fft_execute_vfo_persist(p, x, frames, out, zoom, st, s));
-            return vfo_stage1_finish(vfo, st, vfoOut, s);
-        }
-    }
     if (onepass_ok(p)) {
         VfoWork v{st.a, 0, 1};
         SDRGPU_CHECK(time_mark(p, 0, s));
@@ -2505,24 +1679,11 @@ static int fft_execute_vfo(FftPlan& p, const float2* x, int frames, float* out, 
         SDRGPU_CHECK(dispatch_vfo(p, zoom != nullptr, sc[(c - 1) & 1], cf, out + (long long)fB * p.N, zoomAt(fB),
                                   x + (long long)fA * p.N, nfA, sc[c & 1], v, s));
     }
-    int m = 0;
-    if (p.vfoSide) {
-        SDRGPU_CHECK(ensure_side(p));
-        SDRGPU_HIP(hipEventRecord(p.evFork, s));
-        SDRGPU_HIP(hipStreamWaitEvent(p.s2, p.evFork, 0));
-        m = vfo_stage1_finish(vfo, st, vfoOut, p.s2);
-        if (m < 0) return m;
-        SDRGPU_HIP(hipEventRecord(p.evJoin, p.s2));
-    }
     const int fL = (nchunks - 1) * cf;
     v.hist = 1;
     SDRGPU_CHECK(dispatch_vfo(p, zoom != nullptr, sc[(nchunks - 1) & 1], frames - fL, out + (long long)fL * p.N, zoomAt(fL),
                               nullptr, 0, nullptr, v, s));
     SDRGPU_CHECK(time_mark(p, 1, s));
-    if (p.vfoSide) {
-        SDRGPU_HIP(hipStreamWaitEvent(s, p.evJoin, 0));
-        return m;
-    }
     return vfo_stage1_finish(vfo, st, vfoOut, s);
 }
 
@@ -2544,7 +1705,8 @@ extern "C" int sdrgpu_fft_execute_zoom_vfo_dev(sdrgpu_fft* h, const void* in, in
     if (count > 0x7fffffffLL) { set_error("fft_execute_vfo: %lld samples per call (max 2^31 - 1)", count); return SDRGPU_EARG; }
     // back-to-back frames: the spectrum must cover every sample the VFO consumes, on one device
     if (p.nz != p.N) { set_error("fft_execute_vfo: plan nz %d != N %d (frames must be back to back)", p.nz, p.N); return SDRGPU_EARG; }
-    if (vfo->impl && vfo->impl->device != p.device) {
+    if (!vfo->impl) { set_error("fft_execute_vfo: null VFO block handle"); return SDRGPU_EARG; }
+    if (vfo->impl->device != p.device) {
         set_error("fft_execute_vfo: VFO on device %d, spectrum plan on device %d", vfo->impl->device, p.device);
         return SDRGPU_EARG;
     }
@@ -2646,16 +1808,6 @@ extern "C" int sdrgpu_fft_destroy(sdrgpu_fft* h) {
     for (auto& e : h->p.tev)
         for (auto& ev : e)
             if (ev) (void)hipEventDestroy(ev);
-    if (h->p.s2) {
-        (void)hipStreamSynchronize(h->p.s2);
-        (void)hipStreamDestroy(h->p.s2);
-        (void)hipEventDestroy(h->p.evFork);
-        (void)hipEventDestroy(h->p.evJoin);
-        for (int k = 0; k < 2; k++) {
-            (void)hipEventDestroy(h->p.evA[k]);
-            (void)hipEventDestroy(h->p.evB[k]);
-        }
-    }
     delete h;
     return SDRGPU_OK;
 }

@@ -342,13 +342,13 @@ int fft64_execute(Fft64Plan* p, const float2* in, long long stride, int frames, 
     if (p->N1 == 0) {
         const double2* tw = p->tw1.as<double2>();
         switch (p->N) {
-        case 64: return launch_single64<64>(tw, in, stride, frames, win, nz, out, s);
-        case 128: return launch_single64<128>(tw, in, stride, frames, win, nz, out, s);
-        case 256: return launch_single64<256>(tw, in, stride, frames, win, nz, out, s);
-        case 512: return launch_single64<512>(tw, in, stride, frames, win, nz, out, s);
-        case 1024: return launch_single64<1024>(tw, in, stride, frames, win, nz, out, s);
-        case 2048: return launch_single64<2048>(tw, in, stride, frames, win, nz, out, s);
-        case 4096: return launch_single64<4096>(tw, in, stride, frames, win, nz, out, s);
+        case 64: SDRGPU_CHECK(launch_single64<64>(tw, in, stride, frames, win, nz, out, s)); return frames;
+        case 128: SDRGPU_CHECK(launch_single64<128>(tw, in, stride, frames, win, nz, out, s)); return frames;
+        case 256: SDRGPU_CHECK(launch_single64<256>(tw, in, stride, frames, win, nz, out, s)); return frames;
+        case 512: SDRGPU_CHECK(launch_single64<512>(tw, in, stride, frames, win, nz, out, s)); return frames;
+        case 1024: SDRGPU_CHECK(launch_single64<1024>(tw, in, stride, frames, win, nz, out, s)); return frames;
+        case 2048: SDRGPU_CHECK(launch_single64<2048>(tw, in, stride, frames, win, nz, out, s)); return frames;
+        case 4096: SDRGPU_CHECK(launch_single64<4096>(tw, in, stride, frames, win, nz, out, s)); return frames;
         }
         set_error("fft64: size %d", p->N);
         return SDRGPU_EARG;

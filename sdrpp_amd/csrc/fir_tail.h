@@ -37,7 +37,6 @@ struct TailArgs {
     int S, G;
     int ldsEl;            // float2 elements of the largest workgroup's images (the taps follow)
     int tapTotal;         // floats of all stages' tap tables
-    int var;              // timing variants (SDRGPU_TAIL_VAR, wrong results): 1 no stage loops, 2 no image loads
     int tapOff[TAIL_MAXS];   // float offset of stage s's [D][Q] taps behind the images
     TailStage st[TAIL_MAXS];
 };
@@ -131,7 +130,7 @@ __device__ __forceinline__ void fir_tail_block(const TailArgs& t, int w, bool la
 #pragma unroll
         for (int u = 0; u < TAIL_PF; u++) {
             const int e = g[0].B + tid + u * TAIL_NT;
-            const float2* src = (e < g[0].E && t.var != 2) ? (e < s0.H ? s0.hist + e : t.in + (e - s0.H)) : nullptr;
+            const float2* src = (e < g[0].E) ? (e < s0.H ? s0.hist + e : t.in + (e - s0.H)) : nullptr;
             v[u] = src ? *src : make_float2(0.f, 0.f);
         }
 #pragma unroll
@@ -167,7 +166,7 @@ __device__ __forceinline__ void fir_tail_block(const TailArgs& t, int w, bool la
             const TailGeom q = gs[s];
             if (last)
                 for (int k = tid; k < st.H; k += TAIL_NT) st.histNext[k] = XS[slot(q, st.dsh, st.n + k - q.B)];
-            const int nthr = t.var == 1 ? 0 : (q.b - q.a + TAIL_K - 1) / TAIL_K;
+            const int nthr = (q.b - q.a + TAIL_K - 1) / TAIL_K;
             for (int l = tid; l < nthr; l += TAIL_NT) {
                 float2 acc[TAIL_K];
 #pragma unroll
@@ -214,10 +213,10 @@ __device__ __forceinline__ void fir_tail_block(const TailArgs& t, int w, bool la
 }
 
 // the tail of a VFO whose first stage ran in the front end's pass-A launch, as the pass-B launch
-// carries it (blocks.hip): 1 = t / lds filled and the VFO's first stage committed -- the caller
-// launches the t.G tail workgroups, then calls vfo_tail_commit; 0 = not applicable (nothing changed:
-// the caller then calls vfo_stage1_finish)
+// carries it (blocks.hip): 1 = t / lds filled, no state changed -- the caller launches the t.G tail
+// workgroups, then calls vfo_tail_commit (stage 1 and the tail stages move on together); 0 = not
+// applicable (nothing changed: the caller then calls vfo_stage1_finish)
 int vfo_tail_prepare(::sdrgpu_block* vfo, const VfoStage1& st, void* out, TailArgs* t, size_t* lds);
-int vfo_tail_commit(::sdrgpu_block* vfo, const TailArgs& t);
+int vfo_tail_commit(::sdrgpu_block* vfo, const VfoStage1& st, const TailArgs& t);
 
 }  // namespace sdrgpu

@@ -574,15 +574,25 @@ def gather_id():
 class SpectraGather:
     """Rank-0 gather of spectrum rows over RCCL (sdrgpu_gather_*): one rank per GPU / IQ stream."""
 
-    def __init__(self, rank, world, comm_id, device=0):
+    def __init__(self, rank, world, comm_id, device=0, timeout=None):
+        """device < 0: the calling thread's current HIP device. Every wait on the peers (this
+        constructor, gather_dev, wait) has a deadline: `timeout` s, else SDRGPU_GATHER_TIMEOUT_S
+        (default 120); on expiry the communicator is aborted and SdrGpuError names the rank."""
         assert len(comm_id) == 128
         self.rank, self.world = rank, world
         self._id = ctypes.create_string_buffer(bytes(comm_id), 128)
         self._h = _make(lib.sdrgpu_gather_create, int(device), int(rank), int(world), self._id)
+        if timeout is not None:
+            check(lib.sdrgpu_gather_set_timeout(self._h, float(timeout)))
 
     def gather_dev(self, rows_ptr, count, out_ptr, stream=None):
         """count device floats -> rank 0's out (world x count); asynchronous on `stream`."""
         check(lib.sdrgpu_gather_rows(self._h, _vp(rows_ptr), int(count), _vp(out_ptr or 0), _vp(stream or 0)))
+
+    def wait(self, stream=None, timeout=0.0):
+        """Wait for the gathers enqueued on `stream` against the deadline (timeout <= 0: the
+        handle's); raises SdrGpuError (communicator aborted) when a peer never completes its part."""
+        check(lib.sdrgpu_gather_wait(self._h, _vp(stream or 0), float(timeout)))
 
     def close(self):
         if self._h:

@@ -22,11 +22,15 @@ class StreamShard:
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.backend = backend
         if self.world > 1 and not dist.is_initialized():
+            # the process group's collectives (id broadcast, barriers, max over ranks) share the
+            # gather's deadline: a rank that never arrives ends the run with an error, not a hang
+            import datetime
+            tmo = datetime.timedelta(seconds=float(os.environ.get("SDRGPU_GATHER_TIMEOUT_S", "120")) + 60)
             if backend == "nccl":
                 torch.cuda.set_device(self.local)
-                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local), timeout=tmo)
             else:
-                dist.init_process_group(backend or "gloo")
+                dist.init_process_group(backend or "gloo", timeout=tmo)
 
     # stream parameters of this rank's SDR: a distinct seed and VFO offset per stream
     def seed(self, base=0xACE1):
@@ -135,6 +139,9 @@ class GatherPipeline:
         self.steps += 1
 
     def drain(self, stream):
+        finish = getattr(self.be, "finish", None)
+        if finish is not None:   # the gathers complete (or fail loudly) before anyone waits on them
+            finish()
         for e in self.done:
             if e is not None:
                 self.be.wait(stream, e)
@@ -181,6 +188,12 @@ class CudaGather:
 
     def gather(self, buf, count, out, stream, tag=None):
         self.g.gather_dev(buf.data_ptr(), count, out.data_ptr() if out is not None else 0, stream.cuda_stream)
+
+    def finish(self):
+        """Wait for every enqueued gather against the gather deadline (sdrgpu_gather_wait), so a
+        peer that died fails this rank with an error instead of a device synchronise that never
+        returns."""
+        self.g.wait(self.gstream.cuda_stream)
 
     def elapsed_ms(self, a, b):
         return a.elapsed_time(b)
