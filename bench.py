@@ -239,12 +239,15 @@ def cpu_baseline(config, seconds, bytes_per_sample=None):
     h = r["host"]
     out = {"value": round(r["value_all_cores"], 3), "unit": "MS/s", "cores": r["cores_all"], "kind": "port",
            "cores_source": r["cores_source"], "value_1core": round(r["value_1core"], 3),
-           "sample": f"{r['variant']}: {r['cores_all']} independent streams x {seconds:.0f} s (all-core aggregate), "
+           "value_packed": round(r["value_all_cores_packed"], 3), "value_spread": round(r["value_all_cores_spread"], 3),
+           "placement": r["placement"],
+           "sample": f"{r['variant']}: {r['cores_all']} independent streams x {seconds:.0f} s (all-core aggregate, the "
+                     f"faster of two placements: packed on the first CPUs, spread one per L3 domain over the sockets), "
                      f"1 stream {r['value_1core']:.2f} MS/s; 1-core variants "
                      + ", ".join(f"{k} {v:.2f}" for k, v in r["variants_1core"].items())
                      + f"; {r['build']}; SpeedTester-style 1e6-sample blocks of uniform [-1,1) IQ",
            "host": {"nproc": h["nproc"], "affinity_cpus": h["affinity"], "cgroup_cpu_quota": h["cgroup_cpu_quota"],
-                    "model": h["model"], "core_max_mhz": h["core_max_mhz"]}}
+                    "model": h["model"], "core_max_mhz": h["core_max_mhz"], "placement": h.get("placement")}}
     # the whole machine, extrapolated linearly from one core over every affinity CPU (SMT siblings
     # counted as cores: an upper bound for the CPU side)
     out["value_all_affinity_cpus_linear"] = round(r["value_1core"] * h["affinity"], 1)

@@ -211,3 +211,37 @@ void cf_quad(const float* in, int count, float* out, float* dre, float* dim, flo
     }
     *dre = pr; *dim = pim;
 }
+
+/* ------------------------------------------------ C4 channelizer branch FIRs */
+/* The polyphase channelizer's branch filters (the GPU's algorithm, SURVEY 8d C4: bank layout
+ * polyphase_bank.h:32, 16 taps per branch): u[f][m] = sum_q h[q][m] x[f + q][m] for f < frames,
+ * m < M; x = frames + Q - 1 rows of M complex samples (interleaved), h = Q rows of M real taps.
+ * Eight complex outputs per vector; the Q tap rows and the Q input rows of one output row stay in
+ * L2 (Q x 8 KB each at M = 1024). The caller FFTs each row u[f]. */
+void cf_chan_fir(const float* x, const float* h, int M, int Q, int frames, float* u) {
+    const size_t row = 2 * (size_t)M;
+    for (int f = 0; f < frames; f++) {
+        float* uo = u + (size_t)f * row;
+        int m = 0;
+        for (; m + 8 <= M; m += 8) {
+            v16f acc = splat(0);
+            for (int q = 0; q < Q; q++) {
+                const float* hq = h + (size_t)q * M + m;
+                const v16f hv = {hq[0], hq[0], hq[1], hq[1], hq[2], hq[2], hq[3], hq[3],
+                                 hq[4], hq[4], hq[5], hq[5], hq[6], hq[6], hq[7], hq[7]};
+                acc += ld(x + (size_t)(f + q) * row + 2 * (size_t)m) * hv;
+            }
+            st(uo + 2 * (size_t)m, acc);
+        }
+        for (; m < M; m++) {
+            float re = 0, im = 0;
+            for (int q = 0; q < Q; q++) {
+                const float* xq = x + (size_t)(f + q) * row + 2 * (size_t)m;
+                re += xq[0] * h[(size_t)q * M + m];
+                im += xq[1] * h[(size_t)q * M + m];
+            }
+            uo[2 * (size_t)m] = re;
+            uo[2 * (size_t)m + 1] = im;
+        }
+    }
+}

@@ -112,6 +112,7 @@ def _load():
         "orc_chain_create": (vp, [d, i, d, i]),
         "orc_chain_process": (l, [vp, vp, l, vp, l, vp]),
         "orc_chain_destroy": (None, [vp]),
+        "cf_chan_fir": (None, [vp, vp, i, i, i, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -158,6 +159,16 @@ def channelize(x, h, M, chans):
     out = np.zeros((len(ch), frames), np.complex128)
     rc = lib.orc_channelize(_p(x), len(x), _p(h), len(h), int(M), _p(ch), len(ch), _p(out))
     assert rc == frames
+    return out
+
+
+def chan_branch_fir(x, h, frames, out=None):
+    """CPU-baseline kernel (cpu_fast.c): the channelizer's branch FIRs u[f][m] = sum_q h[q][m] x[f+q][m]
+    over x [frames + Q - 1][M] complex64 and h [Q][M] float32 -> u [frames][M] complex64."""
+    Q, M = h.shape
+    if out is None:
+        out = np.empty((frames, M), np.complex64)
+    lib.cf_chan_fir(_p(x), _p(h), int(M), int(Q), int(frames), _p(out))
     return out
 
 

@@ -47,3 +47,43 @@ def test_fast_rxvfo_wfm_match_precise():
     assert a.shape == b.shape
     a, b = a.view(np.float32), b.view(np.float32)
     assert np.abs(a - b).max() < 2e-3, np.abs(a - b).max()
+
+
+def test_fast_channelizer_branch_fir_matches_numpy():
+    """C4's CPU leg: the C branch FIRs (cpu_fast.c cf_chan_fir) equal the numpy restatement
+    u[f] = sum_q h[q] x[f + q] (fp32 sums in tap order up to the vector FMA contraction)."""
+    M, Q, frames = 1024, 16, 70
+    x = _x((frames + Q - 1) * M, 11).reshape(frames + Q - 1, M)
+    h = oracle.windowed_sinc(Q * M, np.pi / M).reshape(Q, M).astype(np.float32)
+    u = oracle.chan_branch_fir(np.ascontiguousarray(x), np.ascontiguousarray(h), frames)
+    ref = np.zeros((frames, M), np.complex128)
+    for q in range(Q):
+        ref += h[q].astype(np.float64) * x[q:q + frames].astype(np.complex128)
+    assert np.abs(u - ref).max() <= 1e-6 * (1 + np.abs(ref).max())
+
+
+def test_spread_placement_one_stream_per_l3(monkeypatch):
+    """The all-core CPU leg's spread placement: on a 2-socket host with 4 L3
+    domains per socket and SMT siblings, 8 streams land one per L3 domain, alternating sockets, on
+    first threads of distinct cores; 12 streams start a second core per domain only after every
+    domain has one. The packed placement is the first CPUs in order."""
+    import cpu_baseline as cb
+    # cpu c: socket c // 32 (SMT sibling c + 64 on the same core), L3 domain (c % 64) // 8 within it
+    cpus = list(range(128))
+
+    def topo(cs):
+        out = {}
+        for c in cs:
+            p = c % 64
+            out[c] = (str(p // 32), f"l3-{p // 8}", f"core-{p}")
+        return out
+    monkeypatch.setattr(cb, "cpu_topology", topo)
+    place, info = cb.placements(cpus, 8)
+    assert info == {"sockets": 2, "l3_domains": 8}
+    assert place["packed"] == list(range(8))
+    sp = place["spread"]
+    assert len(set((c % 64) // 8 for c in sp)) == 8            # one per L3 domain
+    assert [(c % 64) // 32 for c in sp] == [0, 1] * 4           # sockets alternate
+    assert all(c < 64 for c in sp)                               # first SMT thread of each core
+    sp12 = cb.placements(cpus, 12)[0]["spread"]
+    assert sp12[:8] == sp and len(set(sp12)) == 12 and all(c < 64 for c in sp12)

@@ -989,10 +989,12 @@ def test_spectrum_vfo_fused_xcd(frames_list, pre, chunk_mb, rng, monkeypatch):
 
 
 # ------------------------------------------------- the one-pass 64k spectrum (fft_1p_kernel)
-@pytest.mark.parametrize("nz,skip,frames", [(65536, 0, 9), (40000, 123, 3), (65535, 7, 2)])
+@pytest.mark.parametrize("nz,skip,frames", [(65536, 0, 9), (40000, 123, 3), (65535, 7, 2), (65536, 0, 150),
+                                             (50000, 3, 70)])
 def test_spectrum_onepass_rows_and_zoom(nz, skip, frames, rng, monkeypatch):
     """The one-pass 64k transform (four 16k sub-transforms per frame on four CUs, radix-4 decimation in
-    frequency; SDRGPU_FFT_1P): every row meets the spectrum parity bar against the fp64 truth and
+    frequency; SDRGPU_FFT_1P; persistent workgroups walking several frames each at 70 / 150 frames,
+    a ragged last step): every row meets the spectrum parity bar against the fp64 truth and
     pocketfft on the same frame, zero-padded frames (nz < N) and reshaper strides included; the zoom
     rows (four partial maxima folded) equal fft_scaler's doZoom of the row bit for bit; and the rows
     agree with the two-pass kernels to the last bits near the peak."""
@@ -1016,13 +1018,17 @@ def test_spectrum_onepass_rows_and_zoom(nz, skip, frames, rng, monkeypatch):
     assert d.max() <= 0.05 and np.all(d[rows >= rows.max(axis=1, keepdims=True) - 60] <= 1e-3), d.max()
     w = oracle.create_window(6, nz)
     zr = z.cpu().numpy().reshape(frames, zw)
+    # every frame's zoom row; the fp64-truth bar on every frame of short calls and on the frames at the
+    # persistent grid's step boundaries (64 frames per step) of long ones
+    full = range(frames) if frames <= 16 else sorted({0, 1, 7, 8, 63, 64, 65, frames // 2, frames - 2, frames - 1})
     for j in range(frames):
+        np.testing.assert_array_equal(zr[j], oracle.zoom(rows[j], 0.0, 1.0, 1.0, zw))
+    for j in full:
         xs = x[j * stride:j * stride + nz]
         db_check(rows[j], oracle.fft_truth_power(xs, nz, N, w), N, ref32_fft_db(xs, nz, N, w))
-        np.testing.assert_array_equal(zr[j], oracle.zoom(rows[j], 0.0, 1.0, 1.0, zw))
 
 
-@pytest.mark.parametrize("frames_list,pre", [([13], 1000), ([3, 8], 0)])
+@pytest.mark.parametrize("frames_list,pre", [([13], 1000), ([3, 8], 0), ([130, 67], 77)])
 def test_spectrum_onepass_vfo(frames_list, pre, rng, monkeypatch):
     """The C5 group as ONE launch (SDRGPU_FFT_1P): each of a frame's four workgroups runs a quarter of
     the VFO's first stage, then its 16k sub-transform. Rows and zoom rows bit-identical to the one-pass
