@@ -430,6 +430,7 @@ __device__ __forceinline__ double2 zmul(double2 a, double2 b) {
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
+typedef unsigned bu2 __attribute__((ext_vector_type(2)));
 typedef unsigned bu4 __attribute__((ext_vector_type(4)));
 
 // tile -> (frame, block) of the 1M pass B: G8 adjacent row blocks on one XCD at once. Workgroups x,
@@ -910,7 +911,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         }
     }
     const int b = blockIdx.x, k = b >> 3;
-    const int f = 8 * (k >> 1) + (b & 7), p = k & 1;   // quarters p and p + 2 of frame f
+    const int f = 8 * (k >> 1) + (b & 7), p = k & 1, r0 = 2 * p;   // quarters r0, r0 + 1 of frame f
     if (f >= frames) return;
     T1P(0);
     if constexpr (VFO) vfo_half_block(v, f, p);   // the frame's first reader (HBM), half of its stage 1
@@ -925,12 +926,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
     {
         const int t = threadIdx.x;
         lds[TW512 + t] = tab[t];
-        if (t < 64) lds[W128 + t] = tab[512 + 32 * (p + 2 * (t >> 5)) + (t & 31)];   // W_128^(r i), r = p, p + 2
+        if (t < 64) lds[W128 + t] = tab[512 + 32 * (r0 + (t >> 5)) + (t & 31)];   // W_128^(r i), r = r0, r0 + 1
     }
-    // stage 1: y_p and y_{p+2} from the four quarters. With s = (-1)^p, A = u0 + s u2, q = u1 + s u3:
-    // y_p = A + W_4^p q, y_{p+2} = A - W_4^p q (W_4^(p+2) = -W_4^p; the same bits as A + W_4^(p+2) q)
-    const float s = p ? -1.0f : 1.0f;
-    const float fx = p ? 0.0f : 1.0f, fy = p ? -1.0f : 0.0f;
+    // stage 1: y_r for r = r0 (even) and r0 + 1 (odd) from the four quarters: y_r = A_r + W_4^r q_r with
+    // A_r = u0 + s_r u2, q_r = u1 + s_r u3, s_r = (-1)^r; W_4^r in {1, -i, -1, i} as (fx, fy), one of
+    // them 0, the other +-1 (exact products). The pair's bins 4 m + r0, 4 m + r0 + 1 are adjacent: the
+    // dB rows leave as 8-byte pairs.
+    const float fxa = p ? -1.0f : 1.0f, fyb = p ? 1.0f : -1.0f;   // W_4^r0 = (fxa, 0), W_4^(r0+1) = (0, fyb)
+    auto combine2 = [&](const float2 (&u)[4], float2& ya, float2& yb) {
+        const float2 aa = make_float2(fmaf(1.0f, u[2].x, u[0].x), fmaf(1.0f, u[2].y, u[0].y));
+        const float2 qa = make_float2(fmaf(1.0f, u[3].x, u[1].x), fmaf(1.0f, u[3].y, u[1].y));
+        const float2 ab = make_float2(fmaf(-1.0f, u[2].x, u[0].x), fmaf(-1.0f, u[2].y, u[0].y));
+        const float2 qb = make_float2(fmaf(-1.0f, u[3].x, u[1].x), fmaf(-1.0f, u[3].y, u[1].y));
+        ya = make_float2(aa.x + (fxa * qa.x - 0.0f * qa.y), aa.y + (fxa * qa.y + 0.0f * qa.x));
+        yb = make_float2(ab.x + (0.0f * qb.x - fyb * qb.y), ab.y + (0.0f * qb.y + fyb * qb.x));
+    };
     const unsigned lim = PAD ? (unsigned)nz : 65536u;     // (PAD: range-checked loads, 0 past nz)
     const __amdgpu_buffer_rsrc_t rw = brsrc(win, lim * 4u);
     const __amdgpu_buffer_rsrc_t rx = brsrc(in + (long long)f * frameStride, lim * 8u);
@@ -963,12 +973,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             float2 u[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) u[j] = make_float2(xv[bb & 1][ii][j].x * wv[bb & 1][ii][j], xv[bb & 1][ii][j].y * wv[bb & 1][ii][j]);
-            const float2 a = make_float2(fmaf(s, u[2].x, u[0].x), fmaf(s, u[2].y, u[0].y));
-            const float2 q = make_float2(fmaf(s, u[3].x, u[1].x), fmaf(s, u[3].y, u[1].y));
-            // W_4^p q with W_4^p in {1, -i}: one of fx, fy is 0, the other +-1 (exact products)
-            const float2 wq = make_float2(fx * q.x - fy * q.y, fx * q.y + fy * q.x);
-            za[PB * bb + ii] = make_float2(a.x + wq.x, a.y + wq.y);
-            zb[PB * bb + ii] = make_float2(a.x - wq.x, a.y - wq.y);
+            combine2(u, za[PB * bb + ii], zb[PB * bb + ii]);
         }
         if constexpr (bb + 2 < NB) issue(std::integral_constant<int, bb + 2>{});
         __builtin_amdgcn_sched_barrier(0);
@@ -1038,22 +1043,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
                 const float ww = *reinterpret_cast<const float*>(slot + 16384 + 2048 * j + 4 * t);
                 u[j] = make_float2(xx.x * ww, xx.y * ww);
             }
-            const float2 a = make_float2(fmaf(s, u[2].x, u[0].x), fmaf(s, u[2].y, u[0].y));
-            const float2 q = make_float2(fmaf(s, u[3].x, u[1].x), fmaf(s, u[3].y, u[1].y));
-            const float2 wq = make_float2(fx * q.x - fy * q.y, fx * q.y + fy * q.x);
-            za[i] = make_float2(a.x + wq.x, a.y + wq.y);
-            zb[i] = make_float2(a.x - wq.x, a.y - wq.y);
+            combine2(u, za[i], zb[i]);
             __builtin_amdgcn_sched_barrier(0);
         });
     }
     T1P(2);
     float* zf = ZM ? zpart + ((long long)f << 13) : nullptr;
     const __amdgpu_buffer_rsrc_t ro = brsrc(out + ((long long)f << 16), 65536u * 4u);
-    // the 16k transform of quarter r = p + 2 h from its stage-1 registers z
+    // the 16k transform of quarter r = r0 + h from its stage-1 registers z. Quarter r0's dB values wait in
+    // registers (dA) for quarter r0 + 1's, and the two leave as one 8-byte store per bin pair.
+    float dA[2][16];
     auto transform = [&](auto hc, float2 (&z)[32]) {
         constexpr int h = decltype(hc)::value;
-        const int r = p + 2 * h;
-        __syncthreads();   // (h = 0: the tables staged; h = 1: quarter p's stage-3 reads of the image are done)
+        const int r = r0 + h;
+        __syncthreads();   // (h = 0: the tables staged; h = 1: quarter r0's stage-3 reads of the image are done)
         {   // stage-1 finish: W_128^(r i), radix 32, W_N^(t (4 k2 + r)), into the LDS image
             const int t = tid();
 #pragma unroll
@@ -1085,8 +1088,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             for (int q1 = 0; q1 < 32; q1++) dst[17 * q1] = a[q1];
         }
         __syncthreads();
-        // stage 3: (k2, q1) = (e & 31, e >> 5), e = t, t + 512; dB rows through a buffer resource (the
-        // bin offset 4 (k2 + 32 q1) + r per lane, the q2 step in soffset)
+        // stage 3: (k2, q1) = (e & 31, e >> 5), e = t, t + 512. The thread holds the same (k2, q1) bins
+        // of both quarters, so quarter r0 + 1 stores (dA, dB) at float 4 (k2 + 32 q1 + 1024 q2) + r0
+        // (8-byte aligned: r0 even) through a buffer resource, the q2 step in soffset
         static_for<0, 2>([&](auto ec) {
             constexpr int e = decltype(ec)::value;
             const int t = tid();
@@ -1096,23 +1100,31 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
 #pragma unroll
             for (int t0 = 0; t0 < 16; t0++) c3[t0] = src[t0 ^ sw];
             dft16(c3);
-            float dv[16];
-            const unsigned vo = (unsigned)(4 * (k2 + 32 * q1) + r) * 4u;
+            if constexpr (h == 0) {
 #pragma unroll
-            for (int q2 = 0; q2 < 16; q2++) {
-                dv[q2] = db_of(c3[q2]);
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dv[q2]), ro, vo, q2 * 4096 * 4, 0);   // float 4 (k2 + 32 q1 + 1024 q2) + r
-            }
-            if constexpr (ZM) {   // max over the 8 lanes k2 & 7 (zoom column (k2 >> 3) + 4 q1 + 128 q2)
-                const int lane = t & 63;
-                tr_step<1, 8>(dv, lane);
-                tr_step<2, 4>(dv, lane);
-                tr_step<4, 2>(dv, lane);
-                // lane bits (b0 b1 b2) now select q2 = 8 b0 + 4 b1 + 2 b2 + i in dv[i], i < 2
-                const int q2 = ((lane & 1) << 3) | ((lane & 2) << 1) | (lane & 4) >> 1;
-                float* zp = zf + ((long long)r << 11) + (k2 >> 3) + 4 * q1 + 128 * q2;
-                zp[0] = dv[0];
-                zp[128] = dv[1];
+                for (int q2 = 0; q2 < 16; q2++) dA[e][q2] = db_of(c3[q2]);
+            } else {
+                float dv[16];
+                const unsigned vo = (unsigned)(4 * (k2 + 32 * q1) + r0) * 4u;
+#pragma unroll
+                for (int q2 = 0; q2 < 16; q2++) {
+                    dv[q2] = db_of(c3[q2]);
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(bu2, make_float2(dA[e][q2], dv[q2])), ro, vo,
+                                                          q2 * 4096 * 4, 0);
+                }
+                if constexpr (ZM) {   // max over both quarters and the 8 lanes k2 & 7: zoom column (k2 >> 3) + 4 q1 + 128 q2
+#pragma unroll
+                    for (int q2 = 0; q2 < 16; q2++) dv[q2] = fmaxf(dA[e][q2], dv[q2]);
+                    const int lane = t & 63;
+                    tr_step<1, 8>(dv, lane);
+                    tr_step<2, 4>(dv, lane);
+                    tr_step<4, 2>(dv, lane);
+                    // lane bits (b0 b1 b2) now select q2 = 8 b0 + 4 b1 + 2 b2 + i in dv[i], i < 2
+                    const int q2 = ((lane & 1) << 3) | ((lane & 2) << 1) | (lane & 4) >> 1;
+                    float* zp = zf + ((long long)p << 11) + (k2 >> 3) + 4 * q1 + 128 * q2;
+                    zp[0] = dv[0];
+                    zp[128] = dv[1];
+                }
             }
         });
     };
@@ -1128,13 +1140,13 @@ extern "C" int sdrgpu_debug_1p_times(unsigned long long* host, int n) {
 }
 #endif
 
-// zoom[f][o] = max over the four workgroups' partial maxima (fft_1p_kernel's ZM)
+// zoom[f][o] = max over the two workgroups' partial maxima (fft_1p_kernel's ZM)
 __global__ __launch_bounds__(256) void fft_1p_zoom_kernel(const float* __restrict__ zpart, int frames, float* __restrict__ zoom) {
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
     if (i >= (long long)frames * 2048) return;
     const long long f = i >> 11, o = i & 2047;
     const float* p = zpart + (f << 13) + o;
-    zoom[i] = fmaxf(fmaxf(p[0], p[2048]), fmaxf(p[4096], p[6144]));
+    zoom[i] = fmaxf(p[0], p[2048]);
 }
 
 // ---- the front end's per-block launch: pass A (frame straddling two pushes read in place) + the
