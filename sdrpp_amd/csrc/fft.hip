@@ -866,6 +866,12 @@ __device__ __forceinline__ void dft32(float2* v) {
 // 1.893 ms, r41pb).
 constexpr int k1pPB = 2;   // (PAD) sample rows per load batch: 4 PB loads of x and of w, two batches in flight
 constexpr int k1pSlots = 5;   // LDS-DMA ring slots (24 KiB row sets) in the image region
+#ifndef SDRGPU_1P_DMA
+#define SDRGPU_1P_DMA 1   // (A/B builds: 0 = whole frames through the register ring too)
+#endif
+#ifndef SDRGPU_1P_EARLY_DMA
+#define SDRGPU_1P_EARLY_DMA 0   // (A/B builds) the VFO half after the DMA ring's prologue
+#endif
 #ifdef SDRGPU_1P_TIMING   // (measurement builds) per-workgroup phase stamps of wave 0
 __device__ unsigned long long g_1p_t[16384 * 8];
 #define T1P(k)                                                                                    \
@@ -914,7 +920,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
     const int f = 8 * (k >> 1) + (b & 7), p = k & 1, r0 = 2 * p;   // quarters r0, r0 + 1 of frame f
     if (f >= frames) return;
     T1P(0);
-    if constexpr (VFO) vfo_half_block(v, f, p);   // the frame's first reader (HBM), half of its stage 1
+    // the frame's first reader (HBM), half of its stage 1 (EARLY: behind the DMA ring's prologue, which
+    // then fetches the first row sets while the VFO's loads wait)
+    constexpr bool EARLY = VFO && !PAD && SDRGPU_1P_DMA && SDRGPU_1P_EARLY_DMA;
+    if constexpr (VFO && !EARLY) vfo_half_block(v, f, p);
     T1P(1);
     // Index arithmetic is recomputed from a laundered thread index where it is used: left alone, the
     // compiler hoists the loop-invariant load / LDS / store addresses and spills them.
@@ -978,7 +987,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         if constexpr (bb + 2 < NB) issue(std::integral_constant<int, bb + 2>{});
         __builtin_amdgcn_sched_barrier(0);
     };
-    if constexpr (PAD) {   // zero-padded frames: range-checked register loads through the ring
+    if constexpr (PAD || !SDRGPU_1P_DMA) {   // zero-padded frames: range-checked register loads through the ring
         issue(std::integral_constant<int, 0>{});
         issue(std::integral_constant<int, 1>{});
         static_for<0, NB>(step);
@@ -1027,6 +1036,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             }
         };
         static_for<0, S - 1>(dma);
+        if constexpr (EARLY) vfo_half_block(v, f, p);
         static_for<0, 32>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             constexpr int younger = (S - 2 < 31 - i) ? S - 2 : 31 - i;   // row sets issued after i, in flight
