@@ -869,6 +869,9 @@ constexpr int k1pSlots = 5;   // LDS-DMA ring slots (24 KiB row sets) in the ima
 #ifndef SDRGPU_1P_DMA
 #define SDRGPU_1P_DMA 1   // (A/B builds: 0 = whole frames through the register ring too)
 #endif
+#ifndef SDRGPU_1P_VFO_UNROLL
+#define SDRGPU_1P_VFO_UNROLL 0   // (A/B builds) the VFO half's two segments unrolled
+#endif
 #ifndef SDRGPU_1P_EARLY_DMA
 #define SDRGPU_1P_EARLY_DMA 0   // (A/B builds) the VFO half after the DMA ring's prologue
 #endif
@@ -894,7 +897,11 @@ __device__ __forceinline__ void static_for(F&& fn) {
 // (the quarter pair of a workgroup: its VFO share, 32 segments of the frame's 64)
 __device__ __forceinline__ void vfo_half_block(const VfoWork& v, int g, int p) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#if SDRGPU_1P_VFO_UNROLL
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
     for (int k = 0; k < 2; k++) {
         const long long seg = (long long)(v.frame0 + g) * 64 + p * 32 + k * 16 + wave * 2 + (lane >> 5);
         fir_rows_segment<32, 5, true, false, 32, 32, true>(v.a, seg, lane);
@@ -943,12 +950,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
     // dB rows leave as 8-byte pairs.
     const float fxa = p ? -1.0f : 1.0f, fyb = p ? 1.0f : -1.0f;   // W_4^r0 = (fxa, 0), W_4^(r0+1) = (0, fyb)
     auto combine2 = [&](const float2 (&u)[4], float2& ya, float2& yb) {
-        const float2 aa = make_float2(fmaf(1.0f, u[2].x, u[0].x), fmaf(1.0f, u[2].y, u[0].y));
-        const float2 qa = make_float2(fmaf(1.0f, u[3].x, u[1].x), fmaf(1.0f, u[3].y, u[1].y));
-        const float2 ab = make_float2(fmaf(-1.0f, u[2].x, u[0].x), fmaf(-1.0f, u[2].y, u[0].y));
-        const float2 qb = make_float2(fmaf(-1.0f, u[3].x, u[1].x), fmaf(-1.0f, u[3].y, u[1].y));
-        ya = make_float2(aa.x + (fxa * qa.x - 0.0f * qa.y), aa.y + (fxa * qa.y + 0.0f * qa.x));
-        yb = make_float2(ab.x + (0.0f * qb.x - fyb * qb.y), ab.y + (0.0f * qb.y + fyb * qb.x));
+        const float2 aa = cadd(u[0], u[2]), qa = cadd(u[1], u[3]), ab = csub(u[0], u[2]), qb = csub(u[1], u[3]);
+        ya = make_float2(fmaf(fxa, qa.x, aa.x), fmaf(fxa, qa.y, aa.y));     // aa + W_4^r0 qa (exact products)
+        yb = make_float2(fmaf(-fyb, qb.y, ab.x), fmaf(fyb, qb.x, ab.y));    // ab + W_4^(r0+1) qb
     };
     const unsigned lim = PAD ? (unsigned)nz : 65536u;     // (PAD: range-checked loads, 0 past nz)
     const __amdgpu_buffer_rsrc_t rw = brsrc(win, lim * 4u);
@@ -1023,12 +1027,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         // LDS-DMA in inline asm: the compiler neither counts it (the waits below are explicit) nor
         // drains it with a vmcnt(0) before every LDS read it cannot prove disjoint (it did with the
         // builtin: no row set stayed in flight); M0 set and restored in the same statement
+        // (the row pointers advance by one row step per row set, laundered: left alone, the compiler
+        // precomputes all 96 pointers and spills them to VGPR lanes)
         auto dma = [&](auto ic) {
             constexpr int i = decltype(ic)::value;
             const unsigned lane16 = (unsigned)(tid() & 63) * 16u;
 #pragma unroll
             for (int e = 0; e < 3; e++) {
-                const char* src = gb[e] + (size_t)i * rstep[e] + lane16;
+                const char* src = gb[e] + lane16;
+                gb[e] += rstep[e];
+                asm volatile("" : "+s"(gb[e]));
                 const unsigned dst = __builtin_amdgcn_readfirstlane(ldsBase + (unsigned)((i % S) * SLOT) + loff[e]);
                 unsigned keep;
                 asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -1072,13 +1080,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
 #pragma unroll
             for (int i = 1; i < 32; i++) z[i] = cmul(z[i], lds[W128 + 32 * h + i]);   // W_128^(r i) = W_N^(512 r i)
             dft32(z);
-            double2 c = tab64[t * r];
-            const double2 st = tab64[4 * t];   // W_N^(t r) (W_N^(4 t))^k2
+            // W_N^(t r) (W_N^(4 t))^k2 as two independent fp64 chains over even / odd k2 (a serial chain of
+            // 31 fp64 complex products was the stage's critical path)
+            const double2 st = tab64[4 * t];
+            double2 ce = tab64[t * r], co = zmul(ce, st);
+            const double2 st2 = zmul(st, st);
             float2* row = lds + pad16(t);
 #pragma unroll
-            for (int k2 = 0; k2 < 32; k2++) {
-                row[k2 * RS] = cmul(z[k2], make_float2((float)c.x, (float)c.y));
-                if (k2 < 31) c = zmul(c, st);
+            for (int k2 = 0; k2 < 32; k2 += 2) {
+                row[k2 * RS] = cmul(z[k2], make_float2((float)ce.x, (float)ce.y));
+                row[(k2 + 1) * RS] = cmul(z[k2 + 1], make_float2((float)co.x, (float)co.y));
+                if (k2 < 30) {
+                    ce = zmul(ce, st2);
+                    co = zmul(co, st2);
+                }
             }
         }
         __syncthreads();
@@ -1150,13 +1165,20 @@ extern "C" int sdrgpu_debug_1p_times(unsigned long long* host, int n) {
 }
 #endif
 
-// zoom[f][o] = max over the two workgroups' partial maxima (fft_1p_kernel's ZM)
+// zoom[f][o] = max over the two workgroups' partial maxima (fft_1p_kernel's ZM): 4 columns per thread
+// as 16-B loads / stores (one element per thread took 20.8 us per 2^28-sample step)
 __global__ __launch_bounds__(256) void fft_1p_zoom_kernel(const float* __restrict__ zpart, int frames, float* __restrict__ zoom) {
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
     if (i >= (long long)frames * 2048) return;
     const long long f = i >> 11, o = i & 2047;
-    const float* p = zpart + (f << 13) + o;
-    zoom[i] = fmaxf(p[0], p[2048]);
+    const float4 a = *reinterpret_cast<const float4*>(zpart + (f << 13) + o);
+    const float4 b = *reinterpret_cast<const float4*>(zpart + (f << 13) + 2048 + o);
+    const float4 m = make_float4(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w));
+    if (((uintptr_t)zoom & 15) == 0) {   // (wave-uniform)
+        *reinterpret_cast<float4*>(zoom + i) = m;
+    } else {
+        zoom[i] = m.x; zoom[i + 1] = m.y; zoom[i + 2] = m.z; zoom[i + 3] = m.w;
+    }
 }
 
 // ---- the front end's per-block launch: pass A (frame straddling two pushes read in place) + the
@@ -1609,7 +1631,7 @@ static int launch_1p(FftPlan& p, const float2* in, long long stride, int frames,
                        p.tab1p.as<float2>(), p.tab1p64.as<double2>(), out, ZM ? p.zpart.as<float>() : nullptr, v);
     SDRGPU_HIP(hipGetLastError());
     if (ZM) {
-        const long long n = (long long)frames * 2048;
+        const long long n = (long long)frames * 2048 / 4;
         hipLaunchKernelGGL(fft_1p_zoom_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p.zpart.as<float>(),
                            frames, zoom);
         SDRGPU_HIP(hipGetLastError());

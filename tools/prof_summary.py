@@ -19,8 +19,9 @@ import sys
 
 PEAK = 8000.0
 GROUPS = {
-    "c5": r"fft_vfo_kernel<true|fft_passA_kernel<256, 32>|fft_merged_kernel<256, 32, 256, 32|fft_passB_kernel<256, 32, true>",
-    "c2": r"fft_passA_1m_kernel<16, 2, 128|fft_passB_1m_kernel<8, 0, 192",
+    "c5": r"fft_vfo_kernel<true|fft_passA_kernel<256, 32>|fft_merged_kernel<256, 32, 256, 32|fft_passB_kernel<256, 32, true>"
+          r"|fft_1p_kernel<true, true|fft_1p_zoom_kernel",
+    "c2": r"fft_passA_1m_kernel|fft_passB_1m_kernel",
     "c3": r"fir_mfma_kernel<4, true, true",
     "c4": r"chan2_kernel<1024, false>",
     "c4g": r"chan2_kernel<1024, true>",
