@@ -81,14 +81,13 @@ class C5:
             # the group: 8 B in (read once), 4 B dB + 4/32 B zoom rows out, 8/32 B VFO stage-1 out
             self.kernel_bytes = (12.0 + 4 / 32 + 8 / 32) * self.B
             self.kernel_name = ("spectrum N=65536 + zoom to 2048 + RxVFO stage 1 (D=32, 143 taps, xlator): "
-                                "fft_vfo_kernel<zoom,0,3> x17 (each frame's 8 pass-A column tiles and 4 quarter-frame "
-                                "stage-1 workgroups on one XCD, all one load round, so the stage's read of the IQ is "
-                                "served by that XCD's L2; pass B of the previous chunk)")
+                                "fft_1p_kernel<zoom,vfo,false> (one pass: two workgroups per frame, each half the "
+                                "VFO stage-1 outputs, then two adjacent 16k radix-4 DIF sub-transforms in LDS; the "
+                                "rows stream in by LDS-DMA) + fft_1p_zoom_kernel (folds the two zoom partials)")
             self.fft.set_timing(True)   # the group's own HIP events (the VFO's later stages are outside it)
             self.roofline_note = ("the group includes the VFO's first stage (8 B/sample of input it shares with "
-                                  "the spectrum); round 3's group was the spectrum alone (1.371 ms) with the "
-                                  "stage as a separate 0.407-ms launch: on today's basis that work was 1.778 ms, "
-                                  "frac 0.233")
+                                  "the spectrum); round 4's two-pass group (fft_vfo_kernel, SDRGPU_FFT_1P=0) took "
+                                  "1.63 ms for the same work, round 3's spectrum + separate stage 1.778 ms")
         else:
             self.kernel_bytes = (12.0 + 4 / 32) * self.B            # spectrum: 8 B in, 4 B dB + 4/32 B zoom out
             self.kernel_name = ("spectrum N=65536 + zoom to 2048: fft_passA_kernel<256,32> (chunk 0) + "
@@ -133,8 +132,8 @@ class C2:
         self.spectra = torch.empty(self.frames * self.N, dtype=torch.float32, device="cuda")
         self.bytes_per_sample = 8 + 4 * self.N / self.NZ
         self.kernel_bytes = self.bytes_per_sample * self.B
-        self.kernel_name = ("spectrum N=2^20, nz=1e6: fft_passA_1m_kernel<16,2,128> (persistent, tile-major intermediate, non-temporal input loads) + "
-                            "fft_passB_1m_kernel<8,0,192> (persistent, XCD-grouped rows) per 16-frame chunk")
+        self.kernel_name = ("spectrum N=2^20, nz=1e6: fft_passA_1m_kernel (16 columns, two tiles per workgroup, "
+                            "tile-major intermediate) + fft_passB_1m_kernel (8 rows, XCD-grouped) per 8-frame chunk")
 
     def dominant(self, x, s):
         self.fft.execute_dev(x.data_ptr(), self.NZ, self.frames, self.spectra.data_ptr(), s)
@@ -339,7 +338,7 @@ def spectrum_f64_cost(dev, stream, reps=5):
 def traffic_per_sample(config):
     """HBM bytes per input sample of the dominant launch group, from the newest committed
     rocprofv3 PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/pmc_bytes_per_sample.py)."""
-    for rnd in ("r4", "r3", "r2", "r1"):
+    for rnd in ("r5", "r4", "r3", "r2", "r1"):
         path = os.path.join(ROOT, "profiles", rnd, f"{config}_pmc_traffic.json")
         try:
             d = json.load(open(path))

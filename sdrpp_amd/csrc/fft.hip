@@ -1518,6 +1518,9 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         // one box), so it is the default only for N1 >= 512
         p.sa2 = p.N1 >= 512 ? 16 : 0;
         if (const char* e = tuning_env("SDRGPU_FFT_VFO_FUSE")) p.vfoFuse = atoi(e);
+        // 64k: the one-pass transform (fft_1p_kernel) is the default since r5 (C5 group 1.45 vs 1.63 ms
+        // per 2^28 samples for the two-pass launches, A/B on one box); SDRGPU_FFT_1P=0 keeps the latter
+        p.onepass = fftSize == 65536;
         if (const char* e = tuning_env("SDRGPU_FFT_1P")) p.onepass = atoi(e);
         if (rc >= 0 && fftSize == 65536) {   // fft_1p_kernel's exact twiddles (op1::TAB)
             std::vector<float2> t(op1::TAB);
@@ -1622,7 +1625,9 @@ static bool zoom_fusable(const FftPlan& p, int zoomSize) {
 template <bool ZM, bool VFO>
 static int launch_1p(FftPlan& p, const float2* in, long long stride, int frames, float* out, float* zoom, VfoWork v,
                      hipStream_t s) {
-    const bool pad = p.nz < 65536;
+    // LDS-DMA rows need whole frames, an even frame stride and a 16-B aligned base (16-B pieces);
+    // anything else streams through the range-checked register ring
+    const bool pad = p.nz < 65536 || (stride & 1) || ((uintptr_t)in & 15);
     auto k = pad ? fft_1p_kernel<ZM, VFO, true> : fft_1p_kernel<ZM, VFO, false>;
     SDRGPU_CHECK(set_lds(k, op1::LDS_BYTES));
     if (ZM) SDRGPU_CHECK(p.zpart.ensure(sizeof(float) * 4 * 2048 * (size_t)frames));

@@ -620,6 +620,7 @@ def test_fft_merged_chunks_match_separate_launches(rng, monkeypatch):
         return out.cpu().numpy()
 
     monkeypatch.setenv("SDRGPU_TUNING", "1")
+    monkeypatch.setenv("SDRGPU_FFT_1P", "0")                # the two-pass 64k launches
     monkeypatch.setenv("SDRGPU_FFT_CHUNK_MB", "1")          # 2 frames per chunk -> 4 chunks, merged
     a = rows()
     monkeypatch.setenv("SDRGPU_FFT_CHUNK_MB", "64")
@@ -960,8 +961,16 @@ def _fused_vs_separate(frames_list, pre, rng, zoom=False):
     assert_close_c(ya, yo, 5e-5, "fused VFO vs oracle")
 
 
+def _two_pass(monkeypatch):
+    """The 64k plan's two-pass launches (fft_vfo_kernel group: the round-4 form, kept as the
+    SDRGPU_FFT_1P=0 alternative to the one-pass transform)."""
+    monkeypatch.setenv("SDRGPU_TUNING", "1")
+    monkeypatch.setenv("SDRGPU_FFT_1P", "0")
+
+
 @pytest.mark.parametrize("frames_list,pre", [([8], 0), ([3, 5], 1000), ([1, 2], 307200), ([257], 77)])
-def test_spectrum_vfo_fused(frames_list, pre, rng):
+def test_spectrum_vfo_fused(frames_list, pre, rng, monkeypatch):
+    _two_pass(monkeypatch)
     _fused_vs_separate(frames_list, pre, rng)
 
 
@@ -970,8 +979,8 @@ def test_spectrum_zoom_vfo_fused(frames_list, pre, chunk_mb, rng, monkeypatch):
     """The C5 launch group (rows + zoom rows + the VFO's first stage in one set of launches): 1 MB
     chunks (2 frames per chunk: first pass-A launch, merged launches, last pass-B launch with the
     history workgroup) and single-chunk calls."""
+    _two_pass(monkeypatch)
     if chunk_mb:
-        monkeypatch.setenv("SDRGPU_TUNING", "1")
         monkeypatch.setenv("SDRGPU_FFT_CHUNK_MB", str(chunk_mb))
     _fused_vs_separate(frames_list, pre, rng, zoom=True)
 
@@ -982,15 +991,15 @@ def test_spectrum_vfo_fused_xcd(frames_list, pre, chunk_mb, rng, monkeypatch):
     column tiles, after the pass-B tiles) at frame counts that are not multiples of 8 (padding
     workgroups of the last group of 8 frames) and 1 / 8 MB chunks (merged launches): rows, zoom rows
     and VFO output bit-identical to the separate launches."""
+    _two_pass(monkeypatch)
     if chunk_mb:
-        monkeypatch.setenv("SDRGPU_TUNING", "1")
         monkeypatch.setenv("SDRGPU_FFT_CHUNK_MB", str(chunk_mb))
     _fused_vs_separate(frames_list, pre, rng, zoom=True)
 
 
 # ------------------------------------------------- the one-pass 64k spectrum (fft_1p_kernel)
 @pytest.mark.parametrize("nz,skip,frames", [(65536, 0, 9), (40000, 123, 3), (65535, 7, 2), (65536, 0, 150),
-                                             (50000, 3, 70)])
+                                             (50000, 3, 70), (65536, 1, 5)])
 def test_spectrum_onepass_rows_and_zoom(nz, skip, frames, rng, monkeypatch):
     """The one-pass 64k transform (four 16k sub-transforms per frame on four CUs, radix-4 decimation in
     frequency; SDRGPU_FFT_1P; persistent workgroups walking several frames each at 70 / 150 frames,
@@ -1030,8 +1039,8 @@ def test_spectrum_onepass_rows_and_zoom(nz, skip, frames, rng, monkeypatch):
 
 @pytest.mark.parametrize("frames_list,pre", [([13], 1000), ([3, 8], 0), ([130, 67], 77)])
 def test_spectrum_onepass_vfo(frames_list, pre, rng, monkeypatch):
-    """The C5 group as ONE launch (SDRGPU_FFT_1P): each of a frame's four workgroups runs a quarter of
-    the VFO's first stage, then its 16k sub-transform. Rows and zoom rows bit-identical to the one-pass
+    """The C5 group as ONE launch (SDRGPU_FFT_1P): each of a frame's two workgroups runs half of the
+    VFO's first stage, then its two 16k sub-transforms. Rows and zoom rows bit-identical to the one-pass
     spectrum without the VFO, the VFO output bit-identical to RxVFO.process_dev and within the oracle
     bar (_fused_vs_separate)."""
     monkeypatch.setenv("SDRGPU_TUNING", "1")
@@ -1048,7 +1057,7 @@ def test_spectrum_zoom_rows(frames, chunk_mb, zsize, rng, monkeypatch):
     merged chunk launches), as a separate kernel for other widths."""
     import torch
     if chunk_mb:
-        monkeypatch.setenv("SDRGPU_TUNING", "1")
+        _two_pass(monkeypatch)
         monkeypatch.setenv("SDRGPU_FFT_CHUNK_MB", str(chunk_mb))   # 2 frames per chunk -> merged launches
     N = 65536
     x = iq(rng, N * frames)
