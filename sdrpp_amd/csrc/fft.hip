@@ -875,6 +875,13 @@ constexpr int k1pSlots = 5;   // LDS-DMA ring slots (24 KiB row sets) in the ima
 #ifndef SDRGPU_1P_EARLY_DMA
 #define SDRGPU_1P_EARLY_DMA 0   // (A/B builds) the VFO half after the DMA ring's prologue
 #endif
+#ifndef SDRGPU_1P_LATE
+#define SDRGPU_1P_LATE 0   // (A/B builds) the VFO half 1: after the row loop, 2: between the two transforms
+#endif
+#ifndef SDRGPU_1P_ABL
+#define SDRGPU_1P_ABL 0   // (ablation builds, wrong results, timing only) 1: no loads, 2: no transforms, 4: no VFO,
+                          // 8: fp32 stage-1 twiddles, 16: no dB / stores
+#endif
 #ifdef SDRGPU_1P_TIMING   // (measurement builds) per-workgroup phase stamps of wave 0
 __device__ unsigned long long g_1p_t[16384 * 8];
 #define T1P(k)                                                                                    \
@@ -930,7 +937,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
     // the frame's first reader (HBM), half of its stage 1 (EARLY: behind the DMA ring's prologue, which
     // then fetches the first row sets while the VFO's loads wait)
     constexpr bool EARLY = VFO && !PAD && SDRGPU_1P_DMA && SDRGPU_1P_EARLY_DMA;
-    if constexpr (VFO && !EARLY) vfo_half_block(v, f, p);
+    if constexpr (VFO && !EARLY && !(SDRGPU_1P_ABL & 4) && SDRGPU_1P_LATE == 0) vfo_half_block(v, f, p);
     T1P(1);
     // Index arithmetic is recomputed from a laundered thread index where it is used: left alone, the
     // compiler hoists the loop-invariant load / LDS / store addresses and spills them.
@@ -991,7 +998,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         if constexpr (bb + 2 < NB) issue(std::integral_constant<int, bb + 2>{});
         __builtin_amdgcn_sched_barrier(0);
     };
-    if constexpr (PAD || !SDRGPU_1P_DMA) {   // zero-padded frames: range-checked register loads through the ring
+    if constexpr (SDRGPU_1P_ABL & 1) {
+#pragma unroll
+        for (int i = 0; i < 32; i++) {
+            za[i] = make_float2((float)(tid() + i), (float)i);
+            zb[i] = make_float2((float)i, (float)(tid() - i));
+        }
+    } else if constexpr (PAD || !SDRGPU_1P_DMA) {   // zero-padded frames: range-checked register loads through the ring
         issue(std::integral_constant<int, 0>{});
         issue(std::integral_constant<int, 1>{});
         static_for<0, NB>(step);
@@ -1066,6 +1079,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         });
     }
     T1P(2);
+    if constexpr (VFO && SDRGPU_1P_LATE == 1) vfo_half_block(v, f, p);
     float* zf = ZM ? zpart + ((long long)f << 13) : nullptr;
     const __amdgpu_buffer_rsrc_t ro = brsrc(out + ((long long)f << 16), 65536u * 4u);
     // the 16k transform of quarter r = r0 + h from its stage-1 registers z. Quarter r0's dB values wait in
@@ -1086,6 +1100,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             double2 ce = tab64[t * r], co = zmul(ce, st);
             const double2 st2 = zmul(st, st);
             float2* row = lds + pad16(t);
+            if constexpr (SDRGPU_1P_ABL & 8) {
+                const float2 cf = make_float2((float)ce.x, (float)ce.y), sf = make_float2((float)st.x, (float)st.y);
+#pragma unroll
+                for (int k2 = 0; k2 < 32; k2++) row[k2 * RS] = cmul(z[k2], k2 & 1 ? sf : cf);
+            } else
 #pragma unroll
             for (int k2 = 0; k2 < 32; k2 += 2) {
                 row[k2 * RS] = cmul(z[k2], make_float2((float)ce.x, (float)ce.y));
@@ -1125,7 +1144,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
 #pragma unroll
             for (int t0 = 0; t0 < 16; t0++) c3[t0] = src[t0 ^ sw];
             dft16(c3);
-            if constexpr (h == 0) {
+            if constexpr (SDRGPU_1P_ABL & 16) {
+                if constexpr (h == 1) {
+                    float acc = 0.0f;
+#pragma unroll
+                    for (int q2 = 0; q2 < 16; q2++) acc += c3[q2].x + c3[q2].y;
+                    out[(f << 16) + pe] = acc;
+                }
+            } else if constexpr (h == 0) {
 #pragma unroll
                 for (int q2 = 0; q2 < 16; q2++) dA[e][q2] = db_of(c3[q2]);
             } else {
@@ -1153,7 +1179,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             }
         });
     };
+    if constexpr (SDRGPU_1P_ABL & 2) {
+        float2 acc = make_float2(0.0f, 0.0f);
+#pragma unroll
+        for (int i = 0; i < 32; i++) acc = cadd(acc, cadd(za[i], zb[i]));
+        out[(f << 16) + tid()] = acc.x + acc.y;
+        return;
+    }
     transform(std::integral_constant<int, 0>{}, za);
+    if constexpr (VFO && SDRGPU_1P_LATE == 2) vfo_half_block(v, f, p);
     T1P(3);
     transform(std::integral_constant<int, 1>{}, zb);
     T1P(4);
@@ -1779,6 +1813,12 @@ int sdrgpu::fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const f
     if (n < 0) return n;
     *vfoN = n;
     return frames;
+}
+
+int sdrgpu::fft_set_onepass(sdrgpu_fft* h, int onepass) {
+    if (!h) return SDRGPU_EARG;
+    h->p.onepass = onepass;
+    return SDRGPU_OK;
 }
 
 int sdrgpu::fft_execute_owned(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, hipStream_t s) {

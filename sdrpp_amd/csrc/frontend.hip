@@ -103,6 +103,7 @@ static int fe_update_fft(sdrgpu_frontend* f) {
     if (f->fft) sdrgpu_fft_destroy(f->fft);
     f->fft = nullptr;
     SDRGPU_CHECK(sdrgpu_fft_create(&f->fft, f->device, f->fftSize, nz, f->window));
+    SDRGPU_CHECK(fft_set_onepass(f->fft, 0));   // per-block calls: the two-pass launches (sdrgpu_internal.h)
     f->nz = nz;
     f->skip = skip;
     // the reshaper restarts on a path update: the next frame starts at the next sample

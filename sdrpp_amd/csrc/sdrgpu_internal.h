@@ -147,6 +147,11 @@ namespace sdrgpu {
 // entry points without the cross-stream ordering, for a handle owned by another handle
 int block_run_owned(sdrgpu_block* h, const void* in, int count, void* out, hipStream_t s);
 int fft_execute_owned(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, hipStream_t s);
+// The 64k plan's transform: 1 = the one-pass kernel (the batch default), 0 = the two-pass launches
+// (the front end's: its per-block calls hold a few frames, where two short launches of 8 workgroups
+// per frame finish sooner than one launch of 2 long ones, and its split path reads the straddling
+// frame in place). Returns SDRGPU_EARG for a null handle.
+int fft_set_onepass(sdrgpu_fft* h, int onepass);
 // Up to two device copies of complex samples done by spare workgroups of another launch.
 struct SideCopy {
     float2* dst[2];

@@ -182,3 +182,20 @@ def ref32_fft_db(x, nz, N, window):
 def iq(rng, n, scale=1.0):
     """SpeedTester-style uniform [-1,1) complex IQ (core/src/dsp/bench/speed_tester.h:37-41)."""
     return (rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)).astype(np.complex64) * np.float32(scale)
+
+
+def two_pass_fft(N, nz, window=6):
+    """An FFTSpectrum on the two-pass launches of the 64k plan: the front end's transform (its plans are
+    two-pass, sdrgpu_internal.h fft_set_onepass), which its rows are checked against bit for bit."""
+    from sdrpp_amd import dsp
+    keys = ("SDRGPU_TUNING", "SDRGPU_FFT_1P")
+    old = {k: os.environ.get(k) for k in keys}
+    os.environ.update(SDRGPU_TUNING="1", SDRGPU_FFT_1P="0")
+    try:
+        return dsp.FFTSpectrum(N, nz, window)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v

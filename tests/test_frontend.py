@@ -3,8 +3,8 @@ one by one and vs the oracle.
 
 - Framing follows the Reshaper (keep nz, skip; genReshapeParams): the rows a stream of
   ragged pushes produces are BIT-IDENTICAL to one spectrum batch over the whole stream with
-  frame stride nz + skip (same kernels, same frame data, including frames stitched across
-  two pushes).
+  frame stride nz + skip (same kernels: the front end's plans run the 64k transform as the two-pass
+  launches, _util.two_pass_fft; same frame data, including frames stitched across two pushes).
 - VFO outputs equal a standalone RxVFO fed the same blocks, bit for bit.
 - C1: file_source-style 2.4 MS/s blocks of fs/200 samples, 64k BH7, fftRate 15
   -> nz 65,536, skip 94,464; every row vs the fp64 truth (tests/_util.py db_check).
@@ -16,7 +16,7 @@ import pytest
 import oracle
 import sdrpp_amd
 from sdrpp_amd import dsp
-from _util import db_check, iq, ref32_fft_db
+from _util import db_check, iq, ref32_fft_db, two_pass_fft
 
 pytestmark = pytest.mark.gpu
 
@@ -57,7 +57,7 @@ def test_c1_framing_and_truth():
     nframes = (len(x) - nz) // stride + 1
     assert rows.shape == (nframes, N)
     # bit-identical to one batch with the reshaper's stride
-    sp = dsp.FFTSpectrum(N, nz, 6)
+    sp = two_pass_fft(N, nz)
     w = oracle.create_window(6, nz)
     for j in (0, 1, nframes // 2, nframes - 1):
         frame = x[j * stride:j * stride + nz]
@@ -76,7 +76,7 @@ def test_ragged_pushes_bit_identical(sizes, rng):
     stride = nz + skip
     n = (len(x) - nz) // stride + 1
     assert rows.shape[0] == n
-    sp = dsp.FFTSpectrum(N, nz, 6)
+    sp = two_pass_fft(N, nz)
     for j in range(n):
         assert np.array_equal(rows[j], sp.logmag(x[j * stride:j * stride + nz])), f"frame {j}"
 
@@ -90,7 +90,7 @@ def test_zero_pad_framing(rng):
     x = iq(rng, 205000)
     rows = np.concatenate([fe.push(b) for b in pushes(x, [30011])])
     assert rows.shape[0] == len(x) // nz
-    sp = dsp.FFTSpectrum(N, nz, 6)
+    sp = two_pass_fft(N, nz)
     for j in range(rows.shape[0]):
         assert np.array_equal(rows[j], sp.logmag(x[j * nz:(j + 1) * nz]))
 

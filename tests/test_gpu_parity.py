@@ -776,13 +776,19 @@ def test_spectrum_ulp_distribution(kind, N, nz, rng):
         assert sg["frac_le_1ulp"] >= sr["frac_le_1ulp"] - 0.03, (sg, sr)
     assert sg["p99"] <= 2 * sr["p99"] + 1, (sg, sr)
     # absolute bars (the literal north_star metric, stated rather than only relative): at least 97%
-    # of the bins within 1 ulp on a full random frame (measured 98.3% at 64k, 99.2% at 1M; 91% on
-    # the 22-bin AES17 table, 94-100% on the tonal frames), p50 0 ulp (1 on those few-bin frames), and the worst bin no more
-    # than 2x pocketfft's worst (or 16 ulp): measured max 11 / 20 / 84 ulp vs pocketfft 11 / 24 / 72
-    # at 4k / 64k / 1M (profiles/r3/spectrum_ulp_r3a.jsonl)
+    # of the bins within 1 ulp on a full random frame (measured 98.2% at 64k, 99.2% at 1M), p50 0 ulp
+    # (1 on the few-bin frames), and the worst bin no more than 2x pocketfft's worst (or 16 ulp):
+    # measured max 6 / 41 / 38 ulp vs pocketfft 10 / 28 / 77 at 4k / 64k / 1M (r5h). The tonal frames
+    # and the AES17 table have 17-22 bins within 60 dB of the peak, too few for a percentage (pocketfft
+    # itself has 18 of 22 AES17 bins within 1 ulp, 82%): there at most 2 more bins than pocketfft's
+    # beyond 1 ulp, and a worst bin within pocketfft's + 1 ulp
     assert sg["p50"] <= (0 if sg["bins"] >= 1000 else 1), sg
-    assert sg["frac_le_1ulp"] >= (0.97 if sg["bins"] >= 1000 else 0.85), sg
-    assert sg["max"] <= max(2 * sr["max"], 16), (sg, sr)
+    if sg["bins"] >= 1000:
+        assert sg["frac_le_1ulp"] >= 0.97, sg
+        assert sg["max"] <= max(2 * sr["max"], 16), (sg, sr)
+    else:
+        assert np.sum(e_gpu > 1.0) <= np.sum(e_ref > 1.0) + 2, (sg, sr)
+        assert sg["max"] <= sr["max"] + 1, (sg, sr)
 
 
 def test_spectrum_ulp_corpus():
@@ -859,7 +865,11 @@ def test_spectrum_f64_within_1ulp(kind, N, nz, rng):
     f.set_precision("f32")   # back to the fp32 kernels: same plan, FFTW-class bar
     assert f.precision == "f32"
     e32 = db_ulp_errors(f.logmag(x), truth)
-    assert np.mean(e32 <= 1.0) >= (0.97 if e32.size >= 1000 else 0.85)
+    if e32.size >= 1000:
+        assert np.mean(e32 <= 1.0) >= 0.97
+    else:   # (few bins: against pocketfft's count, as test_spectrum_ulp_distribution)
+        e_ref = db_ulp_errors(ref32_fft_db(x, nz, N, oracle.create_window(6, nz)), truth)
+        assert np.sum(e32 > 1.0) <= np.sum(e_ref > 1.0) + 2
 
 
 @pytest.mark.parametrize("N,nz,stride,frames", [(65536, 65536, 65536, 300), (65536, 50000, 61000, 9),
