@@ -836,6 +836,14 @@ constexpr int LDS_BYTES = (W128 + 64) * 8;
 constexpr int TAB = 512 + 128;          // device table: [q1][t0] W_512^(t0 q1), [r][i] W_128^(r i)
 }
 
+// x w, rounded on its own: never contracted into the radix-4 adds that follow (left to the compiler,
+// whether it fused x w + u into one fma differed between kernel instantiations, so the one-pass rows
+// with and without the fused VFO differed in the last bit)
+__device__ __forceinline__ float2 wmul(float2 x, float w) {
+#pragma clang fp contract(off)
+    return make_float2(x.x * w, x.y * w);
+}
+
 // 32-point DFT as 2 x 16 (even / odd halves), natural order in and out
 __device__ __forceinline__ void dft32(float2* v) {
     constexpr float C[16] = {1.0f, 0.98078528040323044913f, 0.92387953251128675613f, 0.83146961230254523708f,
@@ -864,20 +872,8 @@ __device__ __forceinline__ void dft32(float2* v) {
 // Stage-1 twiddles W_N^(t (4 k2 + r)) by an fp64 recurrence W_N^(t r) (W_N^(4 t))^k2 from two values of
 // an fp64 table, rounded once (against one exact table value each, 128 KB per item from L2: 1.942 ->
 // 1.893 ms, r41pb).
-constexpr int k1pPB = 2;   // (PAD) sample rows per load batch: 4 PB loads of x and of w, two batches in flight
 constexpr int k1pSlots = 5;   // LDS-DMA ring slots (24 KiB row sets) in the image region
-#ifndef SDRGPU_1P_DMA
-#define SDRGPU_1P_DMA 1   // (A/B builds: 0 = whole frames through the register ring too)
-#endif
-#ifndef SDRGPU_1P_VFO_UNROLL
-#define SDRGPU_1P_VFO_UNROLL 0   // (A/B builds) the VFO half's two segments unrolled
-#endif
-#ifndef SDRGPU_1P_EARLY_DMA
-#define SDRGPU_1P_EARLY_DMA 0   // (A/B builds) the VFO half after the DMA ring's prologue
-#endif
-#ifndef SDRGPU_1P_LATE
-#define SDRGPU_1P_LATE 0   // (A/B builds) the VFO half 1: after the row loop, 2: between the two transforms
-#endif
+constexpr int k1pPB = 2;   // (PAD) sample rows per load batch: 4 PB loads of x and of w, two batches in flight
 #ifndef SDRGPU_1P_ABL
 #define SDRGPU_1P_ABL 0   // (ablation builds, wrong results, timing only) 1: no loads, 2: no transforms, 4: no VFO,
                           // 8: fp32 stage-1 twiddles, 16: no dB / stores
@@ -904,11 +900,7 @@ __device__ __forceinline__ void static_for(F&& fn) {
 // (the quarter pair of a workgroup: its VFO share, 32 segments of the frame's 64)
 __device__ __forceinline__ void vfo_half_block(const VfoWork& v, int g, int p) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#if SDRGPU_1P_VFO_UNROLL
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
     for (int k = 0; k < 2; k++) {
         const long long seg = (long long)(v.frame0 + g) * 64 + p * 32 + k * 16 + wave * 2 + (lane >> 5);
         fir_rows_segment<32, 5, true, false, 32, 32, true>(v.a, seg, lane);
@@ -934,10 +926,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
     const int f = 8 * (k >> 1) + (b & 7), p = k & 1, r0 = 2 * p;   // quarters r0, r0 + 1 of frame f
     if (f >= frames) return;
     T1P(0);
-    // the frame's first reader (HBM), half of its stage 1 (EARLY: behind the DMA ring's prologue, which
-    // then fetches the first row sets while the VFO's loads wait)
-    constexpr bool EARLY = VFO && !PAD && SDRGPU_1P_DMA && SDRGPU_1P_EARLY_DMA;
-    if constexpr (VFO && !EARLY && !(SDRGPU_1P_ABL & 4) && SDRGPU_1P_LATE == 0) vfo_half_block(v, f, p);
+    // the frame's first reader (HBM): half of the VFO's stage 1. (Measured and rejected, r5: the VFO
+    // inside the row loop -- from the LDS ring, 1.91 ms; as two batches of segments right after the
+    // ring fetched their lines, 1.60 ms; after the loop / between the transforms, spilled)
+    if constexpr (VFO && !(SDRGPU_1P_ABL & 4)) vfo_half_block(v, f, p);
     T1P(1);
     // Index arithmetic is recomputed from a laundered thread index where it is used: left alone, the
     // compiler hoists the loop-invariant load / LDS / store addresses and spills them.
@@ -992,7 +984,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         for (int ii = 0; ii < PB; ii++) {
             float2 u[4];
 #pragma unroll
-            for (int j = 0; j < 4; j++) u[j] = make_float2(xv[bb & 1][ii][j].x * wv[bb & 1][ii][j], xv[bb & 1][ii][j].y * wv[bb & 1][ii][j]);
+            for (int j = 0; j < 4; j++) u[j] = wmul(xv[bb & 1][ii][j], wv[bb & 1][ii][j]);
             combine2(u, za[PB * bb + ii], zb[PB * bb + ii]);
         }
         if constexpr (bb + 2 < NB) issue(std::integral_constant<int, bb + 2>{});
@@ -1004,7 +996,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             za[i] = make_float2((float)(tid() + i), (float)i);
             zb[i] = make_float2((float)i, (float)(tid() - i));
         }
-    } else if constexpr (PAD || !SDRGPU_1P_DMA) {   // zero-padded frames: range-checked register loads through the ring
+    } else if constexpr (PAD) {   // zero-padded or unaligned frames: range-checked register loads through the ring
         issue(std::integral_constant<int, 0>{});
         issue(std::integral_constant<int, 1>{});
         static_for<0, NB>(step);
@@ -1057,7 +1049,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             }
         };
         static_for<0, S - 1>(dma);
-        if constexpr (EARLY) vfo_half_block(v, f, p);
         static_for<0, 32>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             constexpr int younger = (S - 2 < 31 - i) ? S - 2 : 31 - i;   // row sets issued after i, in flight
@@ -1072,14 +1063,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             for (int j = 0; j < 4; j++) {
                 const float2 xx = *reinterpret_cast<const float2*>(slot + 4096 * j + 8 * t);
                 const float ww = *reinterpret_cast<const float*>(slot + 16384 + 2048 * j + 4 * t);
-                u[j] = make_float2(xx.x * ww, xx.y * ww);
+                u[j] = wmul(xx, ww);
             }
             combine2(u, za[i], zb[i]);
             __builtin_amdgcn_sched_barrier(0);
         });
     }
     T1P(2);
-    if constexpr (VFO && SDRGPU_1P_LATE == 1) vfo_half_block(v, f, p);
     float* zf = ZM ? zpart + ((long long)f << 13) : nullptr;
     const __amdgpu_buffer_rsrc_t ro = brsrc(out + ((long long)f << 16), 65536u * 4u);
     // the 16k transform of quarter r = r0 + h from its stage-1 registers z. Quarter r0's dB values wait in
@@ -1187,7 +1177,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         return;
     }
     transform(std::integral_constant<int, 0>{}, za);
-    if constexpr (VFO && SDRGPU_1P_LATE == 2) vfo_half_block(v, f, p);
     T1P(3);
     transform(std::integral_constant<int, 1>{}, zb);
     T1P(4);
