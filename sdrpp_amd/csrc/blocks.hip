@@ -586,10 +586,95 @@ __global__ __launch_bounds__(WFM_TM) void wfm_short_kernel(
     out[m] = make_float2(acc, acc);
 }
 
-__global__ __launch_bounds__(TAIL_NT) void fir_tail_kernel(TailArgs t) {
+// BroadcastFM mono for big calls (C5: 1,048,576 samples at 240 kS/s per step): the same fused form
+// with 2,048 outputs per workgroup and 8 per thread. The quadrature values of the window go to LDS in
+// fir_tail's row layout (element e at row e mod 8, column e / 8: a thread's 8-output register window
+// reads consecutive columns, conflict-free), then each thread runs its 8 fmaf chains over the padded
+// taps in tap order (fir_kernel at D = 1): one LDS read per 8 FMAs and no quadrature round trip
+// through HBM (quad_kernel + fir_kernel<float, float, 4>: 5.3 + 15.6 us per C5 step, r5m).
+constexpr int WFM_BK = 8, WFM_BNT = 256, WFM_BCH = WFM_BK * WFM_BNT;
+__global__ __launch_bounds__(WFM_BNT) void wfm_big_kernel(
+    const float2* __restrict__ in, int count, const float2* __restrict__ din, float2* __restrict__ dinNext,
+    const float* __restrict__ hist, float* __restrict__ histNext, const float* __restrict__ taps, int Q, int H,
+    float invDev, float2* __restrict__ out) {
+    extern __shared__ float X[];
+    constexpr int K = WFM_BK;
+    const int tid = threadIdx.x;
+    auto qv = [&](long long b) -> float {   // [hist || quad(in)][b], zero past the end
+        if (b < H) return hist[b];
+        const long long i = b - H;
+        if (i >= count) return 0.0f;
+        return quad_value(in[i], i ? in[i - 1] : din[0], invDev);
+    };
+    if (blockIdx.x == gridDim.x - 1) {
+        for (int k = tid; k < H; k += WFM_BNT) histNext[k] = qv((long long)count + k);
+        if (tid == 0) dinNext[0] = in[count - 1];
+        return;
+    }
+    const long long m0 = (long long)blockIdx.x * WFM_BCH;
+    const int RSK = WFM_BNT + Q / K + 2;   // columns per row (Q is a multiple of 8, <= 256: host-checked)
+    float* T = X + K * RSK;                // the taps
+    for (int q = tid; q < Q; q += WFM_BNT) T[q] = taps[q];
+    // the window [m0, m0 + K RSK) of [hist || quad(in)]: interior workgroups issue all their sample
+    // loads at once (one memory round trip), the first and last take the element-wise path
+    constexpr int NF = (K * (WFM_BNT + 256 / K + 2) + WFM_BNT - 1) / WFM_BNT;
+    if (m0 >= H + 1 && m0 + K * RSK - H <= count) {
+        float2 y[NF], yp[NF];
+        const float2* src = in + (m0 - H);
+#pragma unroll
+        for (int k = 0; k < NF; k++) {
+            const int j = tid + k * WFM_BNT;
+            const int jj = j < K * RSK ? j : 0;
+            y[k] = src[jj];
+            yp[k] = src[jj - 1];
+        }
+#pragma unroll
+        for (int k = 0; k < NF; k++) {
+            const int j = tid + k * WFM_BNT;
+            if (j < K * RSK) X[(j & (K - 1)) * RSK + (j >> 3)] = quad_value(y[k], yp[k], invDev);
+        }
+    } else {
+        for (int j = tid; j < K * RSK; j += WFM_BNT) X[(j & (K - 1)) * RSK + (j >> 3)] = qv(m0 + j);
+    }
+    __syncthreads();
+    float acc[K], w[K];
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        acc[i] = 0.0f;
+        w[i] = X[i * RSK + tid];
+    }
+    for (int q0 = 0; q0 < Q; q0 += K) {
+        float hv[K], nx[K];
+#pragma unroll
+        for (int u = 0; u < K; u++) hv[u] = T[q0 + u];   // (LDS broadcasts)
+#pragma unroll
+        for (int u = 0; u < K; u++) nx[u] = X[u * RSK + tid + 1 + q0 / K];
+#pragma unroll
+        for (int u = 0; u < K; u++) {
+#pragma unroll
+            for (int i = 0; i < K; i++) acc[i] = fmaf(w[(i + u) % K], hv[u], acc[i]);
+            w[u] = nx[u];
+        }
+    }
+    const long long m = m0 + (long long)tid * K;
+    if (m + K <= count) {
+        float4* o = reinterpret_cast<float4*>(out + m);   // (out: 8-byte stereo frames; 16-B aligned pairs)
+        if (((uintptr_t)out & 15) == 0) {
+#pragma unroll
+            for (int i = 0; i < K; i += 2) o[i / 2] = make_float4(acc[i], acc[i], acc[i + 1], acc[i + 1]);
+            return;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < K; i++)
+        if (m + i < count) out[m + i] = make_float2(acc[i], acc[i]);
+}
+
+template <int K, int NT>
+__global__ __launch_bounds__(NT) void fir_tail_kernel(TailArgs t) {
     extern __shared__ __attribute__((aligned(16))) float2 XS[];
     __shared__ TailGeom gs[TAIL_MAXS];
-    fir_tail_block(t, blockIdx.x, blockIdx.x == gridDim.x - 1, XS, gs);
+    fir_tail_block<K, NT>(t, blockIdx.x, blockIdx.x == gridDim.x - 1, XS, gs);
 }
 
 // ------------------------------------------------ polyphase resampler
@@ -1295,11 +1380,13 @@ struct ChainBlock : Block {
             f[i] = dynamic_cast<FirBlock*>(kids[i + 1].get());
             if (!f[i] || f[i]->in_dtype != SDRGPU_C64 || f[i]->ttype != SDRGPU_F32 || f[i]->xl || f[i]->quad ||
                 f[i]->stereo || f[i]->offset > f[i]->ntaps - 1 || f[i]->Q % 8 != 0 || (f[i]->D & (f[i]->D - 1)) ||
-                f[i]->D > TAIL_NT / TAIL_K)
+                f[i]->D > TAIL_NT / 8)
                 return 0;
         }
         t = TailArgs{};
         t.S = S;
+        t.K = big ? TAIL_K_BIG : TAIL_K;
+        t.NT = big ? TAIL_NT_BIG : TAIL_NT;
         int n = n0;
         for (int i = 0; i < S; i++) {
             TailStage& st = t.st[i];
@@ -1336,7 +1423,7 @@ struct ChainBlock : Block {
                     maxEl = std::max(maxEl, tail_geometry(t, w, g));
                     nel0 = std::max(nel0, g[0].nel);
                 }
-                if (nel0 <= TAIL_PF * TAIL_NT) break;
+                if (nel0 <= TAIL_PF * t.NT) break;
                 if ((!big && t.G >= 64) || t.G >= std::max(n, 1) || t.G >= (1 << 20)) return 0;
             }
             if (big) {
@@ -1369,7 +1456,8 @@ struct ChainBlock : Block {
     int launch_tail(TailArgs& t, FirBlock** f, size_t lds, const void* s1, void* out, hipStream_t s) {
         t.in = reinterpret_cast<const float2*>(s1);
         t.out = reinterpret_cast<float2*>(out);
-        hipLaunchKernelGGL(fir_tail_kernel, dim3(t.G), dim3(TAIL_NT), lds, s, t);
+        if (t.K == TAIL_K_BIG && t.NT == TAIL_NT_BIG) hipLaunchKernelGGL((fir_tail_kernel<TAIL_K_BIG, TAIL_NT_BIG>), dim3(t.G), dim3(TAIL_NT_BIG), lds, s, t);
+        else hipLaunchKernelGGL((fir_tail_kernel<TAIL_K, TAIL_NT>), dim3(t.G), dim3(TAIL_NT), lds, s, t);
         SDRGPU_HIP(hipGetLastError());
         for (int i = 0; i < t.S; i++) {   // FirBlock::run's state update
             f[i]->cur ^= 1;
@@ -1784,15 +1872,28 @@ extern "C" int sdrgpu_fm_create(sdrgpu_block** h, int device, double samplerate,
     return wrap(h, c, rc);
 }
 
-// [quadrature, stereo FIR at D = 1] with wfm_short_kernel for calls up to kShortMax samples
+// [quadrature, stereo FIR at D = 1] in one launch: wfm_short_kernel for calls up to kShortMax
+// samples, wfm_big_kernel above
 struct WfmBlock : ChainBlock {
     static constexpr int kShortMax = 1 << 15;
     int run(const void* in, int count, void* out, hipStream_t s) override {
         if (kids.size() != 2) return ChainBlock::run(in, count, out, s);
         auto* qb = static_cast<QuadBlock*>(kids[0].get());
         auto* fb = static_cast<FirBlock*>(kids[1].get());
-        if (count <= 0 || count > kShortMax || fb->D != 1) return ChainBlock::run(in, count, out, s);
+        if (count <= 0 || fb->D != 1 || fb->Q % WFM_BK != 0 || fb->Q > 256) return ChainBlock::run(in, count, out, s);
         SDRGPU_SET_DEVICE(device);
+        if (count > kShortMax) {
+            const int blocks = (int)(((long long)count + WFM_BCH - 1) / WFM_BCH);
+            const size_t lds = sizeof(float) * ((size_t)WFM_BK * (WFM_BNT + fb->Q / WFM_BK + 2) + fb->Q);
+            hipLaunchKernelGGL(wfm_big_kernel, dim3(blocks + 1), dim3(WFM_BNT), lds, s, (const float2*)in, count,
+                               qb->din[qb->cur].as<float2>(), qb->din[qb->cur ^ 1].as<float2>(), fb->hist[fb->cur].as<float>(),
+                               fb->hist[fb->cur ^ 1].as<float>(), fb->taps.as<float>(), fb->Q, fb->ntaps - 1, qb->invDev,
+                               (float2*)out);
+            SDRGPU_HIP(hipGetLastError());
+            qb->cur ^= 1;
+            fb->cur ^= 1;
+            return count;
+        }
         const int blocks = (count + WFM_TM - 1) / WFM_TM;
         const size_t lds = sizeof(float) * (size_t)(WFM_TM + fb->Q);
         hipLaunchKernelGGL(wfm_short_kernel, dim3(blocks + 1), dim3(WFM_TM), lds, s, (const float2*)in, count,

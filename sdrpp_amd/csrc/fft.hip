@@ -887,16 +887,6 @@ __device__ unsigned long long g_1p_t[16384 * 8];
 #else
 #define T1P(k) do {} while (0)
 #endif
-// fn(integral_constant<int, I>) for I in [A, B): a compile-time loop (a long `#pragma unroll` loop can
-// stay rolled past the unroller's threshold, and a run-time ring index sends the ring to scratch)
-template <int A, class F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& fn, std::integer_sequence<int, I...>) {
-    (fn(std::integral_constant<int, A + I>{}), ...);
-}
-template <int A, int B, class F>
-__device__ __forceinline__ void static_for(F&& fn) {
-    static_for_impl<A>(fn, std::make_integer_sequence<int, B - A>{});
-}
 // (the quarter pair of a workgroup: its VFO share, 32 segments of the frame's 64)
 __device__ __forceinline__ void vfo_half_block(const VfoWork& v, int g, int p) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1253,7 +1243,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
         return;
     }
     const int w = blockIdx.x - ntiles;
-    fir_tail_block(t, w, w == t.G - 1, lds, gs);
+    fir_tail_block<TAIL_K, TAIL_NT>(t, w, w == t.G - 1, lds, gs);
 }
 
 // ---------------------------------------------------------------- host side
@@ -1784,8 +1774,9 @@ int sdrgpu::fft_execute_split(sdrgpu_fft* h, const float2* head, int nh, const f
     // pass B + the VFO's later stages (one tail launch's workgroups) where the chain has that form
     TailArgs t;
     size_t ldsTail = 0;
-    const int tail = vfo_tail_prepare(vfoBlock, *vfo, vfoOut, &t, &ldsTail);
+    int tail = vfo_tail_prepare(vfoBlock, *vfo, vfoOut, &t, &ldsTail);
     if (tail < 0) return tail;
+    if (tail && (t.NT != TAIL_NT || t.K != TAIL_K)) tail = 0;   // (a big call's workgroups: the later stages run after pass B)
     if (tail) {
         auto k = fft_passB_tail_kernel;
         const size_t lds = std::max(ldsFFT, ldsTail);

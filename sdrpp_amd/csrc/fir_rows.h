@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <type_traits>
+#include <utility>
 
 namespace sdrgpu {
 
@@ -16,6 +17,22 @@ __device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
     return make_float2(fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x));
 }
 
+// packed-fp32 pairs (v_pk_fma_f32 and friends: one instruction for both components, each the same IEEE
+// operation as its scalar form)
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v to_v(float2 a) { return f2v{a.x, a.y}; }
+__device__ __forceinline__ float2 to_f2(f2v a) { return make_float2(a.x, a.y); }
+
+// fn(integral_constant<int, I>) for I in [A, B): a compile-time loop (a long `#pragma unroll` loop can
+// stay rolled past the unroller's threshold, and a run-time ring index sends the ring to scratch)
+template <int A, class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& fn, std::integer_sequence<int, I...>) {
+    (fn(std::integral_constant<int, A + I>{}), ...);
+}
+template <int A, int B, class F>
+__device__ __forceinline__ void static_for(F&& fn) {
+    static_for_impl<A>(fn, std::make_integer_sequence<int, B - A>{});
+}
 // x * (ph0 * step): the xlator's per-slot product, each complex result pinned to plain VGPRs.
 // Left to itself the SLP vectoriser packs a run of these into v_pk_fma pairs that compute both
 // signs of every term (twice the live registers per slot: the PF-slot kernels spilled on it).

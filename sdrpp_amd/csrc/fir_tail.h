@@ -18,12 +18,22 @@ namespace sdrgpu {
 // call on a few CUs, so it is written for latency: one global round trip for all image loads,
 // power-of-two decimations (shifts, not divisions), stage loops kept rolled (small code).
 constexpr int TAIL_MAXS = 4;    // stages
-// consecutive outputs per thread (register window). Each thread's chain of D * Q FMAs per output is
-// the kernel's critical path (one or two waves per stage are busy), so fewer outputs per thread
-// (more waves) measured faster: per-call trace 12.0 / 10.3 / 10.0 / 15.5 us at K = 4 / 2 / 1 / 8;
-// prefetching the next tap chunk's LDS reads measured slower (13.8 us at K = 4, 12.0 at K = 2)
+// consecutive outputs per thread (register window), TailArgs::K. Short calls: each thread's chain of D *
+// Q FMAs per output is the kernel's critical path (one or two waves per stage are busy), so fewer
+// outputs per thread (more waves) measured faster: per-call trace 12.0 / 10.3 / 10.0 / 15.5 us at K =
+// 4 / 2 / 1 / 8; prefetching the next tap chunk's LDS reads measured slower (13.8 us at K = 4, 12.0 at
+// K = 2). Big calls (thousands of workgroups): K = 4, 3 us less per C5 step than 2 (r5o), 8 slower
+// (75.2 vs 58.5 us, r5m); 512- and 128-thread workgroups slower (r5o)
 constexpr int TAIL_K = 2;
-constexpr int TAIL_NT = 256;    // threads per workgroup
+constexpr int TAIL_NT = 256;    // threads per workgroup (short calls)
+#ifndef SDRGPU_TAIL_KBIG
+#define SDRGPU_TAIL_KBIG 4
+#endif
+#ifndef SDRGPU_TAIL_NTBIG
+#define SDRGPU_TAIL_NTBIG 256
+#endif
+constexpr int TAIL_K_BIG = SDRGPU_TAIL_KBIG;     // big calls (A/B builds)
+constexpr int TAIL_NT_BIG = SDRGPU_TAIL_NTBIG;
 constexpr int TAIL_PF = 16;     // image loads per thread issued together
 struct TailStage {
     const float2* hist;   // H samples (newest last)
@@ -35,6 +45,8 @@ struct TailArgs {
     const float2* in;     // stage 0's input (n of stage 0 samples)
     float2* out;          // last stage's output
     int S, G;
+    int K;                // outputs per thread (TAIL_K): the image layout depends on it
+    int NT;               // threads per workgroup (TAIL_NT / TAIL_NT_BIG)
     int ldsEl;            // float2 elements of the largest workgroup's images (the taps follow)
     int tapTotal;         // floats of all stages' tap tables
     int tapOff[TAIL_MAXS];   // float offset of stage s's [D][Q] taps behind the images
@@ -65,13 +77,14 @@ __host__ __device__ inline int tail_geometry(const TailArgs& t, int w, TailGeom*
             q.B = q.B < st.n ? q.B : st.n;
             q.E = len;
         }
-        const int nthr = (hi - lo + TAIL_K - 1) / TAIL_K;
-        int rows = nthr * TAIL_K + st.Q + 2 * TAIL_K;
+        const int K = t.K;
+        const int nthr = (hi - lo + K - 1) / K;
+        int rows = nthr * K + st.Q + 2 * K;
         const int need = (q.E - q.B + st.D - 1) / st.D + 1;
         rows = rows > need ? rows : need;
-        q.RSK = (rows + TAIL_K - 1) / TAIL_K;
-        q.RSP = TAIL_K * q.RSK + 1;
-        q.nel = st.D * q.RSK * TAIL_K;
+        q.RSK = (rows + K - 1) / K;
+        q.RSP = K * q.RSK + 1;
+        q.nel = st.D * q.RSK * K;
         // the previous stage's outputs this image holds: in[] indices of [B, E)
         lo = q.B - st.H > 0 ? q.B - st.H : 0;
         hi = q.E - st.H < st.n ? q.E - st.H : st.n;
@@ -86,22 +99,23 @@ __host__ __device__ inline int tail_geometry(const TailArgs& t, int w, TailGeom*
     }
     return base;
 }
-// Tail workgroup w (last: it also writes every stage's next-call history) on threads [0, TAIL_NT)
-// of the block, images in XS, geometry in gs (LDS). Threads past TAIL_NT (the spectrum's 512-thread
-// pass-B launch, fft.hip) take part in the barriers only.
+// Tail workgroup w (last: it also writes every stage's next-call history) on threads [0, NT) of the
+// block, images in XS, geometry in gs (LDS). Threads past NT (the spectrum's 512-thread pass-B launch,
+// fft.hip) take part in the barriers only. K == t.K, NT == t.NT.
+template <int K, int NT>
 __device__ __forceinline__ void fir_tail_block(const TailArgs& t, int w, bool last, float2* XS, TailGeom* gs) {
     const int tid = threadIdx.x;
-    const bool act = tid < TAIL_NT;
+    const bool act = tid < NT;
     // every global load of the launch is issued in one batch (one memory round trip; a dependent
     // round trip to HBM costs ~1-2 us, which is what this kernel is built to avoid): the stages'
-    // tap tables, the histories of stages >= 1 (H <= TAIL_NT, host-checked) and stage 0's image
-    // (<= TAIL_PF * TAIL_NT elements, host-checked). The geometry is wave-uniform (scalar).
+    // tap tables, the histories of stages >= 1 (H <= NT, host-checked) and stage 0's image
+    // (<= TAIL_PF * NT elements, host-checked). The geometry is wave-uniform (scalar).
     TailGeom g[TAIL_MAXS];
     tail_geometry(t, w, g);
     // image element sx (from B) of stage s -> LDS index (fir_kernel's layout)
     auto slot = [&](const TailGeom& q, int dsh, int sx) {
         const int r = sx >> dsh;
-        return q.base + (sx & ((1 << dsh) - 1)) * q.RSP + (r & (TAIL_K - 1)) * q.RSK + r / TAIL_K;
+        return q.base + (sx & ((1 << dsh) - 1)) * q.RSP + (r & (K - 1)) * q.RSK + r / K;
     };
     float* TS = reinterpret_cast<float*>(XS + t.ldsEl);
     if (act) {
@@ -110,7 +124,7 @@ __device__ __forceinline__ void fir_tail_block(const TailArgs& t, int w, bool la
 #pragma unroll
         for (int u = 0; u < TAIL_TP; u++) {
             tap[u] = 0.f;
-            const int j = tid + u * TAIL_NT;
+            const int j = tid + u * NT;
 #pragma unroll
             for (int s = 0; s < TAIL_MAXS; s++) {
                 if (s >= t.S) break;
@@ -129,22 +143,22 @@ __device__ __forceinline__ void fir_tail_block(const TailArgs& t, int w, bool la
         float2 v[TAIL_PF];
 #pragma unroll
         for (int u = 0; u < TAIL_PF; u++) {
-            const int e = g[0].B + tid + u * TAIL_NT;
+            const int e = g[0].B + tid + u * NT;
             const float2* src = (e < g[0].E) ? (e < s0.H ? s0.hist + e : t.in + (e - s0.H)) : nullptr;
             v[u] = src ? *src : make_float2(0.f, 0.f);
         }
 #pragma unroll
         for (int u = 0; u < TAIL_TP; u++)
-            if (tid + u * TAIL_NT < t.tapTotal) TS[tid + u * TAIL_NT] = tap[u];
+            if (tid + u * NT < t.tapTotal) TS[tid + u * NT] = tap[u];
 #pragma unroll
         for (int s = 0; s < TAIL_MAXS; s++)
             if (tid == s && s < t.S) gs[s] = g[s];
-        {   // stage 0: D | TAIL_NT, so a thread's slots advance by a constant (fixed phase and lane)
+        {   // stage 0: D | NT, so a thread's slots advance by a constant (fixed phase and lane)
             int idx = slot(g[0], s0.dsh, tid);
-            const int inc = (TAIL_NT >> s0.dsh) / TAIL_K;
+            const int inc = (NT >> s0.dsh) / K;
 #pragma unroll
             for (int u = 0; u < TAIL_PF; u++) {
-                if (tid + u * TAIL_NT < g[0].nel) XS[idx] = v[u];
+                if (tid + u * NT < g[0].nel) XS[idx] = v[u];
                 idx += inc;
             }
         }
@@ -155,7 +169,7 @@ __device__ __forceinline__ void fir_tail_block(const TailArgs& t, int w, bool la
             if (s >= t.S) break;
             const int H = t.st[s].H;
             if (g[s].B + tid < H && g[s].B + tid < g[s].E) XS[slot(g[s], t.st[s].dsh, tid)] = hv[s];
-            for (int sx = (g[s].E - g[s].B) + tid; sx < g[s].nel; sx += TAIL_NT) XS[slot(g[s], t.st[s].dsh, sx)] = make_float2(0.f, 0.f);
+            for (int sx = (g[s].E - g[s].B) + tid; sx < g[s].nel; sx += NT) XS[slot(g[s], t.st[s].dsh, sx)] = make_float2(0.f, 0.f);
         }
     }
     __syncthreads();
@@ -165,33 +179,35 @@ __device__ __forceinline__ void fir_tail_block(const TailArgs& t, int w, bool la
             const TailStage& st = t.st[s];
             const TailGeom q = gs[s];
             if (last)
-                for (int k = tid; k < st.H; k += TAIL_NT) st.histNext[k] = XS[slot(q, st.dsh, st.n + k - q.B)];
-            const int nthr = (q.b - q.a + TAIL_K - 1) / TAIL_K;
-            for (int l = tid; l < nthr; l += TAIL_NT) {
-                float2 acc[TAIL_K];
+                for (int k = tid; k < st.H; k += NT) st.histNext[k] = XS[slot(q, st.dsh, st.n + k - q.B)];
+            const int nthr = (q.b - q.a + K - 1) / K;
+            for (int l = tid; l < nthr; l += NT) {
+                // (packed fp32: x h + acc per component is the fmaf of mac(), so the same bits)
+                f2v acc[K];
 #pragma unroll
-                for (int i = 0; i < TAIL_K; i++) acc[i] = make_float2(0.f, 0.f);
+                for (int i = 0; i < K; i++) acc[i] = f2v{0.f, 0.f};
                 constexpr int QC = 8;   // st.Q is a multiple of 8 (FirBlock::upload_taps)
+                static_assert(QC % K == 0, "tap chunks of whole register windows");
                 for (int p = 0; p < st.D; p++) {
-                    const float2* Xj[TAIL_K];
+                    const float2* Xj[K];
 #pragma unroll
-                    for (int j = 0; j < TAIL_K; j++) Xj[j] = XS + q.base + p * q.RSP + j * q.RSK + l;
+                    for (int j = 0; j < K; j++) Xj[j] = XS + q.base + p * q.RSP + j * q.RSK + l;
                     const float* Hp = TS + t.tapOff[s] + p * st.Q;   // wave-uniform LDS broadcasts
-                    float2 w[TAIL_K];
+                    f2v w[K];
 #pragma unroll
-                    for (int i = 0; i < TAIL_K; i++) w[i] = Xj[i][0];
+                    for (int i = 0; i < K; i++) w[i] = to_v(Xj[i][0]);
                     for (int q0 = 0; q0 < st.Q; q0 += QC) {
                         float hv[QC];
-                        float2 nx[QC];
+                        f2v nx[QC];
 #pragma unroll
                         for (int u = 0; u < QC; u++) hv[u] = Hp[q0 + u];
 #pragma unroll
-                        for (int u = 0; u < QC; u++) nx[u] = Xj[u % TAIL_K][1 + (q0 + u) / TAIL_K];
+                        for (int u = 0; u < QC; u++) nx[u] = to_v(Xj[u % K][1 + (q0 + u) / K]);
 #pragma unroll
                         for (int u = 0; u < QC; u++) {
 #pragma unroll
-                            for (int i = 0; i < TAIL_K; i++) mac(acc[i], w[(i + u) % TAIL_K], hv[u]);
-                            w[u % TAIL_K] = nx[u];
+                            for (int i = 0; i < K; i++) acc[i] = __builtin_elementwise_fma(w[(i + u) % K], f2v{hv[u], hv[u]}, acc[i]);
+                            w[u % K] = nx[u];
                         }
                     }
                 }
@@ -199,11 +215,11 @@ __device__ __forceinline__ void fir_tail_block(const TailArgs& t, int w, bool la
                 const TailGeom* qn = &gs[lastStage ? s : s + 1];
                 const int dshN = t.st[lastStage ? s : s + 1].dsh, HN = t.st[lastStage ? s : s + 1].H;
 #pragma unroll
-                for (int i = 0; i < TAIL_K; i++) {
-                    const int m = q.a + l * TAIL_K + i;
+                for (int i = 0; i < K; i++) {
+                    const int m = q.a + l * K + i;
                     if (m < q.b) {
-                        if (lastStage) t.out[m] = acc[i];
-                        else XS[slot(*qn, dshN, HN + m - qn->B)] = acc[i];
+                        if (lastStage) t.out[m] = to_f2(acc[i]);
+                        else XS[slot(*qn, dshN, HN + m - qn->B)] = to_f2(acc[i]);
                     }
                 }
             }
