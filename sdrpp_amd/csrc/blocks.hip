@@ -808,10 +808,6 @@ struct FirBlock : Block {
         ttype = ttype_;
         if (decim < 1) { set_error("fir: decimation %d < 1", decim); return SDRGPU_EARG; }
         D = decim;
-        if (const char* e = tuning_env("SDRGPU_FIR_NT")) forceNT = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FIR_K")) forceK = atoi(e);
-        if (const char* e = tuning_env("SDRGPU_FIR_LDS_KB")) ldsCap = std::max(8, atoi(e));
-        if (const char* e = tuning_env("SDRGPU_FIR_MFMA")) useMfma = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FIR_MFMA_NW")) mfNW = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FIR_MFMA_HALF")) mfHalf = atoi(e);
         if (const char* e = tuning_env("SDRGPU_FIR_MFMA_DC")) mfDc = atoi(e);
@@ -1006,7 +1002,7 @@ struct FirBlock : Block {
         if (xl) return quad ? launch_mfma_ps<true, true>(a, tiles, lds, s) : launch_mfma_ps<true, false>(a, tiles, lds, s);
         return quad ? launch_mfma_ps<false, true>(a, tiles, lds, s) : launch_mfma_ps<false, false>(a, tiles, lds, s);
     }
-    int useMfma = 1;        // SDRGPU_FIR_MFMA (tuning): 0 off, 1 auto, 2 also below 16 taps per phase
+    int useMfma = 1;        // f32 MFMA tiles: 1 auto (>= 16 taps per phase)
     DevBuf gzTaps;
     template <int NW, bool XL, bool QD>
     int launch_mfma(FirArgs& a, int tiles, size_t lds, bool half, hipStream_t s) {
@@ -1058,7 +1054,7 @@ struct FirBlock : Block {
         nco.phase.reset();
         return SDRGPU_OK;
     }
-    int forceK = 0;         // SDRGPU_FIR_K (tuning): outputs per thread
+    int forceK = 0;         // (A/B history: outputs per thread forced)
     int choose_k() const {
         if (forceK == 1 || forceK == 2 || forceK == 4 || forceK == 8) return forceK;
         // register blocking pays when a row feeds several taps per phase (unpadded Q large)
@@ -1068,8 +1064,8 @@ struct FirBlock : Block {
         return 1;
     }
     int NT = 256;
-    int forceNT = 0;        // SDRGPU_FIR_NT (tuning): threads per tile
-    int ldsCap = 76;        // SDRGPU_FIR_LDS_KB (tuning): preferred LDS per tile
+    int forceNT = 0;        // (A/B history: threads per tile forced)
+    int ldsCap = 76;        // preferred LDS per tile (KB)
     template <typename DT, typename TT, int K, bool XL, bool QD, bool ST>
     int launch_t(FirArgs& a, int tiles, size_t lds, hipStream_t s) {
         // taps behind the span in LDS when they fit (<= 16 KB)
@@ -1356,7 +1352,7 @@ struct ChainBlock : Block {
     // later-stage launches become one, 1.760 -> 1.747 ms, 3 interleaved runs, r4j; 512 last-stage
     // outputs per workgroup to start from measured best of 32 / 64 / 128 / 512, r4l)
     int tailMode = -1;
-    int tailBigOut = 512;   // big calls: last-stage outputs per workgroup to start from (SDRGPU_TAIL_OUT, tuning)
+    int tailBigOut = 512;   // big calls: last-stage outputs per workgroup to start from
     // big calls: the workgroup count and image size depend only on (n0, the stages' offsets), which
     // repeat call after call; the per-workgroup geometry scan is kept for the last key
     struct TailKey {
@@ -1370,7 +1366,6 @@ struct ChainBlock : Block {
         if (tailMode < 0) {
             const char* e = tuning_env("SDRGPU_VFO_TAIL");
             tailMode = e ? atoi(e) : 2;
-            if (const char* v = tuning_env("SDRGPU_TAIL_OUT")) tailBigOut = std::max(8, atoi(v));
         }
         const int S = (int)kids.size() - 1;
         if (!tailMode || S < 2 || S > TAIL_MAXS) return 0;

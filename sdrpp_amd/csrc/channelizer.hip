@@ -384,7 +384,7 @@ __global__ void chan_hist_kernel(const float2* __restrict__ hist, const float2* 
 struct ChannelizerBlock : Block {
     int M = 0, ntaps = 0, Hp = 0, offset = 0, fpw = 256;
     // two branches per thread (chan2_kernel, no spill): 1.17 vs 1.63 ms per 2^28 samples
-    // against the one-branch kernel on one box; SDRGPU_CHAN_TWO=0 selects chan_kernel
+    // against the one-branch kernel on one box; chan_kernel is the one-branch form
     bool two = true;
     int dft = 0;             // 0: LDS FFT (chan2_kernel); 1: DFT-GEMM on the matrix cores (M = 1024)
     long long phase = 0;     // absolute input index mod M of the next sample
@@ -405,8 +405,6 @@ struct ChannelizerBlock : Block {
         M = channels;
         ntaps = n;
         Hp = CHAN_Q * M - 1;
-        if (const char* e = tuning_env("SDRGPU_CHAN_FPW")) fpw = std::max(16, atoi(e) / 16 * 16);
-        if (const char* e = tuning_env("SDRGPU_CHAN_TWO")) two = atoi(e) != 0;
         SDRGPU_CHECK(init_stream());
         std::vector<float> pq((size_t)CHAN_Q * M, 0.0f);       // [q][r] = h[q M + r]
         for (int j = 0; j < n; j++) pq[j] = t[j];

@@ -832,8 +832,10 @@ constexpr int M = 16384;
 constexpr int RS = 560;                 // LDS row stride (float2)
 constexpr int TW512 = 32 * RS;          // W_512^(t0 q1) at [q1][t0]
 constexpr int W128 = TW512 + 512;       // W_128^(r i), i < 32
-constexpr int LDS_BYTES = (W128 + 64) * 8;
+constexpr int W128D = (W128 + 64) * 8;   // (bytes) fp64 W_128^(r i), r = r0, r0 + 1, i < 32
+constexpr int LDS_BYTES = W128D + 64 * 16;
 constexpr int TAB = 512 + 128;          // device table: [q1][t0] W_512^(t0 q1), [r][i] W_128^(r i)
+constexpr int TAB64 = 2048 + 128;       // fp64 table: W_N^m (m < 2048), [r][i] W_128^(r i)
 }
 
 // x w, rounded on its own: never contracted into the radix-4 adds that follow (left to the compiler,
@@ -931,7 +933,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
     {
         const int t = threadIdx.x;
         lds[TW512 + t] = tab[t];
-        if (t < 64) lds[W128 + t] = tab[512 + 32 * (r0 + (t >> 5)) + (t & 31)];   // W_128^(r i), r = r0, r0 + 1
+        if (t < 64) reinterpret_cast<double2*>(reinterpret_cast<char*>(lds) + op1::W128D)[t] = tab64[2048 + 32 * (r0 + (t >> 5)) + (t & 31)];
     }
     // stage 1: y_r for r = r0 (even) and r0 + 1 (odd) from the four quarters: y_r = A_r + W_4^r q_r with
     // A_r = u0 + s_r u2, q_r = u1 + s_r u3, s_r = (-1)^r; W_4^r in {1, -i, -1, i} as (fx, fy), one of
@@ -942,6 +944,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         const float2 aa = cadd(u[0], u[2]), qa = cadd(u[1], u[3]), ab = csub(u[0], u[2]), qb = csub(u[1], u[3]);
         ya = make_float2(fmaf(fxa, qa.x, aa.x), fmaf(fxa, qa.y, aa.y));     // aa + W_4^r0 qa (exact products)
         yb = make_float2(fmaf(-fyb, qb.y, ab.x), fmaf(fyb, qb.x, ab.y));    // ab + W_4^(r0+1) qb
+    };
+    // stage 1's twiddle W_128^(r i) = W_N^(512 r i) on row i, applied where the row is combined (few
+    // registers live there): an fp64 product of the fp64 twiddle, rounded once. As an fp32 product with
+    // an fp32 table (two roundings) the near-peak bins of tonal frames were 1-2 ulp off more often than
+    // pocketfft's (AES17: 7 of 22 bins beyond 1 ulp vs 4; 2 with this form, r5x / r5y)
+    auto w128 = [&](float2& y, int h, int i) {
+        const double2 w = reinterpret_cast<const double2*>(reinterpret_cast<const char*>(lds) + op1::W128D)[32 * h + i];
+        const double2 q = zmul(make_double2(y.x, y.y), w);
+        y = make_float2((float)q.x, (float)q.y);
     };
     const unsigned lim = PAD ? (unsigned)nz : 65536u;     // (PAD: range-checked loads, 0 past nz)
     const __amdgpu_buffer_rsrc_t rw = brsrc(win, lim * 4u);
@@ -976,6 +987,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
 #pragma unroll
             for (int j = 0; j < 4; j++) u[j] = wmul(xv[bb & 1][ii][j], wv[bb & 1][ii][j]);
             combine2(u, za[PB * bb + ii], zb[PB * bb + ii]);
+            if (PB * bb + ii > 0) {
+                if (p) w128(za[PB * bb + ii], 0, PB * bb + ii);   // (quarter 0: W_128^0 = 1)
+                w128(zb[PB * bb + ii], 1, PB * bb + ii);
+            }
+            asm volatile("" : "+v"(za[PB * bb + ii].x), "+v"(za[PB * bb + ii].y), "+v"(zb[PB * bb + ii].x), "+v"(zb[PB * bb + ii].y));
         }
         if constexpr (bb + 2 < NB) issue(std::integral_constant<int, bb + 2>{});
         __builtin_amdgcn_sched_barrier(0);
@@ -1056,6 +1072,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
                 u[j] = wmul(xx, ww);
             }
             combine2(u, za[i], zb[i]);
+            if constexpr (i > 0) {
+                if (p) w128(za[i], 0, i);   // (quarter 0: W_128^0 = 1)
+                w128(zb[i], 1, i);
+            }
+            // (pinned here: left alone, the compiler sinks the combine past the loop and keeps the raw
+            // x / w reads live instead, 1.5x the registers, spilled)
+            asm volatile("" : "+v"(za[i].x), "+v"(za[i].y), "+v"(zb[i].x), "+v"(zb[i].y));
             __builtin_amdgcn_sched_barrier(0);
         });
     }
@@ -1071,8 +1094,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         __syncthreads();   // (h = 0: the tables staged; h = 1: quarter r0's stage-3 reads of the image are done)
         {   // stage-1 finish: W_128^(r i), radix 32, W_N^(t (4 k2 + r)), into the LDS image
             const int t = tid();
-#pragma unroll
-            for (int i = 1; i < 32; i++) z[i] = cmul(z[i], lds[W128 + 32 * h + i]);   // W_128^(r i) = W_N^(512 r i)
             dft32(z);
             // W_N^(t r) (W_N^(4 t))^k2 as two independent fp64 chains over even / odd k2 (a serial chain of
             // 31 fp64 complex products was the stage's critical path)
@@ -1273,7 +1294,7 @@ struct FftPlan {
     bool timing = false;
     hipEvent_t tev[kTimed][2] = {};
     long long tcalls = 0;
-    int vfoFuse = 1;                  // SDRGPU_FFT_VFO_FUSE=0 (tuning): spectrum and VFO as separate launch groups
+    int vfoFuse = 1;                  // the VFO's first stage inside the spectrum launches
     int onepass = 0;                  // the 64k plan's one-pass launches (fft_1p_kernel), SDRGPU_FFT_1P (tuning)
     DevBuf tab1p, tab1p64, zpart;
 };
@@ -1530,7 +1551,6 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         // one-column kernel at N1 = 256 (64k: 2.05-2.10 vs 1.86 ms per 2^28 samples, A/B on
         // one box), so it is the default only for N1 >= 512
         p.sa2 = p.N1 >= 512 ? 16 : 0;
-        if (const char* e = tuning_env("SDRGPU_FFT_VFO_FUSE")) p.vfoFuse = atoi(e);
         // 64k: the one-pass transform (fft_1p_kernel) is the default since r5 (C5 group 1.45 vs 1.63 ms
         // per 2^28 samples for the two-pass launches, A/B on one box); SDRGPU_FFT_1P=0 keeps the latter
         p.onepass = fftSize == 65536;
@@ -1545,11 +1565,14 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
                 for (int t0 = 0; t0 < 16; t0++) t[16 * q1 + t0] = w(128LL * t0 * q1);
             for (int r = 0; r < 4; r++)
                 for (int i = 0; i < 32; i++) t[512 + 32 * r + i] = w(512LL * r * i);
-            std::vector<double2> t64(2048);   // W_N^m, m < 2048, fp64 (the stage-1 twiddle recurrence)
-            for (int m = 0; m < 2048; m++) {
-                const double a = -2.0 * M_PI * (double)m / (double)fftSize;
-                t64[m] = make_double2(std::cos(a), std::sin(a));
-            }
+            std::vector<double2> t64(op1::TAB64);   // fp64: W_N^m, m < 2048 (the stage-1 twiddle recurrence); W_128^(r i)
+            auto w64 = [&](long long m) {
+                const double a = -2.0 * M_PI * (double)(m % fftSize) / (double)fftSize;
+                return make_double2(std::cos(a), std::sin(a));
+            };
+            for (int m = 0; m < 2048; m++) t64[m] = w64(m);
+            for (int r = 0; r < 4; r++)
+                for (int i = 0; i < 32; i++) t64[2048 + 32 * r + i] = w64(512LL * r * i);
             rc = p.tab1p.ensure(sizeof(float2) * t.size());
             if (rc >= 0) rc = p.tab1p64.ensure(sizeof(double2) * t64.size());
             if (rc >= 0 && (hipMemcpy(p.tab1p.p, t.data(), sizeof(float2) * t.size(), hipMemcpyHostToDevice) != hipSuccess ||

@@ -82,8 +82,8 @@ struct sdrgpu_frontend {
     hipStream_t cs = nullptr;
     PipeSlot pipe[2];
     long long nextTicket = 0;
-    int split = 1;   // fft_execute_split for pushes that complete frames (SDRGPU_FE_SPLIT=0, tuning: stitch copies)
-    // the first VFO's first stage inside that pass-A launch (SDRGPU_FE_FUSE=0, tuning: its own launch)
+    int split = 1;   // fft_execute_split for pushes that complete frames (else stitch copies)
+    // the first VFO's first stage inside that pass-A launch 
     int fuse = 1;
 };
 
@@ -136,8 +136,6 @@ extern "C" int sdrgpu_frontend_create(sdrgpu_frontend** out, int device, double 
     f->fftSize = fftSize;
     f->fftRate = fftRate;
     f->window = windowType;
-    if (const char* e = tuning_env("SDRGPU_FE_SPLIT")) f->split = atoi(e);
-    if (const char* e = tuning_env("SDRGPU_FE_FUSE")) f->fuse = atoi(e);
     int rc = hipStreamCreateWithFlags(&f->s, hipStreamNonBlocking) == hipSuccess ? SDRGPU_OK : SDRGPU_EHIP;
     if (rc < 0) set_error("frontend_create: hipStreamCreate failed");
     if (rc >= 0) rc = fe_build_preproc(f);
