@@ -945,15 +945,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         ya = make_float2(fmaf(fxa, qa.x, aa.x), fmaf(fxa, qa.y, aa.y));     // aa + W_4^r0 qa (exact products)
         yb = make_float2(fmaf(-fyb, qb.y, ab.x), fmaf(fyb, qb.x, ab.y));    // ab + W_4^(r0+1) qb
     };
-    // stage 1's twiddle W_128^(r i) = W_N^(512 r i) on row i, applied where the row is combined (few
-    // registers live there): an fp64 product of the fp64 twiddle, rounded once. As an fp32 product with
-    // an fp32 table (two roundings) the near-peak bins of tonal frames were 1-2 ulp off more often than
-    // pocketfft's (AES17: 7 of 22 bins beyond 1 ulp vs 4; 2 with this form, r5x / r5y)
-    auto w128 = [&](float2& y, int h, int i) {
-        const double2 w = reinterpret_cast<const double2*>(reinterpret_cast<const char*>(lds) + op1::W128D)[32 * h + i];
-        const double2 q = zmul(make_double2(y.x, y.y), w);
-        y = make_float2((float)q.x, (float)q.y);
-    };
     const unsigned lim = PAD ? (unsigned)nz : 65536u;     // (PAD: range-checked loads, 0 past nz)
     const __amdgpu_buffer_rsrc_t rw = brsrc(win, lim * 4u);
     const __amdgpu_buffer_rsrc_t rx = brsrc(in + (long long)f * frameStride, lim * 8u);
@@ -987,11 +978,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
 #pragma unroll
             for (int j = 0; j < 4; j++) u[j] = wmul(xv[bb & 1][ii][j], wv[bb & 1][ii][j]);
             combine2(u, za[PB * bb + ii], zb[PB * bb + ii]);
-            if (PB * bb + ii > 0) {
-                if (p) w128(za[PB * bb + ii], 0, PB * bb + ii);   // (quarter 0: W_128^0 = 1)
-                w128(zb[PB * bb + ii], 1, PB * bb + ii);
-            }
-            asm volatile("" : "+v"(za[PB * bb + ii].x), "+v"(za[PB * bb + ii].y), "+v"(zb[PB * bb + ii].x), "+v"(zb[PB * bb + ii].y));
+
         }
         if constexpr (bb + 2 < NB) issue(std::integral_constant<int, bb + 2>{});
         __builtin_amdgcn_sched_barrier(0);
@@ -1072,13 +1059,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
                 u[j] = wmul(xx, ww);
             }
             combine2(u, za[i], zb[i]);
-            if constexpr (i > 0) {
-                if (p) w128(za[i], 0, i);   // (quarter 0: W_128^0 = 1)
-                w128(zb[i], 1, i);
-            }
-            // (pinned here: left alone, the compiler sinks the combine past the loop and keeps the raw
-            // x / w reads live instead, 1.5x the registers, spilled)
-            asm volatile("" : "+v"(za[i].x), "+v"(za[i].y), "+v"(zb[i].x), "+v"(zb[i].y));
             __builtin_amdgcn_sched_barrier(0);
         });
     }
@@ -1094,6 +1074,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         __syncthreads();   // (h = 0: the tables staged; h = 1: quarter r0's stage-3 reads of the image are done)
         {   // stage-1 finish: W_128^(r i), radix 32, W_N^(t (4 k2 + r)), into the LDS image
             const int t = tid();
+            // W_128^(r i) = W_N^(512 r i) as an fp64 product of the fp64 twiddle, rounded once. As an fp32
+            // product with an fp32 table (two roundings) the near-peak bins of tonal frames were 1-2 ulp
+            // off more often than pocketfft's (AES17: 7 of 22 bins beyond 1 ulp vs pocketfft's 4; 2 in
+            // this form), +2.7% kernel time (r5x-r5z; applied at the combine instead: +5%)
+            const double2* w128 = reinterpret_cast<const double2*>(reinterpret_cast<const char*>(lds) + op1::W128D) + 32 * h;
+            if (r != 0) {   // (quarter 0: W_128^0 = 1)
+#pragma unroll
+                for (int i = 1; i < 32; i++) {
+                    const double2 q = zmul(make_double2(z[i].x, z[i].y), w128[i]);
+                    z[i] = make_float2((float)q.x, (float)q.y);
+                }
+            }
             dft32(z);
             // W_N^(t r) (W_N^(4 t))^k2 as two independent fp64 chains over even / odd k2 (a serial chain of
             // 31 fp64 complex products was the stage's critical path)

@@ -160,8 +160,43 @@ __device__ __forceinline__ void zfft(double2* lds, const double2* __restrict__ t
     }
 }
 
-// K3 in fp64: 10 log10 |X|^2, rounded once (p = 0 -> -inf, as log10f)
-__device__ __forceinline__ float zdb(double2 X) { return (float)(10.0 * log10(X.x * X.x + X.y * X.y)); }
+// K3 in fp64: 10 log10 |X|^2, rounded once (p = 0 -> -inf, as log10f). 10 log10 p = (10 / ln 10) (e ln 2
+// + ln m) with p = m 2^e, m in [sqrt(1/2), sqrt(2)); ln m = 2 atanh(s) = 2 s (1 + s^2/3 + ... + s^20/21),
+// s = (m - 1) / (m + 1), |s| <= 0.1716, so the series' remainder is below 3e-17 and the result carries
+// a few fp64 ulps (~1e-15 relative), far inside one fp32 ulp of the dB value; about half the VALU of
+// the device libm's log10, which was the pass-B kernel's largest cost (SDRGPU_F64_LIBLOG: A/B builds)
+#ifndef SDRGPU_F64_LIBLOG
+#define SDRGPU_F64_LIBLOG 0
+#endif
+__device__ __forceinline__ float zdb(double2 X) {
+    const double p = X.x * X.x + X.y * X.y;
+#if SDRGPU_F64_LIBLOG
+    return (float)(10.0 * log10(p));
+#else
+    if (!(p > 0.0) || !(p < 1.0e308)) return (float)(10.0 * log10(p));   // (0, inf, nan: the libm path)
+    int e;
+    double m = frexp(p, &e);   // [0.5, 1)
+    if (m < 0.70710678118654752440) {
+        m *= 2.0;
+        e -= 1;
+    }
+    const double s = (m - 1.0) / (m + 1.0), t = s * s;
+    double P = 1.0 / 21.0;
+    P = fma(P, t, 1.0 / 19.0);
+    P = fma(P, t, 1.0 / 17.0);
+    P = fma(P, t, 1.0 / 15.0);
+    P = fma(P, t, 1.0 / 13.0);
+    P = fma(P, t, 1.0 / 11.0);
+    P = fma(P, t, 1.0 / 9.0);
+    P = fma(P, t, 1.0 / 7.0);
+    P = fma(P, t, 1.0 / 5.0);
+    P = fma(P, t, 1.0 / 3.0);
+    const double lnm = 2.0 * s + (2.0 * s * t) * P;   // 2 s (1 + t P)
+    const double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
+    const double ln = fma((double)e, LN2_HI, fma((double)e, LN2_LO, lnm));
+    return (float)(4.34294481903251827651 * ln);
+#endif
+}
 
 // K1: the reference's fp32 window product, then exact promotion
 __device__ __forceinline__ double2 windowed(float2 x, float w) {
@@ -248,6 +283,10 @@ int zset_lds(K kernel, size_t bytes) {
 
 // columns / rows per workgroup for a length-L transform (LDS: S x LS x 16 B <= 140 KB)
 constexpr int zS(int L) { return L <= 256 ? 16 : L <= 1024 ? 8 : L == 2048 ? 2 : 1; }
+#ifndef SDRGPU_F64_SA256
+#define SDRGPU_F64_SA256 16   // (A/B builds) pass-A columns per workgroup at N1 = 256
+#endif
+constexpr int zSA(int L) { return L == 256 ? SDRGPU_F64_SA256 : zS(L); }
 
 template <int L>
 int launch_single64(const double2* tw, const float2* in, long long stride, int frames, const float* win, int nz, float* out,
@@ -264,7 +303,7 @@ int launch_single64(const double2* tw, const float2* in, long long stride, int f
 template <int L>
 int launch_passA64(const double2* tw, const float2* in, long long stride, int frames, const float* win, int nz, int N2, int logN,
                    const double2* thi, const double2* tlo, double2* scratch, hipStream_t s) {
-    constexpr int S = zS(L);
+    constexpr int S = zSA(L);
     if (N2 % S) { set_error("fft64: N2 %d not a multiple of %d", N2, S); return SDRGPU_ESTATE; }
     auto k = fft64_passA_kernel<L, S>;
     const size_t lds = sizeof(double2) * S * ZLds<L>::LS;
