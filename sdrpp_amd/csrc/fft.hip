@@ -1079,12 +1079,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             // off more often than pocketfft's (AES17: 7 of 22 bins beyond 1 ulp vs pocketfft's 4; 2 in
             // this form), +2.7% kernel time (r5x-r5z; applied at the combine instead: +5%)
             const double2* w128 = reinterpret_cast<const double2*>(reinterpret_cast<const char*>(lds) + op1::W128D) + 32 * h;
-            if (r != 0) {   // (quarter 0: W_128^0 = 1)
+            // (also for quarter 0, where W = 1 and the product is exact: a branch around it spilled)
 #pragma unroll
-                for (int i = 1; i < 32; i++) {
-                    const double2 q = zmul(make_double2(z[i].x, z[i].y), w128[i]);
-                    z[i] = make_float2((float)q.x, (float)q.y);
-                }
+            for (int i = 1; i < 32; i++) {
+                const double2 q = zmul(make_double2(z[i].x, z[i].y), w128[i]);
+                z[i] = make_float2((float)q.x, (float)q.y);
             }
             dft32(z);
             // W_N^(t r) (W_N^(4 t))^k2 as two independent fp64 chains over even / odd k2 (a serial chain of
