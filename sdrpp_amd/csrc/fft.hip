@@ -808,22 +808,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
 //     = W_N^(t (4 k2 + r)) give A[t][k2];
 //   stage 2 (LDS): per (k2, t0), a radix-32 DFT over t1 of A[t0 + 16 t1][k2], twiddle W_512^(t0 q1);
 //   stage 3 (LDS): per (k2, q1), a radix-16 DFT over t0 -> Y[k2 + 32 q1 + 1024 q2], dB, store.
-// The four items of a frame run at the same time on one XCD, so the frame is fetched from HBM once and
-// read by the other three from that XCD's L2. Fabric traffic per sample is the input (8 B) and the dB
-// row (4 B): the two-pass transform's 16 B of intermediate are gone (PMC 17.0 B/sample, r4).
-//
-// Persistent and software-pipelined (round 5). Round 4's form (one item per workgroup) moved 17 B per
-// sample but ran its phases one after another on a CU that held nothing else: per item 59k cycles, of
-// which the frame's loads (768 KB per item through the CU: the whole frame and the window, for a
-// quarter of the bins) took ~29k and the stages ~13k (phase stamps, profiles/r4/onepass). Here each
-// workgroup owns a fixed quarter r and walks the frames of its XCD lane; while item j's LDS stages run,
-// item j + 1's sample rows are already loading into a two-batch register ring and are combined into
-// the stage-1 registers between the stage slices (the loads for item j + 1 are issued right after item
-// j's LDS image is written, the combine steps are interleaved with stage 2 and stage 3). The VFO's
-// stage-1 quarter r of frame f (VFO) runs right after item (f, r)'s image is written, while the next
-// item's first batches fly: the lines it reads were just fetched by the frame's four items, and only
-// the ring is live at that point. Workgroup b (XCD lane b mod 8 under round-robin dispatch, for
-// speed only) takes quarter r = (b / 8) mod 4 of frames 8 (j G/32 + b / 32) + b mod 8, j = 0, 1, ...
+// A frame's two workgroups (quarters 0-1 and 2-3, the pair's bins 4 m + r0, 4 m + r0 + 1 adjacent so
+// the dB rows leave as 8-byte pairs) sit on one XCD (blocks of 8 frames under round-robin dispatch, for
+// speed only), so the frame is fetched from HBM once per reader and its second read is mostly served by
+// that XCD's L2. The rows stream into LDS by LDS-DMA through a ring of row sets (below). The default
+// since round 5 (C5 group 1.51 ms, 20.9 B/sample of fabric traffic, against 1.63 ms and 30.4 B for the
+// two-pass launches). Rejected forms: one item per
+// workgroup (1.89 ms), a persistent software-pipelined quarter-per-workgroup walk (2.06 ms, spills), the
+// VFO half inside the row loop (1.60-1.91 ms).
 // LDS image: 32 rows k2 of 544 used float2 (stage 1: column pad16(t); stage 2: column 17 q1 +
 // (t0 ^ ((k2 >> 1) & 15))), row stride 560 (= 16 mod 32): every stage-2/3 access of a half-wave hits
 // 32 distinct 8-byte bank pairs.
