@@ -1278,7 +1278,8 @@ struct FftPlan {
     hipEvent_t tev[kTimed][2] = {};
     long long tcalls = 0;
     int vfoFuse = 1;                  // the VFO's first stage inside the spectrum launches
-    int onepass = 0;                  // the 64k plan's one-pass launches (fft_1p_kernel), SDRGPU_FFT_1P (tuning)
+    int onepass = 0;                  // the 64k plan's one-pass kernel (fft_1p_kernel): 0 never, 1 always, 2 calls of
+                                      // >= k1pMinFrames frames (SDRGPU_FFT_1P, tuning)
     DevBuf tab1p, tab1p64, zpart;
 };
 static int time_mark(FftPlan& p, int which, hipStream_t s) {
@@ -1536,7 +1537,7 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
         p.sa2 = p.N1 >= 512 ? 16 : 0;
         // 64k: the one-pass transform (fft_1p_kernel) is the default since r5 (C5 group 1.45 vs 1.63 ms
         // per 2^28 samples for the two-pass launches, A/B on one box); SDRGPU_FFT_1P=0 keeps the latter
-        p.onepass = fftSize == 65536;
+        p.onepass = fftSize == 65536 ? 2 : 0;
         if (const char* e = tuning_env("SDRGPU_FFT_1P")) p.onepass = atoi(e);
         if (rc >= 0 && fftSize == 65536) {   // fft_1p_kernel's exact twiddles (op1::TAB)
             std::vector<float2> t(op1::TAB);
@@ -1662,7 +1663,13 @@ static int launch_1p(FftPlan& p, const float2* in, long long stride, int frames,
     }
     return SDRGPU_OK;
 }
-static bool onepass_ok(const FftPlan& p) { return p.onepass && p.N == 65536 && p.tab1p.p && !p.f64; }
+// Below k1pMinFrames frames a call runs the two-pass launches: with two workgroups per frame, each two
+// 16k transforms long, a reference-size block (4.7 frames) took 33 us against 27 us for the two-pass
+// launches (per-call trace r6c vs r4); the one-pass kernel fills the device from ~128 frames.
+constexpr int k1pMinFrames = 64;
+static bool onepass_ok(const FftPlan& p, int frames) {
+    return p.N == 65536 && p.tab1p.p && !p.f64 && (p.onepass == 1 || (p.onepass == 2 && frames >= k1pMinFrames));
+}
 
 // frames -> dB rows (and, with zoom != nullptr on a zoom_fusable plan, the full-span zoom rows)
 static int fft_execute_body(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, float* zoom,
@@ -1684,7 +1691,7 @@ static int fft_execute_body(sdrgpu_fft* h, const void* in, long long frameStride
         SDRGPU_CHECK(dispatch_single(p, x, frameStride, frames, out, s));
         return frames;
     }
-    if (onepass_ok(p)) {
+    if (onepass_ok(p, frames)) {
         const int rc = zoom ? launch_1p<true, false>(p, x, frameStride, frames, out, zoom, VfoWork{}, s)
                             : launch_1p<false, false>(p, x, frameStride, frames, out, nullptr, VfoWork{}, s);
         if (rc < 0) return rc;
@@ -1871,7 +1878,7 @@ static bool vfo_fusable(const FftPlan& p, float* zoom, int zoomSize) {
 // side stream beside the last launch they measured slower: 1.725 vs 1.705 ms, r4i).
 static int fft_execute_vfo(FftPlan& p, const float2* x, int frames, float* out, float* zoom, const VfoStage1& st,
                            sdrgpu_block* vfo, void* vfoOut, hipStream_t s) {
-    if (onepass_ok(p)) {
+    if (onepass_ok(p, frames)) {
         VfoWork v{st.a, 0, 1};
         SDRGPU_CHECK(time_mark(p, 0, s));
         const int rc = zoom ? launch_1p<true, true>(p, x, p.N, frames, out, zoom, v, s)
