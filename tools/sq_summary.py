@@ -1,34 +1,53 @@
-"""C3 MFMA FIR issue picture from tools/pmc_r2b.sh counter CSVs (one pass per set):
-python tools/sq_summary.py <dir with c3_mfma_counters.csv, c3_issue_counters.csv, c3_mfma_kernel_trace.csv>
+"""Reduce tools/pmc_sets.sh SQ counter runs to per-kernel per-dispatch means and derived ratios.
 
-SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles, SQ_VALU_MFMA_BUSY_CYCLES cycles
-per SIMD (summed), GRBM_GUI_ACTIVE cycles summed over the 8 XCDs (MI355X_MICROARCH.md)."""
-import csv, json, sys
+  python tools/sq_summary.py gpurun_out/<TAG>   (reads <TAG>_1 .. <TAG>_5/run_counter_collection.csv)
 
-d = sys.argv[1]
-m = {}
-for f in ("c3_mfma_counters.csv", "c3_issue_counters.csv"):
-    acc = {}
-    for r in csv.DictReader(open(f"{d}/{f}")):
-        if "fir_mfma_kernel" in r["Kernel_Name"]:
-            acc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    for k, v in acc.items():
-        m.setdefault(k, sum(v) / len(v))
-dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-       for r in csv.DictReader(open(f"{d}/c3_mfma_kernel_trace.csv")) if "fir_mfma_kernel" in r["Kernel_Name"]]
-t = sum(dur) / len(dur)
-SIMDS = 1024
-cyc = m["GRBM_GUI_ACTIVE"] / 8
-w = m["SQ_WAVE_CYCLES"]
-out = {
-    "kernel": "fir_mfma_kernel<4, XL, QUAD> (C3)", "kernel_us_profiled": round(t * 1e6, 1),
-    "clock_ghz_effective": round(cyc / t / 1e9, 3),
-    "mfma_busy_frac": round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / SIMDS / cyc, 3),
-    "mfma_cycles_per_instruction": round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / m["SQ_INSTS_MFMA"], 2),
-    "waves_per_simd_avg": round(w * 4 / SIMDS / cyc, 2),
-    "wave_cycle_split": {k: round(m[k] / w, 3) for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY")},
-    "active_split": {k: round(m[k] / w, 3) for k in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS")},
-    "lds_bank_conflict_per_lds_active": round(m["SQ_LDS_BANK_CONFLICT"] / m["SQ_ACTIVE_INST_LDS"], 2),
-    "counters_avg_per_dispatch": {k: round(v) for k, v in sorted(m.items())},
-}
-print(json.dumps(out, indent=1))
+Ratios (per dispatch, summed over its waves): VALU instructions per wave; busy fractions of the wave
+cycles: SQ_ACTIVE_INST_VALU, SQ_ACTIVE_INST_ANY, SQ_WAIT_INST_ANY (waiting on a dependency or
+waitcnt), SQ_WAIT_ANY, LDS busy and bank conflicts; the dispatch duration from the kernel trace."""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+
+def main():
+    tag = sys.argv[1]
+    acc = defaultdict(lambda: defaultdict(list))   # kernel -> counter -> per-dispatch values
+    dur = defaultdict(list)
+    for f in sorted(glob.glob(tag + "_[0-9]/run_counter_collection.csv")):
+        per = defaultdict(lambda: defaultdict(float))
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            per[(k, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+            per[(k, r["Dispatch_Id"])]["_ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+        for (k, _), c in per.items():
+            for name, v in c.items():
+                if name == "_ns":
+                    dur[k].append(v)
+                else:
+                    acc[k][name].append(v)
+    out = {}
+    for k, c in acc.items():
+        m = {n: sum(v) / len(v) for n, v in c.items()}
+        d = {"counters_mean_per_dispatch": {n: round(v, 1) for n, v in sorted(m.items())},
+             "dispatch_us_mean": round(sum(dur[k]) / len(dur[k]) / 1e3, 2) if dur[k] else None}
+        wc = m.get("SQ_WAVE_CYCLES")
+        if wc:
+            for n in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_LDS",
+                      "SQ_WAIT_INST_LDS", "SQ_INST_CYCLES_VMEM_RD", "SQ_ACTIVE_INST_SCA"):
+                if n in m:
+                    d[n + "_frac_of_wave_cycles"] = round(m[n] / wc, 3)
+        if m.get("SQ_WAVES"):
+            d["valu_insts_per_wave"] = round(m.get("SQ_INSTS_VALU", 0) / m["SQ_WAVES"], 1)
+            d["vmem_rd_per_wave"] = round(m.get("SQ_INSTS_VMEM_RD", 0) / m["SQ_WAVES"], 1)
+            d["lds_insts_per_wave"] = round(m.get("SQ_INSTS_LDS", 0) / m["SQ_WAVES"], 1)
+        if m.get("SQ_INSTS_LDS"):
+            d["lds_bank_conflict_cycles_per_lds_inst"] = round(m.get("SQ_LDS_BANK_CONFLICT", 0) / m["SQ_INSTS_LDS"], 3)
+        out[k] = d
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
