@@ -449,11 +449,21 @@ __device__ __forceinline__ void tile_fb(int T, int nb, int& b, long long& f) {
 // the next tile's 16 row values per thread loaded while the current tile is transformed and stored.
 // The intermediate is pass A's tile-major layout [block][k1][16 columns]: a row piece of 16 columns is
 // 128 contiguous bytes. Row blocks XCD-grouped by 4 (1.93 vs 1.97 ms per C2 step; ungrouped 2.06).
+// Sequence stride LSB = 1090 float2 (even; Lds<1024>::LS = 1089 elsewhere). After stage 1 a
+// half-wave holds 8 sequences x 2 (read2/write2, banks by float2 index mod 16) or 4 (ds_read_b64, mod
+// 32) consecutive butterflies: at stride 1089 (= 1 mod 32) sequence s and butterfly t + 1 share the
+// banks of s + 1 and t -- the middle stage's accesses 2-way, the last stage's reads 4-way, 3.7
+// conflict cycles per LDS instruction measured (r6e SQ counters, tools/lds_bank_model.py reproduces
+// it); at 1090 (= 2 mod 32) the middle stage is conflict-free and the last stage's reads 2-way.
+#ifndef SDRGPU_PB1M_LS
+#define SDRGPU_PB1M_LS 1090   // (A/B builds: 1089)
+#endif
+constexpr int kPassB1mLS = SDRGPU_PB1M_LS;
 __global__ __launch_bounds__(512) void fft_passB_1m_kernel(const float2* __restrict__ scratch, int frames, int N1, int logN,
                                                            const float2* __restrict__ tw, float* __restrict__ out) {
-    constexpr int L = 1024, T = L / 16, S = 8, XG = 4;
+    constexpr int L = 1024, T = L / 16, S = 8, XG = 4, LSB = kPassB1mLS;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    float2* twl = lds + S * Lds<L>::LS;   // stage twiddles, staged once per workgroup
+    float2* twl = lds + S * LSB;   // stage twiddles, staged once per workgroup
     float2* tw16 = twl + L;                // the middle stage's, bank-conflict-free (stage_lds)
     const int tid = threadIdx.x;
     for (int i = tid; i < L; i += S * T) twl[i] = tw[i];   // (first barrier below orders both)
@@ -484,13 +494,13 @@ __global__ __launch_bounds__(512) void fft_passB_1m_kernel(const float2* __restr
         asm volatile("" : "+v"(tv));
         const int sF2 = tv / T, tF2 = tv % T, sL2 = tv % S, tL2 = tv / S;
         __syncthreads();   // the previous tile's last LDS reads are done
-        stage_first<L>(lds + sF2 * Lds<L>::LS, v, tF2);
+        stage_first<L>(lds + sF2 * LSB, v, tF2);
         __syncthreads();
         int b;
         long long f;
         tile_fb<XG>(tile, nb, b, f);
         const __amdgpu_buffer_rsrc_t ro = brsrc(out + (f << logN) + b * S, 0x7fffffffu);
-        stages_rest<L, true>(lds, twl, sL2, tL2, [&](int k2, float2 y) {
+        stages_rest<L, true, LSB>(lds, twl, sL2, tL2, [&](int k2, float2 y) {
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, db_of(y)), ro, (unsigned)(sL2 + N1 * k2) * 4u, 0, 0);
         }, tw16);
     }
@@ -1412,7 +1422,7 @@ static int dispatch_1m(FftPlan& p, const float2* xc, long long stride, int nf, f
         SDRGPU_HIP(hipGetLastError());
     }
     auto k = fft_passB_1m_kernel;
-    const size_t lds = sizeof(float2) * (8 * Lds<1024>::LS + 1024 + 256);
+    const size_t lds = sizeof(float2) * (8 * kPassB1mLS + 1024 + 256);   // 80,000 B: two workgroups per CU
     SDRGPU_CHECK(set_lds(k, lds));
     SDRGPU_CHECK(resident_grid(p, k, 512, lds, p.gridB));
     const int ntiles = (p.N1 / 8) * nf;

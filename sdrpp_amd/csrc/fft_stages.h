@@ -230,10 +230,10 @@ __device__ __forceinline__ void stage_first(float2* seq, float2 (&v)[16], int t)
 // Stages after the first: LDS -> ... -> store functor. Expects stage_first's LDS writes
 // to be complete (caller's barrier); leaves the LDS free for reuse on return. T16: the radix-16
 // stage with NS = 16 (L >= 256) reads its twiddles from tw16 (stage_lds), staged by the caller.
-template <int L, bool T16 = false, class Store>
+// LS: the sequence stride of the caller's LDS image (stage_first wrote sequence s at lds + s LS).
+template <int L, bool T16 = false, int LS = Lds<L>::LS, class Store>
 __device__ __forceinline__ void stages_rest(float2* lds, const float2* __restrict__ tw, int sL, int tL, Store&& st,
                                             const float2* tw16 = nullptr) {
-    constexpr int LS = Lds<L>::LS;
     const float2* seqL = lds + sL * LS;
     if constexpr (L == 64) {
         stage_last<L, 4, 16>(seqL, tw, tL, st);
