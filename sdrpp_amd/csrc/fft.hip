@@ -882,6 +882,11 @@ constexpr int k1pPB = 2;   // (PAD) sample rows per load batch: 4 PB loads of x 
 #define SDRGPU_1P_ABL 0   // (ablation builds, wrong results, timing only) 1: no loads, 2: no transforms, 4: no VFO,
                           // 8: fp32 stage-1 twiddles, 16: no dB / stores
 #endif
+// The ring's first k1pSlots - 1 row sets are issued before the VFO half, so they land while it computes
+// (C5 group 1.518 -> 1.499 ms, same bits, r6g; A/B builds: 0)
+#ifndef SDRGPU_1P_EARLYDMA
+#define SDRGPU_1P_EARLYDMA 1
+#endif
 #ifdef SDRGPU_1P_TIMING   // (measurement builds) per-workgroup phase stamps of wave 0
 __device__ unsigned long long g_1p_t[16384 * 8];
 #define T1P(k)                                                                                    \
@@ -923,7 +928,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
     // the frame's first reader (HBM): half of the VFO's stage 1. (Measured and rejected, r5: the VFO
     // inside the row loop -- from the LDS ring, 1.91 ms; as two batches of segments right after the
     // ring fetched their lines, 1.60 ms; after the loop / between the transforms, spilled)
-    if constexpr (VFO && !(SDRGPU_1P_ABL & 4)) vfo_half_block(v, f, p);
+    constexpr bool kDma = !PAD && !(SDRGPU_1P_ABL & 1);   // whole frames: the LDS-DMA row ring below
+    constexpr bool kVfo = VFO && !(SDRGPU_1P_ABL & 4);
+    if constexpr (kVfo && !(kDma && SDRGPU_1P_EARLYDMA)) vfo_half_block(v, f, p);
     T1P(1);
     // Index arithmetic is recomputed from a laundered thread index where it is used: left alone, the
     // compiler hoists the loop-invariant load / LDS / store addresses and spills them.
@@ -1044,6 +1051,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             }
         };
         static_for<0, S - 1>(dma);
+        if constexpr (kVfo && SDRGPU_1P_EARLYDMA) vfo_half_block(v, f, p);   // (its loads wait behind the ring's)
         static_for<0, 32>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             constexpr int younger = (S - 2 < 31 - i) ? S - 2 : 31 - i;   // row sets issued after i, in flight
@@ -1110,6 +1118,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             }
         }
         __syncthreads();
+        if constexpr (h == 0) T1P(5);
         {   // stage 2: (k2, t0) = (t >> 4, t & 15)
             const int t = tid();
             const int k2 = t >> 4, t0 = t & 15;
@@ -1126,6 +1135,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             for (int q1 = 0; q1 < 32; q1++) dst[17 * q1] = a[q1];
         }
         __syncthreads();
+        T1P(6 + h);
         // stage 3: (k2, q1) = (e & 31, e >> 5), e = t, t + 512. The thread holds the same (k2, q1) bins
         // of both quarters, so quarter r0 + 1 stores (dA, dB) at float 4 (k2 + 32 q1 + 1024 q2) + r0
         // (8-byte aligned: r0 even) through a buffer resource, the q2 step in soffset

@@ -35,10 +35,15 @@ n = 16384 * 8
 buf = (ctypes.c_ulonglong * n)()
 assert sdrpp_amd.lib.sdrgpu_debug_1p_times(buf, n) == 0
 wgs = 2 * frames
-t = np.frombuffer(buf, dtype=np.uint64).reshape(16384, 8).astype(np.int64)[:wgs, :5]
+t8 = np.frombuffer(buf, dtype=np.uint64).reshape(16384, 8).astype(np.int64)[:wgs]
+t = t8[:, :5]
 d = np.diff(t, axis=1)
 names = ["vfo", "loads", "transform_p", "transform_p2"]
+# stamps 5-7 (after the first quarter's stage-1 finish, after each quarter's stage 2): the transforms by stage
+o = t8[:, [2, 5, 6, 3, 7, 4]]
+stages = ["q0_stage1", "q0_stage2", "q0_stage3_db", "q1_stage1_2", "q1_stage3_db_stores"]
 out = {"workgroups": wgs, "vfo": not novfo, "mean_units": {k: round(float(d[:, i].mean())) for i, k in enumerate(names)},
+       "transform_stages": {k: round(float(np.diff(o, axis=1)[:, i].mean())) for i, k in enumerate(stages)},
        "mean_total": round(float((t[:, 4] - t[:, 0]).mean())),
        "span": float(t[:, 4].max() - t[:, 0].min()),
        "note": "s_memtime units (clock64); ratios between phases are what matter"}
