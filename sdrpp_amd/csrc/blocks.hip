@@ -587,17 +587,23 @@ __global__ __launch_bounds__(WFM_TM) void wfm_short_kernel(
 }
 
 // BroadcastFM mono for big calls (C5: 1,048,576 samples at 240 kS/s per step): the same fused form
-// with 2,048 outputs per workgroup and 8 per thread. The quadrature values of the window go to LDS in
-// fir_tail's row layout (element e at row e mod 8, column e / 8: a thread's 8-output register window
-// reads consecutive columns, conflict-free), then each thread runs its 8 fmaf chains over the padded
-// taps in tap order (fir_kernel at D = 1): one LDS read per 8 FMAs and no quadrature round trip
-// through HBM (quad_kernel + fir_kernel<float, float, 4>: 5.3 + 15.6 us per C5 step, r5m).
-constexpr int WFM_BK = 8, WFM_BNT = 256, WFM_BCH = WFM_BK * WFM_BNT;
+// with K = 4 outputs per thread (1,024 per workgroup). The quadrature values of the window go to LDS in
+// fir_tail's row layout (element e at row e mod K, column e / K: a thread's K-output register window
+// reads consecutive columns, conflict-free), rows r and r + K/2 interleaved as float pairs, so the
+// thread's outputs i and i + K / 2 run as one packed fp32 FMA (v_pk_fma_f32; each lane is the fmaf of the
+// scalar chain, same bits) over the padded taps in tap order (fir_kernel at D = 1): the window pair of
+// outputs (i, i + K/2) at tap u is rows ((i + u) mod K, (i + u + K/2) mod K), one stored pair, swapped
+// (op_sel) when (i + u) mod K >= K/2. No quadrature round trip through HBM (quad_kernel +
+// fir_kernel<float, float, 4>: 5.3 + 15.6 us per C5 step, r5m; scalar chains in this kernel 15.7 us).
+#ifndef SDRGPU_WFM_BK
+#define SDRGPU_WFM_BK 4   // outputs per thread (r6o: 14.6 vs 15.1 us per C5 step at 8, same bits; A/B builds: 8)
+#endif
+constexpr int WFM_BK = SDRGPU_WFM_BK, WFM_BNT = 256, WFM_BCH = WFM_BK * WFM_BNT;
 __global__ __launch_bounds__(WFM_BNT) void wfm_big_kernel(
     const float2* __restrict__ in, int count, const float2* __restrict__ din, float2* __restrict__ dinNext,
     const float* __restrict__ hist, float* __restrict__ histNext, const float* __restrict__ taps, int Q, int H,
     float invDev, float2* __restrict__ out) {
-    extern __shared__ float X[];
+    extern __shared__ __attribute__((aligned(16))) float X[];
     constexpr int K = WFM_BK;
     const int tid = threadIdx.x;
     auto qv = [&](long long b) -> float {   // [hist || quad(in)][b], zero past the end
@@ -614,6 +620,8 @@ __global__ __launch_bounds__(WFM_BNT) void wfm_big_kernel(
     const long long m0 = (long long)blockIdx.x * WFM_BCH;
     const int RSK = WFM_BNT + Q / K + 2;   // columns per row (Q is a multiple of 8, <= 256: host-checked)
     float* T = X + K * RSK;                // the taps
+    const f2v* P = reinterpret_cast<const f2v*>(X);   // P[r * RSK + c] = (row r, row r + K/2) at column c, r < K/2
+    auto at = [&](int j) { return 2 * ((j % (K / 2)) * RSK + j / K) + (j / (K / 2)) % 2; };   // float index of element j
     for (int q = tid; q < Q; q += WFM_BNT) T[q] = taps[q];
     // the window [m0, m0 + K RSK) of [hist || quad(in)]: interior workgroups issue all their sample
     // loads at once (one memory round trip), the first and last take the element-wise path
@@ -631,43 +639,55 @@ __global__ __launch_bounds__(WFM_BNT) void wfm_big_kernel(
 #pragma unroll
         for (int k = 0; k < NF; k++) {
             const int j = tid + k * WFM_BNT;
-            if (j < K * RSK) X[(j & (K - 1)) * RSK + (j >> 3)] = quad_value(y[k], yp[k], invDev);
+            if (j < K * RSK) X[at(j)] = quad_value(y[k], yp[k], invDev);
         }
     } else {
-        for (int j = tid; j < K * RSK; j += WFM_BNT) X[(j & (K - 1)) * RSK + (j >> 3)] = qv(m0 + j);
+        for (int j = tid; j < K * RSK; j += WFM_BNT) X[at(j)] = qv(m0 + j);
     }
     __syncthreads();
-    float acc[K], w[K];
+    f2v acc[K / 2], w[K / 2];   // acc[i] = outputs (i, i + K/2); w[r] = window rows (r, r + K/2)
 #pragma unroll
-    for (int i = 0; i < K; i++) {
-        acc[i] = 0.0f;
-        w[i] = X[i * RSK + tid];
+    for (int i = 0; i < K / 2; i++) {
+        acc[i] = f2v{0.f, 0.f};
+        w[i] = P[i * RSK + tid];
     }
     for (int q0 = 0; q0 < Q; q0 += K) {
-        float hv[K], nx[K];
+        float hv[K];
+        f2v nx[K / 2];
 #pragma unroll
         for (int u = 0; u < K; u++) hv[u] = T[q0 + u];   // (LDS broadcasts)
 #pragma unroll
-        for (int u = 0; u < K; u++) nx[u] = X[u * RSK + tid + 1 + q0 / K];
+        for (int r = 0; r < K / 2; r++) nx[r] = P[r * RSK + tid + 1 + q0 / K];
 #pragma unroll
         for (int u = 0; u < K; u++) {
 #pragma unroll
-            for (int i = 0; i < K; i++) acc[i] = fmaf(w[(i + u) % K], hv[u], acc[i]);
-            w[u] = nx[u];
+            for (int i = 0; i < K / 2; i++) {
+                const int r = (i + u) % K;
+                const f2v x = r < K / 2 ? w[r] : __builtin_shufflevector(w[r - K / 2], w[r - K / 2], 1, 0);
+                acc[i] = __builtin_elementwise_fma(x, f2v{hv[u], hv[u]}, acc[i]);
+            }
+            if (u < K / 2) w[u].x = nx[u].x;   // row u slides to the next column
+            else w[u - K / 2].y = nx[u - K / 2].y;
         }
+    }
+    float a[K];
+#pragma unroll
+    for (int i = 0; i < K / 2; i++) {
+        a[i] = acc[i].x;
+        a[i + K / 2] = acc[i].y;
     }
     const long long m = m0 + (long long)tid * K;
     if (m + K <= count) {
         float4* o = reinterpret_cast<float4*>(out + m);   // (out: 8-byte stereo frames; 16-B aligned pairs)
         if (((uintptr_t)out & 15) == 0) {
 #pragma unroll
-            for (int i = 0; i < K; i += 2) o[i / 2] = make_float4(acc[i], acc[i], acc[i + 1], acc[i + 1]);
+            for (int i = 0; i < K; i += 2) o[i / 2] = make_float4(a[i], a[i], a[i + 1], a[i + 1]);
             return;
         }
     }
 #pragma unroll
     for (int i = 0; i < K; i++)
-        if (m + i < count) out[m + i] = make_float2(acc[i], acc[i]);
+        if (m + i < count) out[m + i] = make_float2(a[i], a[i]);
 }
 
 template <int K, int NT>

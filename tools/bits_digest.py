@@ -3,7 +3,7 @@
 
   python tools/bits_digest.py            -> one JSON line {case: sha256[:16]}
 
-Cases: RxVFO (C5: 61.44 MHz -> 240 kHz) over ragged host calls; the C5 launch group (spectrum rows,
+Cases: RxVFO (C5: 61.44 MHz -> 240 kHz) over ragged host calls; BroadcastFM mono on one big call; the C5 launch group (spectrum rows,
 zoom rows, VFO stage-1 + later stages) over 24 frames; the standalone spectrum over 24 frames."""
 import hashlib
 import json
@@ -41,6 +41,8 @@ def main():
     out["c5_rows"] = h(rows.cpu().numpy())
     out["c5_zoom"] = h(zoom.cpu().numpy())
     out["c5_vfo"] = h(vo[:2 * m].cpu().numpy())
+    w = dsp.BroadcastFM(100000, 240000, True)   # a 1,048,576-sample call: wfm_big_kernel
+    out["wfm_big"] = h(w.process(x[:1 << 20]).view(np.uint32))
     r2 = torch.empty(F * N, device="cuda")
     dsp.FFTSpectrum(N, N, 6).execute_dev(d_x.data_ptr(), N, F, r2.data_ptr())
     torch.cuda.synchronize()
