@@ -78,16 +78,19 @@ class C5:
         self.zoom_count = self.frames * self.ZW
         self.bytes_per_sample = 8 + 4 + 4 / 32 + 8 / 256 + 8 / 256   # SURVEY 8(d) C5 (~12.06 B) + the zoom rows
         if self.fuse:
-            # the group: 8 B in (read once), 4 B dB + 4/32 B zoom rows out, 8/32 B VFO stage-1 out
-            self.kernel_bytes = (12.0 + 4 / 32 + 8 / 32) * self.B
-            self.kernel_name = ("spectrum N=65536 + zoom to 2048 + RxVFO stage 1 (D=32, 143 taps, xlator): "
+            # the group: 8 B in (read once), 4 B dB out, 8/32 B VFO stage-1 out (the zoom rows are folded
+            # from the group's per-workgroup partial maxima in the VFO tail's launch, fft_1p_tail_fold_kernel)
+            self.kernel_bytes = (12.0 + 8 / 32) * self.B
+            self.kernel_name = ("spectrum N=65536 + zoom partials + RxVFO stage 1 (D=32, 143 taps, xlator): "
                                 "fft_1p_kernel<zoom,vfo,false> (one pass: two workgroups per frame, each half the "
                                 "VFO stage-1 outputs, then two adjacent 16k radix-4 DIF sub-transforms in LDS; the "
-                                "rows stream in by LDS-DMA) + fft_1p_zoom_kernel (folds the two zoom partials)")
+                                "rows stream in by LDS-DMA)")
             self.fft.set_timing(True)   # the group's own HIP events (the VFO's later stages are outside it)
             self.roofline_note = ("the group includes the VFO's first stage (8 B/sample of input it shares with "
-                                  "the spectrum); round 4's two-pass group (fft_vfo_kernel, SDRGPU_FFT_1P=0) took "
-                                  "1.63 ms for the same work, round 3's spectrum + separate stage 1.778 ms")
+                                  "the spectrum); the zoom fold (folding the two workgroups' partial maxima into "
+                                  "the 2048-column rows) runs beside the VFO's later stages in one launch after "
+                                  "the group; round 4's two-pass group (fft_vfo_kernel, SDRGPU_FFT_1P=0) took "
+                                  "1.63 ms for the spectrum + zoom + stage 1, round 3's spectrum + separate stage 1.778 ms")
         else:
             self.kernel_bytes = (12.0 + 4 / 32) * self.B            # spectrum: 8 B in, 4 B dB + 4/32 B zoom out
             self.kernel_name = ("spectrum N=65536 + zoom to 2048: fft_passA_kernel<256,32> (chunk 0) + "

@@ -1204,8 +1204,8 @@ extern "C" int sdrgpu_debug_1p_times(unsigned long long* host, int n) {
 
 // zoom[f][o] = max over the two workgroups' partial maxima (fft_1p_kernel's ZM): 4 columns per thread
 // as 16-B loads / stores (one element per thread took 20.8 us per 2^28-sample step)
-__global__ __launch_bounds__(256) void fft_1p_zoom_kernel(const float* __restrict__ zpart, int frames, float* __restrict__ zoom) {
-    const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+__device__ __forceinline__ void zoom_fold_block(const float* __restrict__ zpart, int frames, float* __restrict__ zoom, int blk) {
+    const long long i = ((long long)blk * 256 + threadIdx.x) * 4;
     if (i >= (long long)frames * 2048) return;
     const long long f = i >> 11, o = i & 2047;
     const float4 a = *reinterpret_cast<const float4*>(zpart + (f << 13) + o);
@@ -1216,6 +1216,21 @@ __global__ __launch_bounds__(256) void fft_1p_zoom_kernel(const float* __restric
     } else {
         zoom[i] = m.x; zoom[i + 1] = m.y; zoom[i + 2] = m.z; zoom[i + 3] = m.w;
     }
+}
+__global__ __launch_bounds__(256) void fft_1p_zoom_kernel(const float* __restrict__ zpart, int frames, float* __restrict__ zoom) {
+    zoom_fold_block(zpart, frames, zoom, blockIdx.x);
+}
+// The VFO's later stages (fir_tail_kernel's workgroups, first) and the zoom fold (the rest) in one launch:
+// the tail is latency-bound (dependent fmaf chains, barriers between stages), the fold moves 96 MB per C5
+// step, so the fold's workgroups fill the CUs the tail leaves idle (both need only the one-pass
+// launch's outputs). Same code, same bits as the two launches.
+__global__ __launch_bounds__(TAIL_NT_BIG) void fft_1p_tail_fold_kernel(TailArgs t, const float* __restrict__ zpart, int frames,
+                                                                         float* __restrict__ zoom) {
+    extern __shared__ __attribute__((aligned(16))) float2 XS[];
+    __shared__ TailGeom gs[TAIL_MAXS];
+    const int w = blockIdx.x;
+    if (w < t.G) fir_tail_block<TAIL_K_BIG, TAIL_NT_BIG>(t, w, w == t.G - 1, XS, gs);
+    else zoom_fold_block(zpart, frames, zoom, w - t.G);
 }
 
 // ---- the front end's per-block launch: pass A (frame straddling two pushes read in place) + the
@@ -1664,7 +1679,7 @@ static bool zoom_fusable(const FftPlan& p, int zoomSize) {
 // blocks of 8 frames, + the VFO stage's history workgroup
 template <bool ZM, bool VFO>
 static int launch_1p(FftPlan& p, const float2* in, long long stride, int frames, float* out, float* zoom, VfoWork v,
-                     hipStream_t s) {
+                     hipStream_t s, bool fold = true) {
     // LDS-DMA rows need whole frames, an even frame stride and a 16-B aligned base (16-B pieces);
     // anything else streams through the range-checked register ring
     const bool pad = p.nz < 65536 || (stride & 1) || ((uintptr_t)in & 15);
@@ -1675,7 +1690,7 @@ static int launch_1p(FftPlan& p, const float2* in, long long stride, int frames,
     hipLaunchKernelGGL(k, dim3(g), dim3(512), op1::LDS_BYTES, s, in, stride, frames, p.win.as<float>(), p.nz,
                        p.tab1p.as<float2>(), p.tab1p64.as<double2>(), out, ZM ? p.zpart.as<float>() : nullptr, v);
     SDRGPU_HIP(hipGetLastError());
-    if (ZM) {
+    if (ZM && fold) {
         const long long n = (long long)frames * 2048 / 4;
         hipLaunchKernelGGL(fft_1p_zoom_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p.zpart.as<float>(),
                            frames, zoom);
@@ -1900,11 +1915,25 @@ static int fft_execute_vfo(FftPlan& p, const float2* x, int frames, float* out, 
                            sdrgpu_block* vfo, void* vfoOut, hipStream_t s) {
     if (onepass_ok(p, frames)) {
         VfoWork v{st.a, 0, 1};
+        // with zoom rows and a big-call tail, the zoom fold rides in the tail's launch
+        TailArgs t;
+        size_t ldsTail = 0;
+        int tail = zoom ? vfo_tail_prepare(vfo, st, vfoOut, &t, &ldsTail) : 0;
+        if (tail < 0) return tail;
+        if (tail && (t.NT != TAIL_NT_BIG || t.K != TAIL_K_BIG)) tail = 0;
         SDRGPU_CHECK(time_mark(p, 0, s));
-        const int rc = zoom ? launch_1p<true, true>(p, x, p.N, frames, out, zoom, v, s)
+        const int rc = zoom ? launch_1p<true, true>(p, x, p.N, frames, out, zoom, v, s, !tail)
                             : launch_1p<false, true>(p, x, p.N, frames, out, nullptr, v, s);
         if (rc < 0) return rc;
         SDRGPU_CHECK(time_mark(p, 1, s));
+        if (tail) {
+            auto k = fft_1p_tail_fold_kernel;
+            SDRGPU_CHECK(set_lds(k, ldsTail));
+            const int nz = (int)(((long long)frames * 2048 / 4 + 255) / 256);
+            hipLaunchKernelGGL(k, dim3(t.G + nz), dim3(TAIL_NT_BIG), ldsTail, s, t, p.zpart.as<float>(), frames, zoom);
+            SDRGPU_HIP(hipGetLastError());
+            return vfo_tail_commit(vfo, st, t);
+        }
         return vfo_stage1_finish(vfo, st, vfoOut, s);
     }
     const int cf = p.chunkFrames;
