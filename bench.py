@@ -14,30 +14,23 @@ A step = one batch of B synthetic complex-float IQ samples resident in HBM
 nz = 1e6, zero-padded), c3 (xlator + 256-tap FIR /8 + FM quadrature, fused), c4 (1024-channel
 polyphase channelizer, 16384-tap prototype).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
+Launch: python bench.py [--gpus N --steps K --warmup W]. N > 1 either under torch.distributed.run
+(WORLD_SIZE must equal N) or directly: the parent then starts N rank processes itself before anything
+touches the GPU (launch_ranks) and exits with the first failing rank's status.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
-import sdrpp_amd  # noqa: E402
-from sdrpp_amd import dsp  # noqa: E402
-from sdrpp_amd.multistream import CudaGather, GatherPipeline, StreamShard  # noqa: E402
-
-METRIC = "IQ Msamples/s through FFT+FIR+demod chain; % HBM roofline at 1/2/4/8 GPU"
-HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
-
-
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -49,7 +42,93 @@ def parse():
     ap.add_argument("--no-sub", action="store_true", help="time only --config (no C2/C3/C4 sub-objects)")
     ap.add_argument("--no-ulp", action="store_true", help="skip the live spectrum ulp report (profiling runs: "
                     "only the timed config's kernels run)")
-    return ap.parse_args()
+    ap.add_argument("--runtime", default="hip", choices=["hip", "cpu-rehearsal"],
+                    help="cpu-rehearsal: the same launch / gather / timing control flow on the CPU over gloo with a "
+                         "C5-shaped CPU stand-in workload (tests only; its line says so and is no measurement)")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, grace_s=None):
+    """The parent of an N-GPU run started as `python bench.py --gpus N` (no WORLD_SIZE in the env):
+    start N fresh rank processes of this script -- RANK = LOCAL_RANK = r, WORLD_SIZE = N,
+    MASTER_ADDR 127.0.0.1 and a free port, the launcher torch.distributed.run would give them --
+    and wait for them. The parent itself never touches HIP (it has not imported torch or the
+    library when this runs), so the children are the only GPU processes. Rank 0 prints the JSON
+    line on the inherited stdout. When a rank exits non-zero the others get `grace_s` (the gather
+    deadline + 60 s: the survivors end through their own deadline first) and are then killed; the
+    parent exits with the first failing rank's status. (Mirrors the reference's harness running
+    independent block chains side by side, core/src/dsp/bench/speed_tester.h:31-56.)"""
+    if grace_s is None:
+        grace_s = float(os.environ.get("SDRGPU_BENCH_GRACE_S") or
+                        float(os.environ.get("SDRGPU_GATHER_TIMEOUT_S", "120")) + 60.0)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env))
+    first_bad, t_bad = None, None
+    while True:
+        codes = [p.poll() for p in procs]
+        for r, c in enumerate(codes):
+            if c not in (None, 0) and first_bad is None:
+                first_bad, t_bad = (r, c), time.monotonic()
+                print(f"bench.py: rank {r} exited with status {c}; waiting up to {grace_s:.0f} s for the other "
+                      "ranks", file=sys.stderr, flush=True)
+        if all(c is not None for c in codes):
+            break
+        if first_bad is not None and time.monotonic() - t_bad > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            for p in procs:
+                p.wait()
+            break
+        time.sleep(0.05)
+    if first_bad is not None:
+        r, c = first_bad
+        return c if c > 0 else 128 - c   # a signal (-k) as the shell reports it
+    return 0
+
+
+def _launch_or_continue(argv):
+    """Decides, before any GPU-touching import, whether this process is a rank or the parent of N."""
+    a = parse(argv)
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != a.gpus:
+            print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={ws}: refusing to time a different number of GPUs "
+                  "than asked", file=sys.stderr, flush=True)
+            sys.exit(2)
+        return
+    if a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus, argv))
+    if a.gpus < 1:
+        print(f"bench.py: --gpus {a.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
+
+
+if __name__ == "__main__":
+    _launch_or_continue(sys.argv[1:])
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import sdrpp_amd  # noqa: E402
+from sdrpp_amd import dsp  # noqa: E402
+from sdrpp_amd.multistream import CudaGather, GatherPipeline, StreamShard  # noqa: E402
+
+METRIC = "IQ Msamples/s through FFT+FIR+demod chain; % HBM roofline at 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 
 
 class C5:
@@ -387,6 +466,74 @@ class CudaRuntime:
         return CudaGather(shard, dev)
 
 
+class CpuRehearsalRuntime:
+    """`--runtime cpu-rehearsal`: the device side of run_config on the CPU -- torch CPU tensors,
+    perf_counter events and LazyGlooGather (gathers over gloo that run only when their completion is
+    waited for, so a buffer rewritten before its gather ran would ship the wrong rows) in place of
+    torch.cuda streams and libsdrgpu's RCCL gather. Used by tests/test_bench_multirank.py to run the
+    whole `bench.py --gpus 2` path (self-launch, ranks, gather, verification) without a GPU."""
+    reduce_device = None
+
+    class Event:
+        def record(self, stream=None):
+            self.t = time.perf_counter()
+
+        def elapsed_time(self, other):
+            return (other.t - self.t) * 1e3
+
+    def rand(self, n, seed):
+        g = torch.Generator()
+        g.manual_seed(seed)
+        return torch.rand(n, generator=g) * 2 - 1
+
+    def event(self):
+        return self.Event()
+
+    def handle(self, stream):
+        return stream
+
+    def synchronize(self):
+        pass
+
+    def gather_backend(self, shard, dev):
+        from sdrpp_amd.multistream import LazyGlooGather
+        return LazyGlooGather()
+
+
+class C5Rehearsal:
+    """C5's interface on the CPU for the rehearsal runtime: `frames` rows of ZW columns per step, a
+    function of the step's input, this rank's stream (seed) and the step number, so the gather's
+    verification has something to catch. SDRGPU_BENCH_REHEARSAL_DIE="rank:step" makes that rank exit
+    with status 3 at that step (the failure path of the launcher)."""
+    N, ZW = 4096, 64
+
+    def __init__(self, B, shard, dev):
+        self.B = (B // self.N) * self.N
+        self.frames = self.B // self.N
+        self.zoom = [torch.empty(self.frames * self.ZW) for _ in range(2)]
+        self.zoom_count = self.frames * self.ZW
+        self.rank = shard.rank
+        self.k = 0
+        self.bytes_per_sample = 12.0
+        self.kernel_bytes = 12.0 * self.B
+        self.kernel_name = "cpu rehearsal stand-in (no kernel)"
+        self.history = []
+        die = os.environ.get("SDRGPU_BENCH_REHEARSAL_DIE")
+        self.die = tuple(int(v) for v in die.split(":")) if die else None
+
+    def run(self, x, s, timed_call, buf=0):
+        if self.die is not None and self.die == (self.rank, self.k):
+            print(f"bench.py rank {self.rank}: rehearsal failure injected at step {self.k}", file=sys.stderr, flush=True)
+            os._exit(3)
+
+        def body():
+            rows = x[:2 * self.B].view(self.frames, -1)[:, :self.ZW] + 1000.0 * self.rank + self.k
+            self.zoom[buf].copy_(rows.reshape(-1))
+        timed_call(body)
+        self.history.append(self.zoom[buf].clone())
+        self.k += 1
+
+
 def run_config(config, a, shard, dev, stream, rt=None, workloads=None):
     """Time `a.steps` steps of one config on this rank; returns (B, elapsed_s, kernel_ms, wl)."""
     rt = rt or CudaRuntime()
@@ -582,12 +729,12 @@ def per_call_c5(dev, stream, calls=300, block=307200, single_only=False):
                     "synchronous push per block (staging memcpy, H2D, kernels, read-back)"}
 
 
-def config_result(config, a, world, B, elapsed, kern_ms, wl):
+def config_result(config, a, world, B, elapsed, kern_ms, wl, wname=None):
     value = world * B * a.steps / elapsed / 1e6
     achieved = wl.kernel_bytes / (kern_ms * 1e-3) / 1e9
     tps, tsrc = traffic_per_sample(config)
     r = {"value": round(value, 3), "unit": "MS/s", "ms_per_step": round(elapsed / a.steps * 1e3, 4),
-         "workload": WORKLOADS[config], "samples_per_gpu_per_step": B,
+         "workload": wname or WORKLOADS[config], "samples_per_gpu_per_step": B,
          "bytes_per_sample": round(wl.bytes_per_sample, 4),
          "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -604,8 +751,32 @@ def config_result(config, a, world, B, elapsed, kern_ms, wl):
     return r
 
 
+def rehearsal_main(a):
+    """`--runtime cpu-rehearsal`: this rank's run_config over gloo with the CPU stand-in; rank 0
+    prints the line (marked as a rehearsal, with the gather report and this rank's last rows'
+    checksums so a test can check what rank 0 received)."""
+    shard = StreamShard(backend="gloo")
+    world, rank = shard.world, shard.rank
+    B, elapsed, kern_ms, wl = run_config(a.config, a, shard, None, "compute", rt=CpuRehearsalRuntime(),
+                                         workloads={a.config: C5Rehearsal})
+    head = config_result(a.config, a, world, B, elapsed, kern_ms, wl, wname="C5-shaped CPU stand-in")
+    from sdrpp_amd.multistream import row_checksum
+    sums = shard.all_gather_tensor(row_checksum(wl.history[-1]))
+    if rank == 0:
+        out = {"metric": METRIC, "value": head["value"], "unit": "MS/s", "n_gpus": world, "steps": a.steps,
+               "warmup": a.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+               "runtime": "cpu-rehearsal", "data": "cpu-rehearsal: control flow only, not a measurement",
+               "samples_per_rank_per_step": B, "last_rows_checksums": sums.tolist()}
+        if "gather" in head:
+            out["gather"] = head["gather"]
+        print(json.dumps(out), flush=True)
+    shard.close()
+
+
 def main():
     a = parse()
+    if a.runtime == "cpu-rehearsal":
+        return rehearsal_main(a)
     shard = StreamShard(backend="nccl")
     world, rank = shard.world, shard.rank
     if world == 1:

@@ -214,28 +214,34 @@ extern "C" int sdrgpu_gather_rows(sdrgpu_gather* g, const float* rows, long long
     if (!R) return SDRGPU_ESTATE;
     if (g->device >= 0) SDRGPU_SET_DEVICE(g->device);
     hipStream_t s = (hipStream_t)stream;
-    if (g->rank == 0 && g->world > 1) SDRGPU_HIP(hipMemcpyAsync(out, rows, sizeof(float) * count, hipMemcpyDeviceToDevice, s));
     ncclResult_t e = R->groupStart();
     if (e != ncclSuccess) return gather_fail(R, g, SDRGPU_EHIP, "ncclGroupStart", e, false);
-    bool ok = true;
+    // A non-blocking communicator may answer ncclInProgress for a send/recv: that is an operation
+    // accepted into the group, so every peer's operation is still posted after it; only a real error
+    // stops the posting (and aborts the communicator).
+    ncclResult_t bad = ncclSuccess;
+    auto post = [&](ncclResult_t r) {
+        if (r != ncclSuccess && r != ncclInProgress && bad == ncclSuccess) bad = r;
+    };
     if (g->world == 1) {   // one stream: a send/recv to itself (exercises the communicator like world > 1)
-        ok = (e = R->send(rows, (size_t)count, ncclFloat32, 0, g->comm, s)) == ncclSuccess &&
-             (e = R->recv(out, (size_t)count, ncclFloat32, 0, g->comm, s)) == ncclSuccess;
+        post(R->send(rows, (size_t)count, ncclFloat32, 0, g->comm, s));
+        if (bad == ncclSuccess) post(R->recv(out, (size_t)count, ncclFloat32, 0, g->comm, s));
     } else if (g->rank == 0) {
-        for (int r = 1; ok && r < g->world; r++)
-            ok = (e = R->recv(out + (size_t)r * count, (size_t)count, ncclFloat32, r, g->comm, s)) == ncclSuccess;
+        for (int r = 1; bad == ncclSuccess && r < g->world; r++)
+            post(R->recv(out + (size_t)r * count, (size_t)count, ncclFloat32, r, g->comm, s));
     } else {
-        ok = (e = R->send(rows, (size_t)count, ncclFloat32, 0, g->comm, s)) == ncclSuccess;
+        post(R->send(rows, (size_t)count, ncclFloat32, 0, g->comm, s));
     }
-    // a non-blocking communicator may report ncclInProgress for the calls and the group end
-    if (!ok && e != ncclInProgress) {
+    if (bad != ncclSuccess) {
         (void)R->groupEnd();
-        return gather_fail(R, g, SDRGPU_EHIP, "ncclSend/ncclRecv", e, false);
+        return gather_fail(R, g, SDRGPU_EHIP, "ncclSend/ncclRecv", bad, false);
     }
     e = R->groupEnd();
     bool expired = false;
     if (e == ncclInProgress) e = wait_comm(R, g->comm, deadline_after(g->timeout), &expired);
     if (e != ncclSuccess) return gather_fail(R, g, expired ? SDRGPU_ETIMEOUT : SDRGPU_EHIP, "ncclGroupEnd", e, expired);
+    // rank 0's own rows: a device copy on the same stream (independent of the received slots)
+    if (g->rank == 0 && g->world > 1) SDRGPU_HIP(hipMemcpyAsync(out, rows, sizeof(float) * count, hipMemcpyDeviceToDevice, s));
     return SDRGPU_OK;
 }
 

@@ -1,7 +1,8 @@
 /* A stand-in RCCL for tests/test_gather_deadline.py (CPU suite): the C-ABI gather loads it through
  * SDRGPU_RCCL_LIB. Its "peer" never answers: in mode "init" (STUB_RCCL_MODE) the non-blocking
  * communicator never leaves ncclInProgress; in mode "group" init completes but every group end
- * stays in progress. Each call is appended to the file STUB_RCCL_LOG so the test can check that
+ * stays in progress; in mode "post" init and group end complete but every send/recv answers
+ * ncclInProgress (a non-blocking communicator accepting the operation). Each call is appended to the file STUB_RCCL_LOG so the test can check that
  * the library aborted the communicator. Only the symbols libsdrgpu resolves are defined, with the
  * ABI of rccl.h (enums as int, opaque handles as pointers). */
 #include <stdio.h>
@@ -49,10 +50,14 @@ res_t ncclCommGetAsyncError(void* comm, res_t* st) {
 res_t ncclCommAbort(void* comm) { (void)comm; aborted = 1; note("abort"); return OK; }
 res_t ncclCommDestroy(void* comm) { (void)comm; note("destroy"); return OK; }
 res_t ncclSend(const void* b, size_t n, int t, int peer, void* comm, void* s) {
-    (void)b; (void)n; (void)t; (void)peer; (void)comm; (void)s; note("send"); return OK;
+    (void)b; (void)n; (void)t; (void)peer; (void)comm; (void)s; note("send"); return mode_is("post") ? IN_PROGRESS : OK;
 }
 res_t ncclRecv(void* b, size_t n, int t, int peer, void* comm, void* s) {
-    (void)b; (void)n; (void)t; (void)peer; (void)comm; (void)s; note("recv"); return OK;
+    (void)b; (void)n; (void)t; (void)peer; (void)comm; (void)s;
+    char w[32];
+    snprintf(w, sizeof(w), "recv%d", peer);
+    note(w);
+    return mode_is("post") ? IN_PROGRESS : OK;
 }
 res_t ncclGroupStart(void) { note("groupStart"); return OK; }
 res_t ncclGroupEnd(void) {

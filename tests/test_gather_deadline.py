@@ -88,3 +88,31 @@ def test_gather_after_abort_refuses(stub, tmp_path):
     assert float(secs) < 0.5 and "sdrgpu error -4" in msg and "aborted" in msg, out[-1]
     calls = log.read_text().split()
     assert calls.count("abort") == 1 and calls.count("groupEnd") == 1 and "destroy" not in calls, calls
+
+
+def test_gather_posts_every_peer_when_ops_in_progress(stub, tmp_path):
+    """A non-blocking communicator may answer ncclInProgress for each send/recv: that is
+    an accepted operation, so rank 0 of 3 must still post the receive from every peer (ranks 1 and
+    2) before the group end, and no abort follows. (The rank-0 self copy after the group needs a
+    device; on this CPU host it fails after the group, which is not what is checked here.)"""
+    log = tmp_path / "calls.log"
+    code = textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {ROOT!r})
+        import sdrpp_amd
+        from sdrpp_amd import dsp
+        g = dsp.SpectraGather(0, 3, dsp.gather_id(), device=-1)
+        try:
+            g.gather_dev(0x1000, 16, 0x2000, 0)
+        except sdrpp_amd.SdrGpuError as e:
+            print("ERR", e)
+    """)
+    env = dict(os.environ, SDRGPU_RCCL_LIB=stub, STUB_RCCL_MODE="post", STUB_RCCL_LOG=str(log),
+               SDRGPU_GATHER_TIMEOUT_S="2.0")
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "ncclSend/ncclRecv" not in p.stdout, p.stdout
+    calls = log.read_text().split()
+    g0 = calls.index("groupStart")
+    assert calls[g0 + 1:g0 + 4] == ["recv1", "recv2", "groupEnd"], calls
+    assert "abort" not in calls, calls
