@@ -320,6 +320,8 @@ def cpu_baseline(config, seconds, bytes_per_sample=None):
     h = r["host"]
     out = {"value": round(r["value_all_cores"], 3), "unit": "MS/s", "cores": r["cores_all"], "kind": "port",
            "cores_source": r["cores_source"], "value_1core": round(r["value_1core"], 3),
+           "value_1core_basis": (f"max(1-core run on CPU {r['value_1core_cpu']}: {r['value_1core_run']:.2f}, spread "
+                                 f"streams' per-stream mean: {r['value_1core_spread_mean']:.2f})"),
            "value_packed": round(r["value_all_cores_packed"], 3), "value_spread": round(r["value_all_cores_spread"], 3),
            "placement": r["placement"],
            "sample": f"{r['variant']}: {r['cores_all']} independent streams x {seconds:.0f} s (all-core aggregate, the "

@@ -126,6 +126,18 @@ int sdrgpu_fft_size(sdrgpu_fft* h);
  * device; the zoom rows of sdrgpu_fft_execute_zoom_dev are then computed unfused. */
 int sdrgpu_fft_set_precision(sdrgpu_fft* h, int mode);
 int sdrgpu_fft_get_precision(sdrgpu_fft* h);
+/* 64k transform form (not in the reference; FFTW picks its plan per size the same way). The 64k
+ * plan has two fp32 kernels that round differently: the one-pass transform (one radix-4 DIF step
+ * into four 16k sub-transforms, fft_1p_kernel) and the two-pass 256 x 256 four-step launches. Both
+ * meet the spectrum parity bar against the exact DFT, but they are not bit-identical to each other:
+ * rows of the same frame differ by at most 0.05 dB anywhere and 1e-3 dB within 60 dB of the frame's
+ * peak (tests/test_gpu_parity.py::test_spectrum_64k_rows_vs_call_size). mode 2 (the default) picks
+ * per call: one-pass for calls of >= 64 frames, two-pass below (a reference-size block of 4.7
+ * frames runs faster there), so a stream's 64k rows then depend on how it is batched into calls.
+ * mode 1 (always one-pass) or 0 (always two-pass) pins the form per plan: rows then depend only on
+ * the frame. Other sizes have one form and ignore the mode. The device front end
+ * (sdrgpu_frontend_*) pins its plans to 0. Returns the previous mode. */
+int sdrgpu_fft_set_kernel(sdrgpu_fft* h, int mode);
 int sdrgpu_fft_destroy(sdrgpu_fft* h);
 
 /* ---------------------------------------------------- stream blocks ---- */

@@ -426,6 +426,9 @@ __global__ __launch_bounds__(S / 2 * L / 16) void fft_passA2_kernel(
 // traffic). Measured alternatives (rounds 2-4; kept in git history, not here): 8-column
 // tiles (2.24-2.70 ms), spill-free laundered offsets (same time), the merged pass-B(c-1) + pass-A(c)
 // launches (1.80 vs 1.73 ms), two workgroups per CU (2.16 ms).
+#ifndef SDRGPU_1M_TW64
+#define SDRGPU_1M_TW64 0
+#endif
 __device__ __forceinline__ double2 zmul(double2 a, double2 b) {
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
@@ -606,8 +609,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         unsigned vo = (unsigned)(b * L * S + t * S + 2 * cp) * 8u;
 #pragma unroll
         for (int m = 0; m < 16; m++) {
+#if SDRGPU_1M_TW64   // (accuracy A/B builds) the four-step twiddle product in fp64, one rounding
+            const double2 ad = zmul(make_double2(y[0][m].x, y[0][m].y), cur[0]);
+            const double2 cd = zmul(make_double2(y[1][m].x, y[1][m].y), cur[1]);
+            const float2 a = make_float2((float)ad.x, (float)ad.y), c = make_float2((float)cd.x, (float)cd.y);
+#else
             const float2 a = cmul(y[0][m], make_float2((float)cur[0].x, (float)cur[0].y));
             const float2 c = cmul(y[1][m], make_float2((float)cur[1].x, (float)cur[1].y));
+#endif
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bu4, make_float4(a.x, a.y, c.x, c.y)), rs, vo, 0, 0);
             vo += (unsigned)(T * S * 8);
             asm volatile("" : "+v"(vo));
@@ -809,6 +818,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
 }
 
 // ---- one-pass 64k spectrum: no intermediate leaves the CU ----------------------------------------
+#ifndef SDRGPU_1P_TW64
+#define SDRGPU_1P_TW64 0   // (accuracy A/B builds) 1: stage-1 twiddle products in fp64 (one rounding), 2: stage-2
+                           // W_512 products in fp64 from an fp64 LDS table
+#endif
 // N = 65536 as four 16,384-point transforms (one radix-4 decimation-in-frequency step). Item (f, r)
 // computes the bins 4 m + r of frame f:
 //   X[4 m + r] = sum_{n < M} W_M^(n m) y_r[n],   y_r[n] = W_N^(n r) sum_{j < 4} W_4^(j r) w[n + M j] x[n + M j],
@@ -835,9 +848,10 @@ constexpr int RS = 560;                 // LDS row stride (float2)
 constexpr int TW512 = 32 * RS;          // W_512^(t0 q1) at [q1][t0]
 constexpr int W128 = TW512 + 512;       // W_128^(r i), i < 32
 constexpr int W128D = (W128 + 64) * 8;   // (bytes) fp64 W_128^(r i), r = r0, r0 + 1, i < 32
-constexpr int LDS_BYTES = W128D + 64 * 16;
+constexpr int W512D = W128D + 64 * 16;   // (bytes) fp64 W_512^(t0 q1) at [q1][t0] (SDRGPU_1P_TW64 & 2)
+constexpr int LDS_BYTES = W512D + ((SDRGPU_1P_TW64 & 2) ? 512 * 16 : 0);
 constexpr int TAB = 512 + 128;          // device table: [q1][t0] W_512^(t0 q1), [r][i] W_128^(r i)
-constexpr int TAB64 = 2048 + 128;       // fp64 table: W_N^m (m < 2048), [r][i] W_128^(r i)
+constexpr int TAB64 = 2048 + 128 + 512; // fp64 table: W_N^m (m < 2048), [r][i] W_128^(r i), [q1][t0] W_512^(t0 q1)
 }
 
 // x w, rounded on its own: never contracted into the radix-4 adds that follow (left to the compiler,
@@ -943,6 +957,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         const int t = threadIdx.x;
         lds[TW512 + t] = tab[t];
         if (t < 64) reinterpret_cast<double2*>(reinterpret_cast<char*>(lds) + op1::W128D)[t] = tab64[2048 + 32 * (r0 + (t >> 5)) + (t & 31)];
+        if constexpr (SDRGPU_1P_TW64 & 2) reinterpret_cast<double2*>(reinterpret_cast<char*>(lds) + op1::W512D)[t] = tab64[2176 + t];
     }
     // stage 1: y_r for r = r0 (even) and r0 + 1 (odd) from the four quarters: y_r = A_r + W_4^r q_r with
     // A_r = u0 + s_r u2, q_r = u1 + s_r u3, s_r = (-1)^r; W_4^r in {1, -i, -1, i} as (fx, fy), one of
@@ -1073,7 +1088,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         });
     }
     T1P(2);
-    float* zf = ZM ? zpart + ((long long)f << 13) : nullptr;
+    float* zf = ZM ? zpart + ((long long)f << 12) : nullptr;   // [f][workgroup][2048]
     const __amdgpu_buffer_rsrc_t ro = brsrc(out + ((long long)f << 16), 65536u * 4u);
     // the 16k transform of quarter r = r0 + h from its stage-1 registers z. Quarter r0's dB values wait in
     // registers (dA) for quarter r0 + 1's, and the two leave as one 8-byte store per bin pair.
@@ -1106,6 +1121,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
                 const float2 cf = make_float2((float)ce.x, (float)ce.y), sf = make_float2((float)st.x, (float)st.y);
 #pragma unroll
                 for (int k2 = 0; k2 < 32; k2++) row[k2 * RS] = cmul(z[k2], k2 & 1 ? sf : cf);
+            } else if constexpr (SDRGPU_1P_TW64 & 1) {
+#pragma unroll
+                for (int k2 = 0; k2 < 32; k2 += 2) {
+                    const double2 qe = zmul(make_double2(z[k2].x, z[k2].y), ce);
+                    const double2 qo = zmul(make_double2(z[k2 + 1].x, z[k2 + 1].y), co);
+                    row[k2 * RS] = make_float2((float)qe.x, (float)qe.y);
+                    row[(k2 + 1) * RS] = make_float2((float)qo.x, (float)qo.y);
+                    if (k2 < 30) {
+                        ce = zmul(ce, st2);
+                        co = zmul(co, st2);
+                    }
+                }
             } else
 #pragma unroll
             for (int k2 = 0; k2 < 32; k2 += 2) {
@@ -1127,8 +1154,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
 #pragma unroll
             for (int t1 = 0; t1 < 32; t1++) a[t1] = src[17 * t1];
             dft32(a);
+            if constexpr (SDRGPU_1P_TW64 & 2) {
+                const double2* w512 = reinterpret_cast<const double2*>(reinterpret_cast<const char*>(lds) + op1::W512D);
 #pragma unroll
-            for (int q1 = 1; q1 < 32; q1++) a[q1] = cmul(a[q1], lds[TW512 + 16 * q1 + t0]);
+                for (int q1 = 1; q1 < 32; q1++) {
+                    const double2 q = zmul(make_double2(a[q1].x, a[q1].y), w512[16 * q1 + t0]);
+                    a[q1] = make_float2((float)q.x, (float)q.y);
+                }
+            } else {
+#pragma unroll
+                for (int q1 = 1; q1 < 32; q1++) a[q1] = cmul(a[q1], lds[TW512 + 16 * q1 + t0]);
+            }
             __syncthreads();
             float2* dst = lds + k2 * RS + (t0 ^ ((k2 >> 1) & 15));
 #pragma unroll
@@ -1203,13 +1239,15 @@ extern "C" int sdrgpu_debug_1p_times(unsigned long long* host, int n) {
 #endif
 
 // zoom[f][o] = max over the two workgroups' partial maxima (fft_1p_kernel's ZM): 4 columns per thread
-// as 16-B loads / stores (one element per thread took 20.8 us per 2^28-sample step)
+// as 16-B loads / stores (one element per thread took 20.8 us per 2^28-sample step); 256 threads per
+// workgroup (both launches below)
+static_assert(TAIL_NT_BIG == 256, "zoom_fold_block's indexing and the fold's block count assume 256 threads");
 __device__ __forceinline__ void zoom_fold_block(const float* __restrict__ zpart, int frames, float* __restrict__ zoom, int blk) {
     const long long i = ((long long)blk * 256 + threadIdx.x) * 4;
     if (i >= (long long)frames * 2048) return;
     const long long f = i >> 11, o = i & 2047;
-    const float4 a = *reinterpret_cast<const float4*>(zpart + (f << 13) + o);
-    const float4 b = *reinterpret_cast<const float4*>(zpart + (f << 13) + 2048 + o);
+    const float4 a = *reinterpret_cast<const float4*>(zpart + (f << 12) + o);
+    const float4 b = *reinterpret_cast<const float4*>(zpart + (f << 12) + 2048 + o);
     const float4 m = make_float4(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w));
     if (((uintptr_t)zoom & 15) == 0) {   // (wave-uniform)
         *reinterpret_cast<float4*>(zoom + i) = m;
@@ -1592,6 +1630,8 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
             for (int m = 0; m < 2048; m++) t64[m] = w64(m);
             for (int r = 0; r < 4; r++)
                 for (int i = 0; i < 32; i++) t64[2048 + 32 * r + i] = w64(512LL * r * i);
+            for (int q1 = 0; q1 < 32; q1++)
+                for (int t0 = 0; t0 < 16; t0++) t64[2176 + 16 * q1 + t0] = w64(128LL * t0 * q1);
             rc = p.tab1p.ensure(sizeof(float2) * t.size());
             if (rc >= 0) rc = p.tab1p64.ensure(sizeof(double2) * t64.size());
             if (rc >= 0 && (hipMemcpy(p.tab1p.p, t.data(), sizeof(float2) * t.size(), hipMemcpyHostToDevice) != hipSuccess ||
@@ -1685,7 +1725,7 @@ static int launch_1p(FftPlan& p, const float2* in, long long stride, int frames,
     const bool pad = p.nz < 65536 || (stride & 1) || ((uintptr_t)in & 15);
     auto k = pad ? fft_1p_kernel<ZM, VFO, true> : fft_1p_kernel<ZM, VFO, false>;
     SDRGPU_CHECK(set_lds(k, op1::LDS_BYTES));
-    if (ZM) SDRGPU_CHECK(p.zpart.ensure(sizeof(float) * 4 * 2048 * (size_t)frames));
+    if (ZM) SDRGPU_CHECK(p.zpart.ensure(sizeof(float) * 2 * 2048 * (size_t)frames));   // the two workgroups' partial rows
     const int g = 16 * ((frames + 7) / 8) + (VFO && v.hist ? 1 : 0);
     hipLaunchKernelGGL(k, dim3(g), dim3(512), op1::LDS_BYTES, s, in, stride, frames, p.win.as<float>(), p.nz,
                        p.tab1p.as<float2>(), p.tab1p64.as<double2>(), out, ZM ? p.zpart.as<float>() : nullptr, v);
@@ -1847,6 +1887,14 @@ int sdrgpu::fft_set_onepass(sdrgpu_fft* h, int onepass) {
     if (!h) return SDRGPU_EARG;
     h->p.onepass = onepass;
     return SDRGPU_OK;
+}
+
+extern "C" int sdrgpu_fft_set_kernel(sdrgpu_fft* h, int mode) {
+    if (!h || mode < 0 || mode > 2) { set_error("fft_set_kernel: bad argument"); return SDRGPU_EARG; }
+    FftPlan& p = h->p;
+    const int prev = p.N == 65536 ? p.onepass : 2;
+    if (p.N == 65536) p.onepass = mode;   // (read at call time: calls in flight keep their form)
+    return prev;
 }
 
 int sdrgpu::fft_execute_owned(sdrgpu_fft* h, const void* in, long long frameStride, int frames, float* out, hipStream_t s) {

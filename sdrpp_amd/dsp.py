@@ -224,6 +224,12 @@ class FFTSpectrum:
     def set_precision(self, precision):
         check(lib.sdrgpu_fft_set_precision(self._h, {"f32": 0, "f64": 1}[precision]))
 
+    def set_kernel(self, mode):
+        """64k transform form (sdrgpu_fft_set_kernel): "two-pass", "one-pass" or "auto" (per call size,
+        the default). Returns the previous mode's name."""
+        names = ("two-pass", "one-pass", "auto")
+        return names[check(lib.sdrgpu_fft_set_kernel(self._h, names.index(mode)))]
+
     @property
     def precision(self):
         return ("f32", "f64")[check(lib.sdrgpu_fft_get_precision(self._h))]

@@ -87,3 +87,14 @@ def test_spread_placement_one_stream_per_l3(monkeypatch):
     assert all(c < 64 for c in sp)                               # first SMT thread of each core
     sp12 = cb.placements(cpus, 12)[0]["spread"]
     assert sp12[:8] == sp and len(set(sp12)) == 12 and all(c < 64 for c in sp12)
+
+
+def test_measure_one_core_not_below_streams():
+    """the 1-core figure is never below what a stream of the all-core leg reached,
+    so the all-core aggregate is at most (stream count) x the 1-core figure and the whole-host bound
+    bench.py builds on it is not understated."""
+    import cpu_baseline as cb
+    r = cb.measure("c3", 0.3, max_cores=2)
+    assert r["value_1core"] >= r["value_1core_run"] and r["value_1core"] >= r["value_1core_spread_mean"]
+    assert r["value_all_cores"] <= r["cores_all"] * r["value_1core"] * (1 + 1e-9), r
+    assert r["value_1core_cpu"] in r["host"]["placement"]["cpus_spread"]

@@ -771,26 +771,93 @@ def test_spectrum_ulp_distribution(kind, N, nz, rng):
     e_ref = db_ulp_errors(ref32_fft_db(x, nz, N, w), truth)
     sg, sr = ulp_summary(e_gpu), ulp_summary(e_ref)
     write_report("spectrum_ulp", {"case": kind, "N": N, "nz": nz, "gpu": sg, "pocketfft_f32": sr})
-    # (the median of 17-22 near-peak bins of a tonal frame moves between 0 and 1 ulp with any change of
-    # rounding order: there it may exceed pocketfft's by one)
-    assert sg["p50"] <= sr["p50"] + (0 if sg["bins"] >= 1000 else 1), (sg, sr)
-    if sg["bins"] >= 1000:   # (a tonal frame has only a handful of bins within 60 dB of its peak)
-        assert sg["frac_le_1ulp"] >= sr["frac_le_1ulp"] - 0.03, (sg, sr)
-    assert sg["p99"] <= 2 * sr["p99"] + 1, (sg, sr)
-    # absolute bars (the literal north_star metric, stated rather than only relative): at least 97%
-    # of the bins within 1 ulp on a full random frame (measured 98.2% at 64k, 99.2% at 1M), p50 0 ulp
-    # (1 on the few-bin frames), and the worst bin no more than 2x pocketfft's worst (or 16 ulp):
-    # measured max 6 / 41 / 38 ulp vs pocketfft 10 / 28 / 77 at 4k / 64k / 1M (r5h). The tonal frames
-    # and the AES17 table have 17-22 bins within 60 dB of the peak, too few for a percentage (pocketfft
-    # itself has 18 of 22 AES17 bins within 1 ulp, 82%): there at most 2 more bins than pocketfft's
-    # beyond 1 ulp, and a worst bin within pocketfft's + 1 ulp
-    assert sg["p50"] <= (0 if sg["bins"] >= 1000 else 1), sg
     if sg["bins"] >= 1000:
+        # full random frames: the distribution in pocketfft's class -- median no worse, the fraction
+        # within 1 ulp within 3 points of its own, p99 within 2x (+1 ulp) -- and the absolute bars (the
+        # literal north_star metric, stated rather than only relative): at least 97% of the bins within
+        # 1 ulp (measured 98.2% at 64k, 99.2% at 1M), p50 0 ulp, the worst bin no more than 2x
+        # pocketfft's worst (or 16 ulp): measured max 6 / 41 / 38 ulp vs pocketfft 10 / 28 / 77 at
+        # 4k / 64k / 1M (r5h)
+        assert sg["p50"] <= sr["p50"], (sg, sr)
+        assert sg["frac_le_1ulp"] >= sr["frac_le_1ulp"] - 0.03, (sg, sr)
+        assert sg["p99"] <= 2 * sr["p99"] + 1, (sg, sr)
+        assert sg["p50"] == 0, sg
         assert sg["frac_le_1ulp"] >= 0.97, sg
         assert sg["max"] <= max(2 * sr["max"], 16), (sg, sr)
     else:
-        assert np.sum(e_gpu > 1.0) <= np.sum(e_ref > 1.0) + 2, (sg, sr)
-        assert sg["max"] <= sr["max"] + 1, (sg, sr)
+        # The tonal frames and the AES17 table have 17-22 bins within 60 dB of the peak: a relative bar
+        # against pocketfft on one such frame is a coin flip, so the relative comparison is
+        # made over the tonal corpus (test_spectrum_ulp_tonal_corpus). Here only absolute floors, so a
+        # regression to the fp32-twiddle form (7 of AES17's 22 bins beyond 1 ulp) still fails: at least
+        # 85% of the bins within 1 ulp (measured 2 of 22 / 2 of 17 / 1 of 18 beyond) and no bin past 8 ulp
+        assert sg["frac_le_1ulp"] >= 0.85, sg
+        assert sg["max"] <= 8, sg
+
+
+def _tonal_frame(N, nz, k):
+    """Frame k of the tonal corpus: a 0.5-amplitude tone and a -34 dB second tone at seed-dependent
+    frequencies over a -80 dB uniform noise floor (the test_spectrum_ulp_distribution 'tones' kind)."""
+    r = np.random.default_rng(0x70E5 + 7919 * k + N)
+    n = np.arange(nz)
+    f1 = 0.1234567 + 0.0371 * k + r.uniform(-1e-3, 1e-3)
+    f2 = -0.3 + 0.0113 * k + r.uniform(-1e-3, 1e-3)
+    x = (0.5 * np.exp(2j * np.pi * f1 * n) + 0.01 * np.exp(2j * np.pi * f2 * n)).astype(np.complex64)
+    return (x + iq(r, nz, 1e-4)).astype(np.complex64)
+
+
+def test_spectrum_ulp_tonal_corpus():
+    """the few-bin frames judged over a corpus instead of one frame at a time. 16
+    tonal 64k frames and 6 tonal 1M frames (nz = 1e6) at fixed seeds, plus the AES17 golden table; the
+    64k frames through both 64k forms (sdrgpu_fft_set_kernel: one-pass, the bench's headline kernel,
+    and two-pass, the per-block front end's). Over all of a form's frames, against pocketfft single
+    precision on the same frames (bins within 60 dB of each frame's peak, fp32 ulps of the correctly
+    rounded dB of the exact DFT): the pooled median no worse than pocketfft's, the total count of bins
+    beyond 1 ulp no more than pocketfft's, and the worst bin no worse than pocketfft's worst. The
+    report goes to profiles/ (spectrum_tonal_corpus)."""
+    g = np.load(GOLDEN + "/fft_aes17.npz")
+    frames = [("aes17", 65536, 65536, g["x"], g["power_f64"])]
+    for k in range(16):
+        x = _tonal_frame(65536, 65536, k)
+        frames.append((f"tones{k}", 65536, 65536, x, None))
+    for k in range(6):
+        x = _tonal_frame(1 << 20, 1000000, k)
+        frames.append((f"tones{k}", 1 << 20, 1000000, x, None))
+    forms = {"64k-one-pass": (65536, "one-pass"), "64k-two-pass": (65536, "two-pass"), "1M": (1 << 20, None)}
+    pools = {name: {"gpu": [], "ref": [], "frames": []} for name in forms}
+    plans = {}
+    for tag, N, nz, x, truth in frames:
+        w = oracle.create_window(6, nz)
+        if truth is None:
+            truth = oracle.fft_truth_power(x, nz, N, w)
+        e_ref = db_ulp_errors(ref32_fft_db(x, nz, N, w), truth)
+        for name, (fN, mode) in forms.items():
+            if fN != N:
+                continue
+            if name not in plans:
+                plans[name] = dsp.FFTSpectrum(N, nz, 6)
+                if mode:
+                    plans[name].set_kernel(mode)
+            e = db_ulp_errors(plans[name].logmag(x), truth)
+            pools[name]["gpu"].append(e)
+            pools[name]["ref"].append(e_ref)
+            pools[name]["frames"].append({"frame": tag, "bins": int(e.size), "gpu_gt1": int(np.sum(e > 1.0)),
+                                          "pocketfft_gt1": int(np.sum(e_ref > 1.0)), "gpu_max": float(e.max()),
+                                          "pocketfft_max": float(e_ref.max())})
+    summary = {}
+    for name, pl in pools.items():
+        eg, er = np.concatenate(pl["gpu"]), np.concatenate(pl["ref"])
+        summary[name] = {"frames": len(pl["gpu"]), "bins": int(eg.size),
+                         "gpu": {"p50": float(np.median(eg)), "mean": float(eg.mean()), "gt1": int(np.sum(eg > 1.0)),
+                                 "max": float(eg.max())},
+                         "pocketfft": {"p50": float(np.median(er)), "mean": float(er.mean()), "gt1": int(np.sum(er > 1.0)),
+                                       "max": float(er.max())},
+                         "per_frame": pl["frames"]}
+    write_report("spectrum_tonal_corpus", summary)
+    for name, sm in summary.items():
+        gs, rs = sm["gpu"], sm["pocketfft"]
+        assert gs["p50"] <= rs["p50"], (name, gs, rs)
+        assert gs["gt1"] <= rs["gt1"], (name, gs, rs)
+        assert gs["max"] <= rs["max"], (name, gs, rs)
 
 
 def test_spectrum_ulp_corpus():
@@ -867,11 +934,9 @@ def test_spectrum_f64_within_1ulp(kind, N, nz, rng):
     f.set_precision("f32")   # back to the fp32 kernels: same plan, FFTW-class bar
     assert f.precision == "f32"
     e32 = db_ulp_errors(f.logmag(x), truth)
-    if e32.size >= 1000:
-        assert np.mean(e32 <= 1.0) >= 0.97
-    else:   # (few bins: against pocketfft's count, as test_spectrum_ulp_distribution)
-        e_ref = db_ulp_errors(ref32_fft_db(x, nz, N, oracle.create_window(6, nz)), truth)
-        assert np.sum(e32 > 1.0) <= np.sum(e_ref > 1.0) + 2
+    # (few bins: the absolute floor of test_spectrum_ulp_distribution; the relative comparison with
+    # pocketfft is made over the tonal corpus, test_spectrum_ulp_tonal_corpus)
+    assert np.mean(e32 <= 1.0) >= (0.97 if e32.size >= 1000 else 0.85)
 
 
 @pytest.mark.parametrize("N,nz,stride,frames", [(65536, 65536, 65536, 300), (65536, 50000, 61000, 9),
@@ -1017,7 +1082,7 @@ def test_spectrum_onepass_rows_and_zoom(nz, skip, frames, rng, monkeypatch):
     frequency; SDRGPU_FFT_1P; persistent workgroups walking several frames each at 70 / 150 frames,
     a ragged last step): every row meets the spectrum parity bar against the fp64 truth and
     pocketfft on the same frame, zero-padded frames (nz < N) and reshaper strides included; the zoom
-    rows (four partial maxima folded) equal fft_scaler's doZoom of the row bit for bit; and the rows
+    rows (the two workgroups' partial maxima folded) equal fft_scaler's doZoom of the row bit for bit; and the rows
     agree with the two-pass kernels to the last bits near the peak."""
     import torch
     monkeypatch.setenv("SDRGPU_TUNING", "1")
@@ -1058,6 +1123,43 @@ def test_spectrum_onepass_vfo(frames_list, pre, rng, monkeypatch):
     monkeypatch.setenv("SDRGPU_TUNING", "1")
     monkeypatch.setenv("SDRGPU_FFT_1P", "1")
     _fused_vs_separate(frames_list, pre, rng, zoom=True)
+
+
+def test_spectrum_64k_rows_vs_call_size(rng):
+    """the 64k plan's default (sdrgpu_fft_set_kernel mode 2) runs the one-pass kernel on
+    calls of >= 64 frames and the two-pass launches below, so the same frames give different bits as a
+    64-frame call and as a 63 + 1 split. The bound sdrgpu.h states holds at the switch point (<= 0.05 dB
+    anywhere, <= 1e-3 dB within 60 dB of the frame's peak), and pinning the form per plan (mode 1 or 0)
+    makes every row independent of the call size, bit for bit."""
+    import torch
+    N, frames = 65536, 64
+    x = iq(rng, N * frames)
+    d_x = torch.from_numpy(x.view(np.float32)).cuda()
+
+    def rows(f, split):
+        out = torch.empty(frames * N, device="cuda")
+        f0 = 0
+        for n in split:
+            assert f.execute_dev(d_x.data_ptr() + 8 * N * f0, N, n, out.data_ptr() + 4 * N * f0) == n
+            f0 += n
+        torch.cuda.synchronize()
+        return out.cpu().numpy().reshape(frames, N)
+
+    f = dsp.FFTSpectrum(N, N, 6)
+    auto64, auto63 = rows(f, [64]), rows(f, [63, 1])
+    assert not np.array_equal(auto64, auto63)   # (the two forms really ran)
+    d = np.abs(auto64 - auto63)
+    near = auto64 >= auto64.max(axis=1, keepdims=True) - 60
+    assert d.max() <= 0.05 and d[near].max() <= 1e-3, (d.max(), d[near].max())
+    for mode in ("one-pass", "two-pass"):
+        assert f.set_kernel(mode) in ("auto", "one-pass")
+        a, b = rows(f, [64]), rows(f, [63, 1])
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(a, auto64 if mode == "one-pass" else auto63)
+    w = oracle.create_window(6, N)
+    for j in (0, 63):
+        xs = x[j * N:(j + 1) * N]
+        db_check(auto63[j], oracle.fft_truth_power(xs, N, N, w), N, ref32_fft_db(xs, N, N, w))
 
 
 # ------------------------------------------------- waterfall zoom fused into the spectrum

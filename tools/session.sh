@@ -19,6 +19,10 @@
 #   ablib   interleaved A/B of the in-tree build against sdrpp_amd/lib_<v> builds (AB_LIBS; built with
 #           python sdrpp_amd/build.py --variant <v> DEFINE ...)
 #   sq      SQ counter sets for SQ_CFG / SQ_RX (tools/pmc_sets.sh)
+#   testk   the -m gpu tests matching PYTEST_K only (a kernel change's own tests before an A/B)
+#   bits    tools/bits_digest.py (output digests of the C5 / C2 chains) for the in-tree build and each
+#           sdrpp_amd/lib_<v> of AB_LIBS -> TAG_bits_<v>.json (a variant must not change the bits)
+#   ulpcorpus the tonal + random spectrum ulp corpus tests alone, reports kept -> TAG_reports/
 # Every GPU step runs under its own timeout; the session stops at the first failure.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R" || exit 1
 OUT=$R/gpurun_out; TAG=${1:-s}; shift; mkdir -p "$OUT"
@@ -105,6 +109,21 @@ for step in $STEPS_LIST; do
   sq)
     bash tools/pmc_sets.sh "${TAG}_sq" "${SQ_RX:-fir_mfma_kernel}" "$R/bench.py" --config ${SQ_CFG:-c3} --no-sub --no-cpu --no-ulp --steps 3 --warmup 1 >> "$OUT/${TAG}_sq.log" 2>&1
     st sq $? ;;
+  testk)
+    SDRGPU_REPORT_DIR=$OUT/${TAG}_reports timeout -k 10 600 python -u -m pytest tests -m gpu -k "$PYTEST_K" -v -p no:cacheprovider \
+      --timeout 200 --timeout-method thread > "$OUT/${TAG}_testk.log" 2>&1
+    st_tests testk $? ;;
+  bits)
+    for v in tree ${AB_LIBS:-}; do
+      L=$R/sdrpp_amd/lib/libsdrgpu.so; [ "$v" = tree ] || L=$R/sdrpp_amd/lib_$v/libsdrgpu.so
+      SDRGPU_LIB_PATH=$L timeout -k 10 300 python tools/bits_digest.py > "$OUT/${TAG}_bits_$v.json" 2> "$OUT/${TAG}_bits_$v.err"
+      st bits_$v $?
+    done ;;
+  ulpcorpus)
+    SDRGPU_REPORT_DIR=$OUT/${TAG}_reports timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu \
+      -k "ulp_corpus or tonal_corpus or ulp_distribution" -v -p no:cacheprovider --timeout 400 --timeout-method thread \
+      > "$OUT/${TAG}_ulpcorpus.log" 2>&1
+    st_tests ulpcorpus $? ;;
   *) echo "unknown step $step" >> "$ST"; exit 2 ;;
   esac
 done
