@@ -155,6 +155,15 @@ class C5:
         # the spectrum group and the VFO as separate launch groups, as in round 3
         self.fuse = os.environ.get("BENCH_C5_FUSE", "1") != "0"
         self.zoom_count = self.frames * self.ZW
+        # BENCH_C5_TAIL=1: the VFO's later stages, the zoom fold and the WFM on a stream of their own
+        # (sdrgpu_fft_set_tail_stream), overlapping the next step's spectrum launch, as the reference runs the
+        # spectrum and each VFO chain on threads of their own (iq_frontend.cpp:15-52). Off by default: the
+        # step gained 5 us of 1.57 ms while the spectrum launch it overlaps stretched by 60 us (it fills every
+        # CU), which the roofline of that launch would carry (profiles/r6/c5_tail_stream_ab_r7b.txt)
+        self.tail = None
+        if self.fuse and os.environ.get("BENCH_C5_TAIL", "0") != "0" and dev is not None:
+            self.tail = torch.cuda.Stream()
+            self.fft.set_tail_stream(self.tail.cuda_stream)
         self.bytes_per_sample = 8 + 4 + 4 / 32 + 8 / 256 + 8 / 256   # SURVEY 8(d) C5 (~12.06 B) + the zoom rows
         if self.fuse:
             # the group: 8 B in (read once), 4 B dB out, 8/32 B VFO stage-1 out (the zoom rows are folded
@@ -176,6 +185,10 @@ class C5:
                                 "fft_merged_kernel<256,32,256,32,false,zoom> (pass B chunk c + pass A chunk c+1) x15 + "
                                 "fft_passB_kernel<256,32,zoom> (last chunk)")
 
+    def rows_stream(self, stream):
+        """The stream on which the zoom rows of a step are complete (the gather waits for it)."""
+        return self.tail if self.tail is not None else stream
+
     def run(self, x, s, timed_call, buf=0):
         # the front end's splitter hands the same block to the spectrum and the VFO
         # (iq_frontend.cpp:15-52); the VFO output then feeds the WFM demodulator
@@ -183,6 +196,9 @@ class C5:
             z = self.zoom[buf].data_ptr() if self.with_zoom else 0
             m = self.fft.execute_zoom_vfo_dev(x.data_ptr(), self.frames, self.spectra.data_ptr(), z, self.ZW, self.vfo,
                                               self.ifbuf.data_ptr(), s)
+            if self.tail is not None and self.with_zoom:   # the VFO output is complete on the tail stream
+                self.wfm.process_dev(self.ifbuf.data_ptr(), m, self.audio.data_ptr(), self.tail.cuda_stream)
+                return
         else:
             if self.with_zoom:
                 timed_call(lambda: self.fft.execute_zoom_dev(x.data_ptr(), self.N, self.frames, self.spectra.data_ptr(),
@@ -574,7 +590,8 @@ def run_config(config, a, shard, dev, stream, rt=None, workloads=None):
             if timed:
                 e1.record(stream)
                 evs.append((e0, e1))
-        buf = pipe.acquire(stream) if pipe is not None else 0
+        rs = wl.rows_stream(stream) if hasattr(wl, "rows_stream") else stream   # where the zoom rows are written
+        buf = pipe.acquire(rs) if pipe is not None else 0
         if hasattr(wl, "run"):
             wl.run(x, rt.handle(stream), timed_call, buf)
         else:
@@ -582,7 +599,7 @@ def run_config(config, a, shard, dev, stream, rt=None, workloads=None):
         if timed:
             ev.append(evs)
         if pipe is not None:
-            pipe.publish(buf, stream, timed=timed)
+            pipe.publish(buf, rs, timed=timed)
 
     def drain():
         if pipe is not None:

@@ -110,6 +110,14 @@ int sdrgpu_fft_execute_vfo_dev(sdrgpu_fft* h, const void* in, int frames, float*
 /* the same + the waterfall's full-span zoom rows (as sdrgpu_fft_execute_zoom_dev; zoomOut may be NULL) */
 int sdrgpu_fft_execute_zoom_vfo_dev(sdrgpu_fft* h, const void* in, int frames, float* out, float* zoomOut,
                                     int zoomSize, sdrgpu_block* vfo, void* vfoOut, void* stream);
+/* (not in the reference; its IQFrontEnd hands the spectrum and each VFO to blocks on their own
+ * threads, iq_frontend.cpp:15-52) A second stream for sdrgpu_fft_execute_zoom_vfo_dev calls with zoom
+ * rows: the VFO's later stages and the zoom fold run on `tailStream`, so they overlap the next call's
+ * spectrum launch on the call's stream instead of following it. Then `out` (the dB rows) is complete
+ * on the call's stream, while `vfoOut` and `zoomOut` are complete on `tailStream`: their consumers
+ * (a demodulator, a gather) must run on, or wait for, `tailStream`. Results are bit-identical to the
+ * one-stream calls. NULL turns it off (waiting for tails in flight). */
+int sdrgpu_fft_set_tail_stream(sdrgpu_fft* h, void* tailStream);
 /* (measurement, not in the reference) HIP events around each call's spectrum launch group -- the
  * fused VFO stage included, the VFO's later stages not; group_times returns the last
  * min(n, calls, 256) group times in ms, oldest first, waiting for them */

@@ -75,6 +75,7 @@ def _load():
         "sdrgpu_fft_set_precision": (i, [vp, i]),
         "sdrgpu_fft_get_precision": (i, [vp]),
         "sdrgpu_fft_set_kernel": (i, [vp, i]),
+        "sdrgpu_fft_set_tail_stream": (i, [vp, vp]),
         "sdrgpu_fft_destroy": (i, [vp]),
         "sdrgpu_xlator_create": (i, [pp, i, d]),
         "sdrgpu_xlator_set_offset": (i, [vp, d]),

@@ -426,9 +426,6 @@ __global__ __launch_bounds__(S / 2 * L / 16) void fft_passA2_kernel(
 // traffic). Measured alternatives (rounds 2-4; kept in git history, not here): 8-column
 // tiles (2.24-2.70 ms), spill-free laundered offsets (same time), the merged pass-B(c-1) + pass-A(c)
 // launches (1.80 vs 1.73 ms), two workgroups per CU (2.16 ms).
-#ifndef SDRGPU_1M_TW64
-#define SDRGPU_1M_TW64 0
-#endif
 __device__ __forceinline__ double2 zmul(double2 a, double2 b) {
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
@@ -609,14 +606,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         unsigned vo = (unsigned)(b * L * S + t * S + 2 * cp) * 8u;
 #pragma unroll
         for (int m = 0; m < 16; m++) {
-#if SDRGPU_1M_TW64   // (accuracy A/B builds) the four-step twiddle product in fp64, one rounding
-            const double2 ad = zmul(make_double2(y[0][m].x, y[0][m].y), cur[0]);
-            const double2 cd = zmul(make_double2(y[1][m].x, y[1][m].y), cur[1]);
-            const float2 a = make_float2((float)ad.x, (float)ad.y), c = make_float2((float)cd.x, (float)cd.y);
-#else
             const float2 a = cmul(y[0][m], make_float2((float)cur[0].x, (float)cur[0].y));
             const float2 c = cmul(y[1][m], make_float2((float)cur[1].x, (float)cur[1].y));
-#endif
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bu4, make_float4(a.x, a.y, c.x, c.y)), rs, vo, 0, 0);
             vo += (unsigned)(T * S * 8);
             asm volatile("" : "+v"(vo));
@@ -818,10 +809,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
 }
 
 // ---- one-pass 64k spectrum: no intermediate leaves the CU ----------------------------------------
-#ifndef SDRGPU_1P_TW64
-#define SDRGPU_1P_TW64 0   // (accuracy A/B builds) 1: stage-1 twiddle products in fp64 (one rounding), 2: stage-2
-                           // W_512 products in fp64 from an fp64 LDS table
-#endif
 // N = 65536 as four 16,384-point transforms (one radix-4 decimation-in-frequency step). Item (f, r)
 // computes the bins 4 m + r of frame f:
 //   X[4 m + r] = sum_{n < M} W_M^(n m) y_r[n],   y_r[n] = W_N^(n r) sum_{j < 4} W_4^(j r) w[n + M j] x[n + M j],
@@ -848,10 +835,9 @@ constexpr int RS = 560;                 // LDS row stride (float2)
 constexpr int TW512 = 32 * RS;          // W_512^(t0 q1) at [q1][t0]
 constexpr int W128 = TW512 + 512;       // W_128^(r i), i < 32
 constexpr int W128D = (W128 + 64) * 8;   // (bytes) fp64 W_128^(r i), r = r0, r0 + 1, i < 32
-constexpr int W512D = W128D + 64 * 16;   // (bytes) fp64 W_512^(t0 q1) at [q1][t0] (SDRGPU_1P_TW64 & 2)
-constexpr int LDS_BYTES = W512D + ((SDRGPU_1P_TW64 & 2) ? 512 * 16 : 0);
+constexpr int LDS_BYTES = W128D + 64 * 16;
 constexpr int TAB = 512 + 128;          // device table: [q1][t0] W_512^(t0 q1), [r][i] W_128^(r i)
-constexpr int TAB64 = 2048 + 128 + 512; // fp64 table: W_N^m (m < 2048), [r][i] W_128^(r i), [q1][t0] W_512^(t0 q1)
+constexpr int TAB64 = 2048 + 128;       // fp64 table: W_N^m (m < 2048), [r][i] W_128^(r i)
 }
 
 // x w, rounded on its own: never contracted into the radix-4 adds that follow (left to the compiler,
@@ -957,7 +943,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
         const int t = threadIdx.x;
         lds[TW512 + t] = tab[t];
         if (t < 64) reinterpret_cast<double2*>(reinterpret_cast<char*>(lds) + op1::W128D)[t] = tab64[2048 + 32 * (r0 + (t >> 5)) + (t & 31)];
-        if constexpr (SDRGPU_1P_TW64 & 2) reinterpret_cast<double2*>(reinterpret_cast<char*>(lds) + op1::W512D)[t] = tab64[2176 + t];
     }
     // stage 1: y_r for r = r0 (even) and r0 + 1 (odd) from the four quarters: y_r = A_r + W_4^r q_r with
     // A_r = u0 + s_r u2, q_r = u1 + s_r u3, s_r = (-1)^r; W_4^r in {1, -i, -1, i} as (fx, fy), one of
@@ -1121,18 +1106,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
                 const float2 cf = make_float2((float)ce.x, (float)ce.y), sf = make_float2((float)st.x, (float)st.y);
 #pragma unroll
                 for (int k2 = 0; k2 < 32; k2++) row[k2 * RS] = cmul(z[k2], k2 & 1 ? sf : cf);
-            } else if constexpr (SDRGPU_1P_TW64 & 1) {
-#pragma unroll
-                for (int k2 = 0; k2 < 32; k2 += 2) {
-                    const double2 qe = zmul(make_double2(z[k2].x, z[k2].y), ce);
-                    const double2 qo = zmul(make_double2(z[k2 + 1].x, z[k2 + 1].y), co);
-                    row[k2 * RS] = make_float2((float)qe.x, (float)qe.y);
-                    row[(k2 + 1) * RS] = make_float2((float)qo.x, (float)qo.y);
-                    if (k2 < 30) {
-                        ce = zmul(ce, st2);
-                        co = zmul(co, st2);
-                    }
-                }
             } else
 #pragma unroll
             for (int k2 = 0; k2 < 32; k2 += 2) {
@@ -1154,17 +1127,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
 #pragma unroll
             for (int t1 = 0; t1 < 32; t1++) a[t1] = src[17 * t1];
             dft32(a);
-            if constexpr (SDRGPU_1P_TW64 & 2) {
-                const double2* w512 = reinterpret_cast<const double2*>(reinterpret_cast<const char*>(lds) + op1::W512D);
 #pragma unroll
-                for (int q1 = 1; q1 < 32; q1++) {
-                    const double2 q = zmul(make_double2(a[q1].x, a[q1].y), w512[16 * q1 + t0]);
-                    a[q1] = make_float2((float)q.x, (float)q.y);
-                }
-            } else {
-#pragma unroll
-                for (int q1 = 1; q1 < 32; q1++) a[q1] = cmul(a[q1], lds[TW512 + 16 * q1 + t0]);
-            }
+            for (int q1 = 1; q1 < 32; q1++) a[q1] = cmul(a[q1], lds[TW512 + 16 * q1 + t0]);
             __syncthreads();
             float2* dst = lds + k2 * RS + (t0 ^ ((k2 >> 1) & 15));
 #pragma unroll
@@ -1237,273 +1201,6 @@ extern "C" int sdrgpu_debug_1p_times(unsigned long long* host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_1p_t), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : -1;
 }
 #endif
-
-// ---- one-pass 64k spectrum, 16-wave form (round 6) ----------------------------------------------
-#ifndef SDRGPU_1P16_DEFAULT
-#define SDRGPU_1P16_DEFAULT 0
-#endif
-// The same decomposition as fft_1p_kernel (one radix-4 DIF step; a workgroup transforms the quarter
-// pair r0, r0 + 1 of frame f; the frame's two workgroups on one XCD), with 1,024 threads per workgroup:
-// 16 waves, 4 per SIMD at 128 VGPRs, so every phase (the VFO half, the ring loads, the LDS stages) has
-// twice the waves to hide its latency. The 16k transform is M = 16 x 32 x 32:
-//   stage 1 (registers): thread t holds y_r[t + 1024 i], i < 16 (the four quarters combined as they
-//     arrive); W_64^(r i) (fp64 product, one rounding), a radix-16 DFT over i, and W_N^(t (4 k2 + r)) give
-//     A[t][k2], k2 < 16;
-//   stage 2 (LDS): per (k2, t0), t = t0 + 32 t1, a radix-32 DFT over t1 -> q1, twiddle W_1024^(t0 q1);
-//   stage 3 (LDS): per (k2, q1), a radix-32 DFT over t0 -> q2: Y[k2 + 16 q1 + 512 q2], dB, store.
-// A radix-32 item is held by a lane pair (lane ^ 1): lane e holds the 16 inputs of parity e, both run
-// a radix-16 DFT, lane 1 scales by W_32^k, and one DPP swap gives lane e the outputs k + 16 e
-// (X[k] = E + W O, X[k + 16] = E - W O, each one rounding: the same arithmetic as a radix-2 step).
-// Stage 1 writes [k2][t] (row stride 1026: the stage-2 pairs read 64 banks-distinct float2 per wave
-// up to the pair's 2-way); stages 2 -> 3 go through [q1][t0][k2] (k2 fastest: contiguous 8-byte pairs
-// of dB rows per 16 lanes). The rows stream into LDS by LDS-DMA through 3 ring slots of one row set
-// each (row set i = samples [1024 i, 1024 i + 1024) of the four quarters: x 4 x 8 KiB, w 4 x 4 KiB;
-// 48 pieces of 1 KiB, 3 per wave).
-namespace op16 {
-constexpr int M = 16384;
-constexpr int RS1 = 1026;                    // stage-1 image [k2][t] row stride (float2)
-constexpr int SLOT = 49152;                  // ring slot (bytes): one row set
-constexpr int NSLOT = 3;
-constexpr int IMG = NSLOT * SLOT;            // bytes (>= the stage images: 16 x 1026 x 8, 16384 x 8)
-constexpr int TW1K = IMG;                    // bytes: fp32 W_1024^(t0 q1) at [q1][t0]
-constexpr int W64D = TW1K + 1024 * 8;        // bytes: fp64 W_64^(r i) at [h][i], r = r0 + h, i < 16
-constexpr int LDS_BYTES = W64D + 32 * 16;
-constexpr int TAB = 1024;                    // device fp32 table: [q1][t0] W_1024^(t0 q1)
-constexpr int TAB64 = 4096 + 64;             // device fp64 table: W_N^m (m < 4096), [r][i] W_64^(r i)
-static_assert(16 * RS1 * 8 <= IMG && 16384 * 8 <= IMG, "op16 images fit the ring region");
-static_assert(LDS_BYTES <= 160 * 1024, "op16 LDS");
-}
-
-// the radix-32 DFT of a lane pair (module comment): in a[m] = x[2 m + e], out a[k] = X[k + 16 e]
-__device__ __forceinline__ void pair_dft32(float2 (&a)[16], int e) {
-    constexpr float C[16] = {1.0f, 0.98078528040323044913f, 0.92387953251128675613f, 0.83146961230254523708f,
-                             0.70710678118654752440f, 0.55557023301960222474f, 0.38268343236508977173f,
-                             0.19509032201612826785f, 0.0f, -0.19509032201612826785f, -0.38268343236508977173f,
-                             -0.55557023301960222474f, -0.70710678118654752440f, -0.83146961230254523708f,
-                             -0.92387953251128675613f, -0.98078528040323044913f};
-    dft16(a);
-    const float sg = e ? -1.0f : 1.0f;
-#pragma unroll
-    for (int k = 1; k < 16; k++) {   // lane 1: O[k] W_32^k (W_32^k = (C[k], -sin(2 pi k / 32))); lane 0: E[k] (x 1, exact)
-        const float wr = e ? C[k] : 1.0f, wi = e ? -C[(k + 8) & 15] * (k < 8 ? -1.0f : 1.0f) : 0.0f;
-        a[k] = cmul(a[k], make_float2(wr, wi));
-    }
-#pragma unroll
-    for (int k = 0; k < 16; k++) {   // X[k + 16 e] = E[k] +- W O[k]: partner + sg * own (exact sign)
-        const float px = xchg<1>(a[k].x, 0), py = xchg<1>(a[k].y, 0);
-        a[k] = make_float2(fmaf(sg, a[k].x, px), fmaf(sg, a[k].y, py));
-    }
-}
-
-__device__ __forceinline__ void vfo_half_block16(const VfoWork& v, int g, int p) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const long long seg = (long long)(v.frame0 + g) * 64 + p * 32 + wave * 2 + (lane >> 5);
-    fir_rows_segment<32, 5, true, false, 32, 32, true>(v.a, seg, lane);
-}
-
-template <bool ZM, bool VFO, bool PAD>
-__global__ __launch_bounds__(1024) void fft_1p16_kernel(
-    const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz,
-    const float2* __restrict__ tab, const double2* __restrict__ tab64, float* __restrict__ out, float* __restrict__ zpart,
-    VfoWork v) {
-    using op16::M;
-    using op16::RS1;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    if constexpr (VFO) {
-        if (v.hist && blockIdx.x == gridDim.x - 1) {   // the stage's history carry (fir.h:80)
-            (void)fir_hist_block<float2, true, false>(v.a);
-            return;
-        }
-    }
-    const int b = blockIdx.x, k = b >> 3;
-    const int f = 8 * (k >> 1) + (b & 7), p = k & 1, r0 = 2 * p;   // quarters r0, r0 + 1 of frame f
-    if (f >= frames) return;
-    constexpr bool kDma = !PAD;
-    if constexpr (VFO && !kDma) vfo_half_block16(v, f, p);
-    auto tid = [] {
-        int u = threadIdx.x;
-        asm volatile("" : "+v"(u));
-        return u;
-    };
-    char* const lb = reinterpret_cast<char*>(lds);
-    {
-        const int t = threadIdx.x;
-        reinterpret_cast<float2*>(lb + op16::TW1K)[t] = tab[t];
-        if (t < 32) reinterpret_cast<double2*>(lb + op16::W64D)[t] = tab64[4096 + 16 * (r0 + (t >> 4)) + (t & 15)];
-    }
-    const float fxa = p ? -1.0f : 1.0f, fyb = p ? 1.0f : -1.0f;   // W_4^r0 = (fxa, 0), W_4^(r0+1) = (0, fyb)
-    auto combine2 = [&](const float2 (&u)[4], float2& ya, float2& yb) {
-        const float2 aa = cadd(u[0], u[2]), qa = cadd(u[1], u[3]), ab = csub(u[0], u[2]), qb = csub(u[1], u[3]);
-        ya = make_float2(fmaf(fxa, qa.x, aa.x), fmaf(fxa, qa.y, aa.y));
-        yb = make_float2(fmaf(-fyb, qb.y, ab.x), fmaf(fyb, qb.x, ab.y));
-    };
-    float2 za[16], zb[16];
-    if constexpr (PAD) {   // zero-padded or unaligned frames: range-checked register loads, two rows in flight
-        const unsigned lim = (unsigned)nz;
-        const __amdgpu_buffer_rsrc_t rw = brsrc(win, lim * 4u);
-        const __amdgpu_buffer_rsrc_t rx = brsrc(in + (long long)f * frameStride, lim * 8u);
-        float2 xv[2][4];
-        float wv[2][4];
-        auto issue = [&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            const int t = tid();
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int n = t + 1024 * i + M * j;
-                xv[i & 1][j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, n * 8, 0, 0));
-                wv[i & 1][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, n * 4, 0, 0));
-            }
-        };
-        issue(std::integral_constant<int, 0>{});
-        issue(std::integral_constant<int, 1>{});
-        static_for<0, 16>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            float2 u[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) u[j] = wmul(xv[i & 1][j], wv[i & 1][j]);
-            combine2(u, za[i], zb[i]);
-            if constexpr (i + 2 < 16) issue(std::integral_constant<int, i + 2>{});
-            __builtin_amdgcn_sched_barrier(0);
-        });
-    } else {
-        constexpr int S = op16::NSLOT, SLOT = op16::SLOT;
-        typedef __attribute__((address_space(3))) char lchar;
-        const unsigned ldsBase = (unsigned)(size_t)(lchar*)lds;
-        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        const char* gb[3];
-        unsigned rstep[3], loff[3];
-        const float2* xf = in + (long long)f * frameStride;
-#pragma unroll
-        for (int e = 0; e < 3; e++) {
-            const int m = 3 * wave + e;
-            const int jx = m >> 3, cx = m & 7, jw = (m - 32) >> 2, cw = (m - 32) & 3;
-            gb[e] = m < 32 ? reinterpret_cast<const char*>(xf + M * jx + 128 * cx)
-                           : reinterpret_cast<const char*>(win + M * jw + 256 * cw);
-            rstep[e] = m < 32 ? 1024u * 8u : 1024u * 4u;
-            loff[e] = m < 32 ? (unsigned)(8192 * jx + 1024 * cx) : (unsigned)(32768 + 4096 * jw + 1024 * cw);
-        }
-        auto dma = [&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            const unsigned lane16 = (unsigned)(tid() & 63) * 16u;
-#pragma unroll
-            for (int e = 0; e < 3; e++) {
-                const char* src = gb[e] + lane16;
-                gb[e] += rstep[e];
-                asm volatile("" : "+s"(gb[e]));
-                const unsigned dst = __builtin_amdgcn_readfirstlane(ldsBase + (unsigned)((i % S) * SLOT) + loff[e]);
-                unsigned keep;
-                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                             : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-            }
-        };
-        static_for<0, S - 1>(dma);
-        if constexpr (VFO) vfo_half_block16(v, f, p);   // (its loads wait behind the ring's)
-        static_for<0, 16>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            constexpr int younger = (S - 2 < 15 - i) ? S - 2 : 15 - i;   // row sets issued after i, in flight
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * younger) : "memory");
-            __builtin_amdgcn_s_barrier();   // every wave's pieces landed; every read of slot i - 1 done
-            asm volatile("" ::: "memory");
-            if constexpr (i + S - 1 < 16) dma(std::integral_constant<int, i + S - 1>{});
-            const int t = tid();
-            const char* slot = lb + (i % S) * SLOT;
-            float2 u[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const float2 xx = *reinterpret_cast<const float2*>(slot + 8192 * j + 8 * t);
-                const float ww = *reinterpret_cast<const float*>(slot + 32768 + 4096 * j + 4 * t);
-                u[j] = wmul(xx, ww);
-            }
-            combine2(u, za[i], zb[i]);
-            __builtin_amdgcn_sched_barrier(0);
-        });
-    }
-    float* zf = ZM ? zpart + ((long long)f << 12) : nullptr;   // [f][p][2048]
-    const __amdgpu_buffer_rsrc_t ro = brsrc(out + ((long long)f << 16), 65536u * 4u);
-    float dA[16];   // quarter r0's dB values, paired with quarter r0 + 1's in 8-byte stores
-    auto transform = [&](auto hc, float2 (&z)[16]) {
-        constexpr int h = decltype(hc)::value;
-        const int r = r0 + h;
-        __syncthreads();   // (h = 0: the tables staged, the ring's reads done; h = 1: quarter r0's stage-3 reads done)
-        {   // stage-1 finish
-            const int t = tid();
-            const double2* w64 = reinterpret_cast<const double2*>(lb + op16::W64D) + 16 * h;
-#pragma unroll
-            for (int i = 1; i < 16; i++) {
-                const double2 q = zmul(make_double2(z[i].x, z[i].y), w64[i]);
-                z[i] = make_float2((float)q.x, (float)q.y);
-            }
-            dft16(z);
-            const double2 st = tab64[4 * t];
-            double2 ce = tab64[t * r], co = zmul(ce, st);
-            const double2 st2 = zmul(st, st);
-            float2* col = lds + t;
-#pragma unroll
-            for (int k2 = 0; k2 < 16; k2 += 2) {
-                col[k2 * RS1] = cmul(z[k2], make_float2((float)ce.x, (float)ce.y));
-                col[(k2 + 1) * RS1] = cmul(z[k2 + 1], make_float2((float)co.x, (float)co.y));
-                if (k2 < 14) {
-                    ce = zmul(ce, st2);
-                    co = zmul(co, st2);
-                }
-            }
-        }
-        __syncthreads();
-        {   // stage 2: item (k2, t0), lane pair e
-            const int u = tid(), l = u & 63;
-            const int e = l & 1, k2 = (l >> 1) & 15, t0 = 2 * (u >> 6) + (l >> 5);
-            float2 a[16];
-            const float2* src = lds + k2 * RS1 + t0 + 32 * e;
-#pragma unroll
-            for (int m = 0; m < 16; m++) a[m] = src[64 * m];
-            pair_dft32(a, e);
-            const float2* tw = reinterpret_cast<const float2*>(lb + op16::TW1K) + 512 * e + t0;
-#pragma unroll
-            for (int kk = 0; kk < 16; kk++) a[kk] = cmul(a[kk], tw[32 * kk]);   // (q1 = 0: W = (1, 0), exact)
-            __syncthreads();
-            float2* dst = lds + (16 * e * 32 + t0) * 16 + k2;
-#pragma unroll
-            for (int kk = 0; kk < 16; kk++) dst[kk * 32 * 16] = a[kk];
-        }
-        __syncthreads();
-        {   // stage 3: item (k2, q1), lane pair e; outputs q2 = kk + 16 e
-            const int u = tid(), l = u & 63;
-            const int e = l & 1, k2 = (l >> 1) & 15, q1 = 2 * (u >> 6) + (l >> 5);
-            float2 c[16];
-            const float2* src = lds + (q1 * 32 + e) * 16 + k2;
-#pragma unroll
-            for (int m = 0; m < 16; m++) c[m] = src[32 * m];
-            pair_dft32(c, e);
-            if constexpr (h == 0) {
-#pragma unroll
-                for (int kk = 0; kk < 16; kk++) dA[kk] = db_of(c[kk]);
-            } else {
-                float dv[16];
-                const unsigned vo = (unsigned)(4 * (k2 + 16 * q1 + 8192 * e) + r0) * 4u;
-#pragma unroll
-                for (int kk = 0; kk < 16; kk++) {
-                    dv[kk] = db_of(c[kk]);
-                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(bu2, make_float2(dA[kk], dv[kk])), ro, vo,
-                                                          kk * 2048 * 4, 0);
-                }
-                if constexpr (ZM) {   // zoom column (m >> 3) = (k2 >> 3) + 2 q1 + 64 q2: max over both quarters and k2 & 7
-#pragma unroll
-                    for (int kk = 0; kk < 16; kk++) dv[kk] = fmaxf(dA[kk], dv[kk]);
-                    tr_step<2, 8>(dv, l);
-                    tr_step<4, 4>(dv, l);
-                    tr_step<8, 2>(dv, l);
-                    // lane bits (b1 b2 b3) now select kk = 8 b1 + 4 b2 + 2 b3 + i in dv[i], i < 2
-                    const int kb = ((l & 2) << 2) | (l & 4) | ((l & 8) >> 2);
-                    float* zp = zf + ((long long)p << 11) + ((l >> 4) & 1) + 2 * q1 + 64 * (kb + 16 * e);
-                    zp[0] = dv[0];
-                    zp[64] = dv[1];
-                }
-            }
-        }
-    };
-    transform(std::integral_constant<int, 0>{}, za);
-    transform(std::integral_constant<int, 1>{}, zb);
-}
 
 // zoom[f][o] = max over the two workgroups' partial maxima (fft_1p_kernel's ZM): 4 columns per thread
 // as 16-B loads / stores (one element per thread took 20.8 us per 2^28-sample step); 256 threads per
@@ -1621,8 +1318,6 @@ struct FftPlan {
     int onepass = 0;                  // the 64k plan's one-pass kernel (fft_1p_kernel): 0 never, 1 always, 2 calls of
                                       // >= k1pMinFrames frames (SDRGPU_FFT_1P, tuning)
     DevBuf tab1p, tab1p64, zpart;
-    int form16 = SDRGPU_1P16_DEFAULT;   // the one-pass kernel's 16-wave form (fft_1p16_kernel; SDRGPU_FFT_1P16)
-    DevBuf tab16, tab16_64;
     // sdrgpu_fft_set_tail_stream: the fused VFO's later stages and the zoom fold of
     // sdrgpu_fft_execute_(zoom_)vfo_dev run on this stream, overlapping the next call's spectrum launch.
     // Their inputs (the VFO's stage-1 outputs, the zoom partials) are double-buffered per call parity;
@@ -1908,25 +1603,7 @@ extern "C" int sdrgpu_fft_create(sdrgpu_fft** out, int device, int fftSize, int 
             for (int m = 0; m < 2048; m++) t64[m] = w64(m);
             for (int r = 0; r < 4; r++)
                 for (int i = 0; i < 32; i++) t64[2048 + 32 * r + i] = w64(512LL * r * i);
-            for (int q1 = 0; q1 < 32; q1++)
-                for (int t0 = 0; t0 < 16; t0++) t64[2176 + 16 * q1 + t0] = w64(128LL * t0 * q1);
-            // the 16-wave form's: [q1][t0] W_1024^(t0 q1); fp64 W_N^m (m < 4096), [r][i] W_64^(r i)
-            std::vector<float2> t16(op16::TAB);
-            for (int q1 = 0; q1 < 32; q1++)
-                for (int t0 = 0; t0 < 32; t0++) t16[32 * q1 + t0] = w(64LL * t0 * q1);
-            std::vector<double2> t16d(op16::TAB64);
-            for (int m = 0; m < 4096; m++) t16d[m] = w64(m);
-            for (int r = 0; r < 4; r++)
-                for (int i = 0; i < 16; i++) t16d[4096 + 16 * r + i] = w64(1024LL * r * i);
-            if (const char* e = tuning_env("SDRGPU_FFT_1P16")) p.form16 = atoi(e);
-            rc = p.tab16.ensure(sizeof(float2) * t16.size());
-            if (rc >= 0) rc = p.tab16_64.ensure(sizeof(double2) * t16d.size());
-            if (rc >= 0 && (hipMemcpy(p.tab16.p, t16.data(), sizeof(float2) * t16.size(), hipMemcpyHostToDevice) != hipSuccess ||
-                            hipMemcpy(p.tab16_64.p, t16d.data(), sizeof(double2) * t16d.size(), hipMemcpyHostToDevice) != hipSuccess)) {
-                set_error("fft: twiddle upload failed");
-                rc = SDRGPU_EHIP;
-            }
-            if (rc >= 0) rc = p.tab1p.ensure(sizeof(float2) * t.size());
+            rc = p.tab1p.ensure(sizeof(float2) * t.size());
             if (rc >= 0) rc = p.tab1p64.ensure(sizeof(double2) * t64.size());
             if (rc >= 0 && (hipMemcpy(p.tab1p.p, t.data(), sizeof(float2) * t.size(), hipMemcpyHostToDevice) != hipSuccess ||
                             hipMemcpy(p.tab1p64.p, t64.data(), sizeof(double2) * t64.size(), hipMemcpyHostToDevice) != hipSuccess)) {
@@ -2020,17 +1697,10 @@ static int launch_1p(FftPlan& p, const float2* in, long long stride, int frames,
     DevBuf& zp = zpb ? *zpb : p.zpart;
     if (ZM) SDRGPU_CHECK(zp.ensure(sizeof(float) * 2 * 2048 * (size_t)frames));   // the two workgroups' partial rows
     const int g = 16 * ((frames + 7) / 8) + (VFO && v.hist ? 1 : 0);
-    if (p.form16 && p.tab16.p) {
-        auto k = pad ? fft_1p16_kernel<ZM, VFO, true> : fft_1p16_kernel<ZM, VFO, false>;
-        SDRGPU_CHECK(set_lds(k, op16::LDS_BYTES));
-        hipLaunchKernelGGL(k, dim3(g), dim3(1024), op16::LDS_BYTES, s, in, stride, frames, p.win.as<float>(), p.nz,
-                           p.tab16.as<float2>(), p.tab16_64.as<double2>(), out, ZM ? zp.as<float>() : nullptr, v);
-    } else {
-        auto k = pad ? fft_1p_kernel<ZM, VFO, true> : fft_1p_kernel<ZM, VFO, false>;
-        SDRGPU_CHECK(set_lds(k, op1::LDS_BYTES));
-        hipLaunchKernelGGL(k, dim3(g), dim3(512), op1::LDS_BYTES, s, in, stride, frames, p.win.as<float>(), p.nz,
-                           p.tab1p.as<float2>(), p.tab1p64.as<double2>(), out, ZM ? zp.as<float>() : nullptr, v);
-    }
+    auto k = pad ? fft_1p_kernel<ZM, VFO, true> : fft_1p_kernel<ZM, VFO, false>;
+    SDRGPU_CHECK(set_lds(k, op1::LDS_BYTES));
+    hipLaunchKernelGGL(k, dim3(g), dim3(512), op1::LDS_BYTES, s, in, stride, frames, p.win.as<float>(), p.nz,
+                       p.tab1p.as<float2>(), p.tab1p64.as<double2>(), out, ZM ? zp.as<float>() : nullptr, v);
     SDRGPU_HIP(hipGetLastError());
     if (ZM && fold) {
         const long long n = (long long)frames * 2048 / 4;

@@ -224,6 +224,11 @@ class FFTSpectrum:
     def set_precision(self, precision):
         check(lib.sdrgpu_fft_set_precision(self._h, {"f32": 0, "f64": 1}[precision]))
 
+    def set_tail_stream(self, stream):
+        """sdrgpu_fft_set_tail_stream: the fused VFO's later stages and the zoom fold of
+        execute_zoom_vfo_dev on `stream` (a HIP stream handle, or 0 / None to turn it off)."""
+        check(lib.sdrgpu_fft_set_tail_stream(self._h, stream or None))
+
     def set_kernel(self, mode):
         """64k transform form (sdrgpu_fft_set_kernel): "two-pass", "one-pass" or "auto" (per call size,
         the default). Returns the previous mode's name."""
