@@ -23,7 +23,6 @@
 #include <cmath>
 #include <vector>
 #include "sdrgpu_internal.h"
-#include "fir_rows.h"   // static_for
 
 namespace sdrgpu {
 namespace {
@@ -339,255 +338,11 @@ int upload_zt(DevBuf& b, long long L, int count, long long step) {
     return SDRGPU_OK;
 }
 
-// ---- N = 65536 in one pass (round 6) ---------------------------------------------------------------
-// No double2 intermediate: one radix-8 decimation-in-frequency step splits the frame into eight 8,192-
-// point transforms, X[8 m + r] = sum_{n < M} W_M^(n m) y_r[n], y_r[n] = W_N^(n r) sum_{j < 8} W_8^(j r)
-// v[n + M j], M = 8192, v = the fp32 window product promoted exactly. An 8k fp64 image (128 KB) fits the
-// LDS. Workgroup (f, p) computes r0 = 2 p and r0 + 1, so a frame's four workgroups (one XCD) each read the
-// frame (its first reader from HBM, the others mostly from that XCD's L2) and the dB rows of the pair
-// leave as 8-byte bin pairs. The 8k transform is M = 16 x 32 x 16 (cf. fft.hip's fft_1p_kernel):
-//   stage 1 (registers): thread t holds y_r[t + 512 i], i < 16; W_128^(r i), a radix-16 DFT over i, and
-//     W_N^(t (8 k2 + r)) (fp64 recurrence from table values) give A[t][k2];
-//   stage 2 (LDS): per (k2, t0), t = t0 + 32 t1: radix 16 over t1 -> q1, twiddle W_512^(t0 q1);
-//   stage 3 (LDS): per (k2, q1): radix 32 over t0 -> q2 on a lane pair (each lane a radix 16 of its
-//     parity, one DPP swap): Y[k2 + 16 q1 + 256 q2], dB, store.
-// Whole aligned frames stream into LDS by LDS-DMA through 3 ring slots of one row set (samples
-// [512 i, 512 i + 512) of the eight eighths: x 8 x 4 KiB, w 8 x 2 KiB; 48 pieces, 6 per wave); other
-// frames (zero padding, odd strides) through range-checked register loads.
-namespace z1p {
-constexpr int M = 8192;
-constexpr int RS = 513;                    // stage-1 image [k2][t] row stride (double2)
-constexpr int SLOT = 49152;                // ring slot (bytes)
-constexpr int NSLOT = 3;
-constexpr int IMG = NSLOT * SLOT;          // bytes (>= 16 x 513 x 16, 8192 x 16)
-constexpr int TW = IMG;                    // bytes: W_512^(t0 q1) at [q1][t0], q1 < 16, t0 < 32
-constexpr int W128 = TW + 512 * 16;        // bytes: W_128^(r i) at [h][i], r = r0 + h, i < 16
-constexpr int LDS_BYTES = W128 + 32 * 16;
-constexpr int TAB = 4096 + 512 + 128;      // device table: W_N^m (m < 4096), [q1][t0] W_512^(t0 q1), [r][i] W_128^(r i)
-static_assert(16 * RS * 16 <= IMG && M * 16 <= IMG && LDS_BYTES <= 160 * 1024, "z1p LDS");
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t zrsrc(const void* p, unsigned bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-// the double of the partner lane (lane ^ 1), as two DPP moves (quad_perm [1,0,3,2])
-__device__ __forceinline__ double zswap1(double v) {
-    const long long u = __builtin_bit_cast(long long, v);
-    const int lo = __builtin_amdgcn_update_dpp((int)u, (int)u, 0xB1, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp((int)(u >> 32), (int)(u >> 32), 0xB1, 0xF, 0xF, false);
-    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-// radix 32 on a lane pair: in a[m] = x[2 m + e], out a[k] = X[k + 16 e]
-__device__ __forceinline__ void zpair_dft32(double2 (&a)[16], int e) {
-    zdft<16>(a);
-    const double sg = e ? -1.0 : 1.0;
-#pragma unroll
-    for (int k = 1; k < 16; k++) {
-        const double c = cos(-2.0 * M_PI * k / 32.0), sn = sin(-2.0 * M_PI * k / 32.0);   // (constant-folded)
-        a[k] = zmul(a[k], make_double2(e ? c : 1.0, e ? sn : 0.0));
-    }
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const double px = zswap1(a[k].x), py = zswap1(a[k].y);
-        a[k] = make_double2(fma(sg, a[k].x, px), fma(sg, a[k].y, py));
-    }
-}
-
-template <bool PAD>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void fft64_1p_kernel(
-    const float2* __restrict__ in, long long frameStride, int frames, const float* __restrict__ win, int nz,
-    const double2* __restrict__ tab, float* __restrict__ out) {
-    using z1p::M;
-    using z1p::RS;
-    extern __shared__ __attribute__((aligned(16))) double2 zlds[];
-    const int b = blockIdx.x, k = b >> 3;
-    const int f = 8 * (k >> 2) + (b & 7), p = k & 3, r0 = 2 * p;   // transforms r0, r0 + 1 of frame f
-    if (f >= frames) return;
-    auto tid = [] {
-        int u = threadIdx.x;
-        asm volatile("" : "+v"(u));
-        return u;
-    };
-    char* const lb = reinterpret_cast<char*>(zlds);
-    {
-        const int t = threadIdx.x;
-        reinterpret_cast<double2*>(lb + z1p::TW)[t] = tab[4096 + t];
-        if (t < 32) reinterpret_cast<double2*>(lb + z1p::W128)[t] = tab[4096 + 512 + 16 * (r0 + (t >> 4)) + (t & 15)];
-    }
-    // y_r0, y_r0+1 from the eight eighths: Y_r = E_r + W_8^r O_r, E / O the 4-point DFTs of the even /
-    // odd eighths at r mod 4 (r0 mod 4 in {0, 2}, r0 + 1 mod 4 in {1, 3}: signs sg0, sg1)
-    const double sg0 = (p & 1) ? -1.0 : 1.0, sg1 = (p & 1) ? 1.0 : -1.0;
-    const double R2 = 0.70710678118654752440;
-    const double2 w80 = p == 0 ? make_double2(1.0, 0.0) : p == 1 ? make_double2(0.0, -1.0) : p == 2 ? make_double2(-1.0, 0.0)
-                                                                                                   : make_double2(0.0, 1.0);
-    const double2 w81 = p == 0 ? make_double2(R2, -R2) : p == 1 ? make_double2(-R2, -R2) : p == 2 ? make_double2(-R2, R2)
-                                                                                                 : make_double2(R2, R2);
-    auto combine = [&](const double2 (&v)[8], double2& ya, double2& yb) {
-        const double2 a0 = zadd(v[0], v[4]), b0 = zsub(v[0], v[4]), c0 = zadd(v[2], v[6]), d0 = zsub(v[2], v[6]);
-        const double2 a1 = zadd(v[1], v[5]), b1 = zsub(v[1], v[5]), c1 = zadd(v[3], v[7]), d1 = zsub(v[3], v[7]);
-        const double2 E0 = make_double2(fma(sg0, c0.x, a0.x), fma(sg0, c0.y, a0.y));
-        const double2 O0 = make_double2(fma(sg0, c1.x, a1.x), fma(sg0, c1.y, a1.y));
-        const double2 E1 = make_double2(fma(-sg1, d0.y, b0.x), fma(sg1, d0.x, b0.y));   // b -+ i d
-        const double2 O1 = make_double2(fma(-sg1, d1.y, b1.x), fma(sg1, d1.x, b1.y));
-        ya = zadd(E0, zmul(O0, w80));
-        yb = zadd(E1, zmul(O1, w81));
-    };
-    double2 za[16], zb[16];
-    if constexpr (PAD) {
-        const __amdgpu_buffer_rsrc_t rw = zrsrc(win, (unsigned)nz * 4u);
-        const __amdgpu_buffer_rsrc_t rx = zrsrc(in + (long long)f * frameStride, (unsigned)nz * 8u);
-        float2 xv[2][8];
-        float wv[2][8];
-        auto issue = [&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            const int t = tid();
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int n = t + 512 * i + M * j;
-                xv[i & 1][j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, n * 8, 0, 0));
-                wv[i & 1][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, n * 4, 0, 0));
-            }
-        };
-        issue(std::integral_constant<int, 0>{});
-        issue(std::integral_constant<int, 1>{});
-        static_for<0, 16>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            double2 v[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) v[j] = windowed(xv[i & 1][j], wv[i & 1][j]);
-            if constexpr (i + 2 < 16) issue(std::integral_constant<int, i + 2>{});
-            combine(v, za[i], zb[i]);
-        });
-    } else {
-        constexpr int S = z1p::NSLOT, SLOT = z1p::SLOT;
-        typedef __attribute__((address_space(3))) char lchar;
-        const unsigned ldsBase = (unsigned)(size_t)(lchar*)zlds;
-        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        const char* gb[6];
-        unsigned rstep[6], loff[6];
-        const float2* xf = in + (long long)f * frameStride;
-#pragma unroll
-        for (int e = 0; e < 6; e++) {
-            const int m = 6 * wave + e;
-            const int jx = m >> 2, cx = m & 3, jw = (m - 32) >> 1, cw = (m - 32) & 1;
-            gb[e] = m < 32 ? reinterpret_cast<const char*>(xf + M * jx + 128 * cx)
-                           : reinterpret_cast<const char*>(win + M * jw + 256 * cw);
-            rstep[e] = m < 32 ? 512u * 8u : 512u * 4u;
-            loff[e] = m < 32 ? (unsigned)(4096 * jx + 1024 * cx) : (unsigned)(32768 + 2048 * jw + 1024 * cw);
-        }
-        auto dma = [&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            const unsigned lane16 = (unsigned)(tid() & 63) * 16u;
-#pragma unroll
-            for (int e = 0; e < 6; e++) {
-                const char* src = gb[e] + lane16;
-                gb[e] += rstep[e];
-                asm volatile("" : "+s"(gb[e]));
-                const unsigned dst = __builtin_amdgcn_readfirstlane(ldsBase + (unsigned)((i % S) * SLOT) + loff[e]);
-                unsigned keep;
-                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                             : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-            }
-        };
-        static_for<0, S - 1>(dma);
-        static_for<0, 16>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            constexpr int younger = (S - 2 < 15 - i) ? S - 2 : 15 - i;   // row sets issued after i, in flight
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * younger) : "memory");
-            __builtin_amdgcn_s_barrier();   // every wave's pieces landed; every read of slot i - 1 done
-            asm volatile("" ::: "memory");
-            if constexpr (i + S - 1 < 16) dma(std::integral_constant<int, i + S - 1>{});
-            const int t = tid();
-            const char* slot = lb + (i % S) * SLOT;
-            double2 v[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const float2 xx = *reinterpret_cast<const float2*>(slot + 4096 * j + 8 * t);
-                const float ww = *reinterpret_cast<const float*>(slot + 32768 + 2048 * j + 4 * t);
-                v[j] = windowed(xx, ww);
-            }
-            combine(v, za[i], zb[i]);
-            __builtin_amdgcn_sched_barrier(0);
-        });
-    }
-    const __amdgpu_buffer_rsrc_t ro = zrsrc(out + ((long long)f << 16), 65536u * 4u);
-    float dA[16];   // transform r0's dB values, paired with r0 + 1's in 8-byte stores
-    auto transform = [&](auto hc, double2 (&z)[16]) {
-        constexpr int h = decltype(hc)::value;
-        const int r = r0 + h;
-        __syncthreads();   // (h = 0: the tables staged, the ring's reads done; h = 1: r0's stage-3 reads done)
-        {   // stage-1 finish
-            const int t = tid();
-            const double2* w128 = reinterpret_cast<const double2*>(lb + z1p::W128) + 16 * h;
-#pragma unroll
-            for (int i = 1; i < 16; i++) z[i] = zmul(z[i], w128[i]);
-            zdft<16>(z);
-            const double2 st = tab[8 * t];
-            double2 ce = tab[t * r], co = zmul(ce, st);
-            const double2 st2 = zmul(st, st);
-            double2* col = zlds + t;
-#pragma unroll
-            for (int k2 = 0; k2 < 16; k2 += 2) {
-                col[k2 * RS] = zmul(z[k2], ce);
-                col[(k2 + 1) * RS] = zmul(z[k2 + 1], co);
-                if (k2 < 14) {
-                    ce = zmul(ce, st2);
-                    co = zmul(co, st2);
-                }
-            }
-        }
-        __syncthreads();
-        {   // stage 2: item (k2, t0) = (u & 15, u >> 4)
-            const int u = tid();
-            const int k2 = u & 15, t0 = u >> 4;
-            double2 a[16];
-            const double2* src = zlds + k2 * RS + t0;
-#pragma unroll
-            for (int t1 = 0; t1 < 16; t1++) a[t1] = src[32 * t1];
-            zdft<16>(a);
-            const double2* tw = reinterpret_cast<const double2*>(lb + z1p::TW) + t0;
-#pragma unroll
-            for (int q1 = 1; q1 < 16; q1++) a[q1] = zmul(a[q1], tw[32 * q1]);
-            __syncthreads();
-            double2* dst = zlds + t0 * 16 + k2;
-#pragma unroll
-            for (int q1 = 0; q1 < 16; q1++) dst[q1 * 32 * 16] = a[q1];
-        }
-        __syncthreads();
-        {   // stage 3: item (k2, q1), lane pair e: outputs q2 = kk + 16 e
-            const int u = tid();
-            const int e = u & 1, k2 = (u >> 1) & 15, q1 = u >> 5;
-            double2 c[16];
-            const double2* src = zlds + (q1 * 32 + e) * 16 + k2;
-#pragma unroll
-            for (int m = 0; m < 16; m++) c[m] = src[32 * m];
-            zpair_dft32(c, e);
-            if constexpr (h == 0) {
-#pragma unroll
-                for (int kk = 0; kk < 16; kk++) dA[kk] = zdb(c[kk]);
-            } else {
-                const unsigned vo = (unsigned)(8 * (k2 + 16 * q1 + 4096 * e) + r0) * 4u;
-#pragma unroll
-                for (int kk = 0; kk < 16; kk++) {
-                    const float dv = zdb(c[kk]);
-                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned,
-                                                                             make_float2(dA[kk], dv)),
-                                                          ro, vo, kk * 8192, 0);
-                }
-            }
-        }
-    };
-    transform(std::integral_constant<int, 0>{}, za);
-    transform(std::integral_constant<int, 1>{}, zb);
-}
-
 }  // namespace
 
 struct Fft64Plan {
     int N = 0, logN = 0, N1 = 0, N2 = 0, chunkFrames = 1;
     DevBuf tw1, tw2, thi, tlo, scratch;
-    DevBuf tab1p;   // N = 65536: fft64_1p_kernel's table (z1p::TAB)
-    int onepass = 1;   // N = 65536: the one-pass kernel (SDRGPU_F64_1P=0: the two passes, A/B)
 };
 
 int fft64_create(Fft64Plan** out, int N) {
@@ -610,24 +365,6 @@ int fft64_create(Fft64Plan** out, int N) {
         if (rc >= 0) rc = upload_zt(p->thi, N, nhi, 1024);   // W_N^(1024 h)
         if (rc >= 0) rc = upload_zt(p->tlo, N, 1024, 1);     // W_N^l
         p->chunkFrames = std::max(1, (int)((128LL << 20) / ((long long)N * 16)));
-        if (rc >= 0 && N == 65536) {
-            std::vector<double2> t(z1p::TAB);
-            auto w = [&](long long m) {
-                const double a = -2.0 * M_PI * (double)(m % N) / (double)N;
-                return make_double2(std::cos(a), std::sin(a));
-            };
-            for (int m = 0; m < 4096; m++) t[m] = w(m);
-            for (int q1 = 0; q1 < 16; q1++)
-                for (int t0 = 0; t0 < 32; t0++) t[4096 + 32 * q1 + t0] = w(128LL * t0 * q1);   // W_512^(t0 q1)
-            for (int r = 0; r < 8; r++)
-                for (int i = 0; i < 16; i++) t[4096 + 512 + 16 * r + i] = w(512LL * r * i);     // W_128^(r i)
-            rc = p->tab1p.ensure(sizeof(double2) * t.size());
-            if (rc >= 0 && hipMemcpy(p->tab1p.p, t.data(), sizeof(double2) * t.size(), hipMemcpyHostToDevice) != hipSuccess) {
-                set_error("fft64: table upload failed");
-                rc = SDRGPU_EHIP;
-            }
-            if (const char* e = tuning_env("SDRGPU_F64_1P")) p->onepass = atoi(e);
-        }
     }
     if (rc < 0) {
         delete p;
@@ -654,15 +391,6 @@ int fft64_execute(Fft64Plan* p, const float2* in, long long stride, int frames, 
         }
         set_error("fft64: size %d", p->N);
         return SDRGPU_EARG;
-    }
-    if (p->N == 65536 && p->onepass && p->tab1p.p) {
-        const bool pad = nz < 65536 || (stride & 1) || ((uintptr_t)in & 15);
-        auto k = pad ? fft64_1p_kernel<true> : fft64_1p_kernel<false>;
-        SDRGPU_CHECK(zset_lds(k, z1p::LDS_BYTES));
-        hipLaunchKernelGGL(k, dim3(32 * ((frames + 7) / 8)), dim3(512), z1p::LDS_BYTES, s, in, stride, frames, win, nz,
-                           p->tab1p.as<double2>(), out);
-        SDRGPU_HIP(hipGetLastError());
-        return frames;
     }
     SDRGPU_CHECK(p->scratch.ensure((size_t)std::min(p->chunkFrames, frames) * p->N * sizeof(double2)));
     double2* sc = p->scratch.as<double2>();
