@@ -1386,6 +1386,7 @@ struct ChainBlock : Block {
         if (tailMode < 0) {
             const char* e = tuning_env("SDRGPU_VFO_TAIL");
             tailMode = e ? atoi(e) : 2;
+            if (const char* b = tuning_env("SDRGPU_TAIL_BIGOUT")) tailBigOut = std::max(32, atoi(b));
         }
         const int S = (int)kids.size() - 1;
         if (!tailMode || S < 2 || S > TAIL_MAXS) return 0;
@@ -1464,7 +1465,7 @@ struct ChainBlock : Block {
         t.tapTotal = tapF;
         if (tapF > 2 * TAIL_NT) return 0;                 // two tap loads per thread
         lds = sizeof(float2) * (size_t)maxEl + sizeof(float) * (size_t)tapF;
-        if (lds > 64 * 1024) return 0;
+        if (lds > TAIL_LDSMAX) return 0;
         return 1;
     }
     // the tail launch over kid 0's output s1 (n0 samples) into out, and the kids' state update

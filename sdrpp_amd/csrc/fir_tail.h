@@ -34,7 +34,14 @@ constexpr int TAIL_NT = 256;    // threads per workgroup (short calls)
 #endif
 constexpr int TAIL_K_BIG = SDRGPU_TAIL_KBIG;     // big calls (A/B builds)
 constexpr int TAIL_NT_BIG = SDRGPU_TAIL_NTBIG;
-constexpr int TAIL_PF = 16;     // image loads per thread issued together
+#ifndef SDRGPU_TAIL_PF
+#define SDRGPU_TAIL_PF 16
+#endif
+#ifndef SDRGPU_TAIL_LDSMAX
+#define SDRGPU_TAIL_LDSMAX 65536
+#endif
+constexpr int TAIL_PF = SDRGPU_TAIL_PF;     // image loads per thread issued together (A/B builds)
+constexpr int TAIL_LDSMAX = SDRGPU_TAIL_LDSMAX;   // bytes of LDS a tail workgroup may take
 struct TailStage {
     const float2* hist;   // H samples (newest last)
     float2* histNext;     // next call's history: [hist || in][n + k], k < H
