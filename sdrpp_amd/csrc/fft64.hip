@@ -161,39 +161,34 @@ __device__ __forceinline__ void zfft(double2* lds, const double2* __restrict__ t
 }
 
 // K3 in fp64: 10 log10 |X|^2, rounded once (p = 0 -> -inf, as log10f). 10 log10 p = (10 / ln 10) (e ln 2
-// + ln m) with p = m 2^e, m in [sqrt(1/2), sqrt(2)); ln m = 2 atanh(s) = 2 s (1 + s^2/3 + ... + s^20/21),
-// s = (m - 1) / (m + 1), |s| <= 0.1716, so the series' remainder is below 3e-17 and the result carries
-// a few fp64 ulps (~1e-15 relative), far inside one fp32 ulp of the dB value; about half the VALU of
-// the device libm's log10, which was the pass-B kernel's largest cost (SDRGPU_F64_LIBLOG: A/B builds)
+// + ln c_k + ln(1 + u)) with p = m 2^e, m in [1/2, 1), c_k the centre of m's 1/256-wide interval k (a
+// 128-entry fp64 table of ln c_k and 1 / c_k, L1-resident) and u = m / c_k - 1 (one fma, |u| <= 2^-8):
+// ln(1 + u) by six terms of its series (remainder below u^7 / 7 ~ 1e-17), so the result carries a few fp64
+// ulps (~1e-15 relative), far inside one fp32 ulp of the dB value. Round 6: the table replaces a ten-term
+// atanh series behind an fp64 division (the pass-B kernel's largest cost); SDRGPU_F64_LIBLOG: A/B builds.
 #ifndef SDRGPU_F64_LIBLOG
 #define SDRGPU_F64_LIBLOG 0
 #endif
-__device__ __forceinline__ float zdb(double2 X) {
+constexpr int kLnTab = 128;
+__device__ __forceinline__ float zdb(double2 X, const double2* __restrict__ lnt) {
     const double p = X.x * X.x + X.y * X.y;
 #if SDRGPU_F64_LIBLOG
     return (float)(10.0 * log10(p));
 #else
     if (!(p > 0.0) || !(p < 1.0e308)) return (float)(10.0 * log10(p));   // (0, inf, nan: the libm path)
     int e;
-    double m = frexp(p, &e);   // [0.5, 1)
-    if (m < 0.70710678118654752440) {
-        m *= 2.0;
-        e -= 1;
-    }
-    const double s = (m - 1.0) / (m + 1.0), t = s * s;
-    double P = 1.0 / 21.0;
-    P = fma(P, t, 1.0 / 19.0);
-    P = fma(P, t, 1.0 / 17.0);
-    P = fma(P, t, 1.0 / 15.0);
-    P = fma(P, t, 1.0 / 13.0);
-    P = fma(P, t, 1.0 / 11.0);
-    P = fma(P, t, 1.0 / 9.0);
-    P = fma(P, t, 1.0 / 7.0);
-    P = fma(P, t, 1.0 / 5.0);
-    P = fma(P, t, 1.0 / 3.0);
-    const double lnm = 2.0 * s + (2.0 * s * t) * P;   // 2 s (1 + t P)
+    const double m = frexp(p, &e);   // [0.5, 1)
+    const int k = min((int)((m - 0.5) * 256.0), kLnTab - 1);
+    const double2 t = lnt[k];         // (ln c_k, 1 / c_k)
+    const double u = fma(m, t.y, -1.0);
+    double P = -1.0 / 6.0;
+    P = fma(P, u, 1.0 / 5.0);
+    P = fma(P, u, -1.0 / 4.0);
+    P = fma(P, u, 1.0 / 3.0);
+    P = fma(P, u, -1.0 / 2.0);
+    const double l1u = fma(u * u, P, u);   // u + u^2 (-1/2 + u / 3 - ...)
     const double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
-    const double ln = fma((double)e, LN2_HI, fma((double)e, LN2_LO, lnm));
+    const double ln = fma((double)e, LN2_HI, fma((double)e, LN2_LO, t.x + l1u));
     return (float)(4.34294481903251827651 * ln);
 #endif
 }
@@ -207,7 +202,8 @@ __device__ __forceinline__ double2 windowed(float2 x, float w) {
 template <int L, int S>
 __global__ __launch_bounds__(S * L / 16) void fft64_single_kernel(const float2* __restrict__ in, long long stride, int frames,
                                                                   const float* __restrict__ win, int nz,
-                                                                  const double2* __restrict__ twL, float* __restrict__ out) {
+                                                                  const double2* __restrict__ twL, float* __restrict__ out,
+                                                                  const double2* __restrict__ lnt) {
     extern __shared__ __attribute__((aligned(16))) double2 zlds[];
     constexpr int LS = ZLds<L>::LS, NT = S * L / 16;
     const long long f0 = (long long)blockIdx.x * S;
@@ -221,12 +217,14 @@ __global__ __launch_bounds__(S * L / 16) void fft64_single_kernel(const float2* 
     __syncthreads();
     zfft<L, S, false>(zlds, twL, [&](int s, int k, double2 X) {
         const long long f = f0 + s;
-        if (f < frames) out[f * L + k] = zdb(X);
+        if (f < frames) out[f * L + k] = zdb(X, lnt);
     });
 }
 
 // ---- pass A: S columns of one frame ---------------------------------------------------------------
-// frame viewed as N1 x N2 (x[n1 N2 + n2]); column FFT over n1 -> k1; x W_N^(n2 k1) on the store
+// frame viewed as N1 x N2 (x[n1 N2 + n2]); column FFT over n1 -> k1; x W_N^(n2 k1) on the store.
+// (The output order of zstage's last stage is relied on by the twiddle recurrence below. Round 6, measured: a persistent form with the next tile's loads in flight spilled at two workgroups
+// per CU and ran at half the speed of this one-tile kernel, r7i.)
 template <int L, int S>
 __global__ __launch_bounds__(S * L / 16) void fft64_passA_kernel(const float2* __restrict__ in, long long stride, int frames,
                                                                  const float* __restrict__ win, int nz, int N2, int logN,
@@ -240,27 +238,66 @@ __global__ __launch_bounds__(S * L / 16) void fft64_passA_kernel(const float2* _
     if (f >= frames) return;
     const float2* x = in + f * stride;
     const int c0 = b * S;
-    for (int e = threadIdx.x; e < S * L; e += NT) {   // column fastest: S x 8-B row segments
+    // column fastest: S x 8-B row segments. Each thread's 16 elements are loaded in one batch (all
+    // in flight), then written to LDS: as a loop the loads waited one by one (vmcnt(0) per element;
+    // round 6: 82 -> 57 us per 128 64k frames, r7f)
+    static_assert(S * L == 16 * NT, "16 elements per thread");
+    float2 xv[16];
+    float wv[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int e = threadIdx.x + k * NT;
+        const int n = (e / S) * N2 + c0 + e % S;
+        const int nc = n < nz ? n : 0;   // (zero padding: an in-bounds load, selected away)
+        xv[k] = x[nc];
+        wv[k] = win[nc];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int e = threadIdx.x + k * NT;
         const int c = e % S, n1 = e / S;
         const int n = n1 * N2 + c0 + c;
-        double2 v = make_double2(0.0, 0.0);
-        if (n < nz) v = windowed(x[n], win[n]);
-        zlds[c * LS + zpad(n1)] = v;
+        zlds[c * LS + zpad(n1)] = n < nz ? windowed(xv[k], wv[k]) : make_double2(0.0, 0.0);
     }
     __syncthreads();
     const int N = 1 << logN;
     double2* sc = scratch + (f << logN);
+    // The last stage (radix R, NS = L / R, BPT = 16 / R butterflies per thread) hands this thread its outputs
+    // k1 = t + (L / 16) b + NS r in order b = 0.., r = 0..R-1: W_N^(n2 k1) by an fp64 recurrence from three
+    // table products, W_N^(n2 t), W_N^(n2 L / 16) (next b), W_N^(n2 NS) (next r), one fp64 product per output
+    // (at most ~20 in a chain: a few fp64 ulps) instead of two dependent table loads (r7g: 57 -> 47 us per
+    // 128 64k frames)
+    constexpr int RL = L == 64 ? 4 : L == 128 ? 8 : L == 256 ? 16 : L == 512 ? 2 : L == 1024 ? 4 : L == 2048 ? 8 : 16;
+    constexpr int NSL = L / RL;
+    auto twn = [&](long long e) {
+        const int m = (int)(e & (N - 1));   // exact argument mod N
+        return zmul(thi[m >> 10], tlo[m & 1023]);
+    };
+    double2 cb = make_double2(1.0, 0.0), w = cb, sb = cb, sr = cb;
+    int idx = 0;
     zfft<L, S, true>(zlds, twL, [&](int c, int k1, double2 X) {
         const int n2 = c0 + c;
-        const int m = (int)(((long long)n2 * k1) & (N - 1));   // W_N^(n2 k1), exact argument mod N
-        sc[(long long)k1 * N2 + n2] = zmul(X, zmul(thi[m >> 10], tlo[m & 1023]));
+        if (idx == 0) {
+            cb = twn((long long)n2 * k1);
+            sb = twn((long long)n2 * (L / 16));
+            sr = twn((long long)n2 * NSL);
+            w = cb;
+        } else if (idx % RL == 0) {
+            cb = zmul(cb, sb);
+            w = cb;
+        } else {
+            w = zmul(w, sr);
+        }
+        idx++;
+        sc[(long long)k1 * N2 + n2] = zmul(X, w);
     });
 }
 
 // ---- pass B: S rows k1 of one frame ----------------------------------------------------------------
 template <int L, int S>
 __global__ __launch_bounds__(S * L / 16) void fft64_passB_kernel(const double2* __restrict__ scratch, int frames, int N1, int logN,
-                                                                 const double2* __restrict__ twL, float* __restrict__ out) {
+                                                                 const double2* __restrict__ twL, float* __restrict__ out,
+                                                                 const double2* __restrict__ lnt) {
     extern __shared__ __attribute__((aligned(16))) double2 zlds[];
     constexpr int LS = ZLds<L>::LS, NT = S * L / 16;
     const int nb = N1 / S;
@@ -269,10 +306,18 @@ __global__ __launch_bounds__(S * L / 16) void fft64_passB_kernel(const double2* 
     if (f >= frames) return;
     const int r0 = b * S;
     const double2* sc = scratch + (f << logN) + (long long)r0 * L;
-    for (int e = threadIdx.x; e < S * L; e += NT) zlds[(e / L) * LS + zpad(e % L)] = sc[e];   // S contiguous rows
+    static_assert(S * L == 16 * NT, "16 elements per thread");
+    double2 rv[16];   // S contiguous rows, each thread's 16 elements loaded in one batch
+#pragma unroll
+    for (int k = 0; k < 16; k++) rv[k] = sc[threadIdx.x + k * NT];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int e = threadIdx.x + k * NT;
+        zlds[(e / L) * LS + zpad(e % L)] = rv[k];
+    }
     __syncthreads();
     float* o = out + (f << logN);
-    zfft<L, S, true>(zlds, twL, [&](int s, int k2, double2 X) { o[r0 + s + (long long)N1 * k2] = zdb(X); });
+    zfft<L, S, true>(zlds, twL, [&](int s, int k2, double2 X) { o[r0 + s + (long long)N1 * k2] = zdb(X, lnt); });
 }
 
 template <typename K>
@@ -287,15 +332,19 @@ constexpr int zS(int L) { return L <= 256 ? 16 : L <= 1024 ? 8 : L == 2048 ? 2 :
 #define SDRGPU_F64_SA256 16   // (A/B builds) pass-A columns per workgroup at N1 = 256
 #endif
 constexpr int zSA(int L) { return L == 256 ? SDRGPU_F64_SA256 : zS(L); }
+#ifndef SDRGPU_F64_SB256
+#define SDRGPU_F64_SB256 16   // (A/B builds) pass-B rows per workgroup at N2 = 256 (32: 128-B dB segments, 1 workgroup per CU: slower, r7h)
+#endif
+constexpr int zSB(int L) { return L == 256 ? SDRGPU_F64_SB256 : zS(L); }
 
 template <int L>
 int launch_single64(const double2* tw, const float2* in, long long stride, int frames, const float* win, int nz, float* out,
-                    hipStream_t s) {
+                    const double2* lnt, hipStream_t s) {
     constexpr int S = zS(L);
     auto k = fft64_single_kernel<L, S>;
     const size_t lds = sizeof(double2) * S * ZLds<L>::LS;
     SDRGPU_CHECK(zset_lds(k, lds));
-    hipLaunchKernelGGL(k, dim3((frames + S - 1) / S), dim3(S * L / 16), lds, s, in, stride, frames, win, nz, tw, out);
+    hipLaunchKernelGGL(k, dim3((frames + S - 1) / S), dim3(S * L / 16), lds, s, in, stride, frames, win, nz, tw, out, lnt);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
@@ -315,13 +364,14 @@ int launch_passA64(const double2* tw, const float2* in, long long stride, int fr
 }
 
 template <int L>
-int launch_passB64(const double2* tw, const double2* scratch, int frames, int N1, int logN, float* out, hipStream_t s) {
-    constexpr int S = zS(L);
+int launch_passB64(const double2* tw, const double2* scratch, int frames, int N1, int logN, float* out, const double2* lnt,
+                   hipStream_t s) {
+    constexpr int S = zSB(L);
     if (N1 % S) { set_error("fft64: N1 %d not a multiple of %d", N1, S); return SDRGPU_ESTATE; }
     auto k = fft64_passB_kernel<L, S>;
     const size_t lds = sizeof(double2) * S * ZLds<L>::LS;
     SDRGPU_CHECK(zset_lds(k, lds));
-    hipLaunchKernelGGL(k, dim3((N1 / S) * frames), dim3(S * L / 16), lds, s, scratch, frames, N1, logN, tw, out);
+    hipLaunchKernelGGL(k, dim3((N1 / S) * frames), dim3(S * L / 16), lds, s, scratch, frames, N1, logN, tw, out, lnt);
     SDRGPU_HIP(hipGetLastError());
     return SDRGPU_OK;
 }
@@ -343,6 +393,7 @@ int upload_zt(DevBuf& b, long long L, int count, long long step) {
 struct Fft64Plan {
     int N = 0, logN = 0, N1 = 0, N2 = 0, chunkFrames = 1;
     DevBuf tw1, tw2, thi, tlo, scratch;
+    DevBuf lnt;   // zdb's (ln c_k, 1 / c_k), k < kLnTab
 };
 
 int fft64_create(Fft64Plan** out, int N) {
@@ -354,7 +405,20 @@ int fft64_create(Fft64Plan** out, int N) {
     p->N = N;
     p->logN = logN;
     int rc;
-    if (N <= 4096) {
+    {
+        std::vector<double2> t(kLnTab);
+        for (int k = 0; k < kLnTab; k++) {
+            const double c = 0.5 + (k + 0.5) / 256.0;
+            t[k] = make_double2(std::log(c), 1.0 / c);
+        }
+        rc = p->lnt.ensure(sizeof(double2) * kLnTab);
+        if (rc >= 0 && hipMemcpy(p->lnt.p, t.data(), sizeof(double2) * kLnTab, hipMemcpyHostToDevice) != hipSuccess) {
+            set_error("fft64: table upload failed");
+            rc = SDRGPU_EHIP;
+        }
+    }
+    if (rc < 0) {
+    } else if (N <= 4096) {
         rc = upload_zt(p->tw1, N, N, 1);
     } else {
         p->N1 = 1 << ((logN + 1) / 2);
@@ -378,16 +442,17 @@ void fft64_destroy(Fft64Plan* p) { delete p; }
 
 int fft64_execute(Fft64Plan* p, const float2* in, long long stride, int frames, const float* win, int nz, float* out,
                   hipStream_t s) {
+    const double2* lt = p->lnt.as<double2>();
     if (p->N1 == 0) {
         const double2* tw = p->tw1.as<double2>();
         switch (p->N) {
-        case 64: SDRGPU_CHECK(launch_single64<64>(tw, in, stride, frames, win, nz, out, s)); return frames;
-        case 128: SDRGPU_CHECK(launch_single64<128>(tw, in, stride, frames, win, nz, out, s)); return frames;
-        case 256: SDRGPU_CHECK(launch_single64<256>(tw, in, stride, frames, win, nz, out, s)); return frames;
-        case 512: SDRGPU_CHECK(launch_single64<512>(tw, in, stride, frames, win, nz, out, s)); return frames;
-        case 1024: SDRGPU_CHECK(launch_single64<1024>(tw, in, stride, frames, win, nz, out, s)); return frames;
-        case 2048: SDRGPU_CHECK(launch_single64<2048>(tw, in, stride, frames, win, nz, out, s)); return frames;
-        case 4096: SDRGPU_CHECK(launch_single64<4096>(tw, in, stride, frames, win, nz, out, s)); return frames;
+        case 64: SDRGPU_CHECK(launch_single64<64>(tw, in, stride, frames, win, nz, out, lt, s)); return frames;
+        case 128: SDRGPU_CHECK(launch_single64<128>(tw, in, stride, frames, win, nz, out, lt, s)); return frames;
+        case 256: SDRGPU_CHECK(launch_single64<256>(tw, in, stride, frames, win, nz, out, lt, s)); return frames;
+        case 512: SDRGPU_CHECK(launch_single64<512>(tw, in, stride, frames, win, nz, out, lt, s)); return frames;
+        case 1024: SDRGPU_CHECK(launch_single64<1024>(tw, in, stride, frames, win, nz, out, lt, s)); return frames;
+        case 2048: SDRGPU_CHECK(launch_single64<2048>(tw, in, stride, frames, win, nz, out, lt, s)); return frames;
+        case 4096: SDRGPU_CHECK(launch_single64<4096>(tw, in, stride, frames, win, nz, out, lt, s)); return frames;
         }
         set_error("fft64: size %d", p->N);
         return SDRGPU_EARG;
@@ -407,11 +472,11 @@ int fft64_execute(Fft64Plan* p, const float2* in, long long stride, int frames, 
         default: set_error("fft64: N1 %d", p->N1); return SDRGPU_EARG;
         }
         switch (p->N2) {
-        case 64: SDRGPU_CHECK(launch_passB64<64>(t2, sc, nf, p->N1, p->logN, o, s)); break;
-        case 128: SDRGPU_CHECK(launch_passB64<128>(t2, sc, nf, p->N1, p->logN, o, s)); break;
-        case 256: SDRGPU_CHECK(launch_passB64<256>(t2, sc, nf, p->N1, p->logN, o, s)); break;
-        case 512: SDRGPU_CHECK(launch_passB64<512>(t2, sc, nf, p->N1, p->logN, o, s)); break;
-        case 1024: SDRGPU_CHECK(launch_passB64<1024>(t2, sc, nf, p->N1, p->logN, o, s)); break;
+        case 64: SDRGPU_CHECK(launch_passB64<64>(t2, sc, nf, p->N1, p->logN, o, lt, s)); break;
+        case 128: SDRGPU_CHECK(launch_passB64<128>(t2, sc, nf, p->N1, p->logN, o, lt, s)); break;
+        case 256: SDRGPU_CHECK(launch_passB64<256>(t2, sc, nf, p->N1, p->logN, o, lt, s)); break;
+        case 512: SDRGPU_CHECK(launch_passB64<512>(t2, sc, nf, p->N1, p->logN, o, lt, s)); break;
+        case 1024: SDRGPU_CHECK(launch_passB64<1024>(t2, sc, nf, p->N1, p->logN, o, lt, s)); break;
         default: set_error("fft64: N2 %d", p->N2); return SDRGPU_EARG;
         }
     }
