@@ -101,6 +101,15 @@ def test_bench_cli_gpus2_self_launches_two_ranks():
     assert abs(r["value"] - 2 * r["samples_per_rank_per_step"] * 4 / (r["ms_per_step"] * 4e-3) / 1e6) <= 2e-3 * r["value"]
 
 
+def test_bench_cli_gpus4_self_launch():
+    """The same self-launch at four ranks: rank 0 receives and verifies every rank's rows."""
+    p, _ = _bench(["--gpus", "4"] + REH)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert r["n_gpus"] == 4 and r["gather"]["verified"] is True and r["gather"]["ranks"] == 4
+    assert len({tuple(c) for c in r["last_rows_checksums"]}) == 4
+
+
 def test_bench_cli_gpus1_runs_in_process():
     p, _ = _bench(["--gpus", "1"] + REH)
     assert p.returncode == 0, p.stderr[-3000:]
