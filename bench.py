@@ -438,7 +438,7 @@ def spectrum_f64_cost(dev, stream, reps=5):
 def traffic_per_sample(config):
     """HBM bytes per input sample of the dominant launch group, from the newest committed
     rocprofv3 PMC passes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/pmc_bytes_per_sample.py)."""
-    for rnd in ("r5", "r4", "r3", "r2", "r1"):
+    for rnd in ("r6", "r5", "r4", "r3", "r2", "r1"):
         path = os.path.join(ROOT, "profiles", rnd, f"{config}_pmc_traffic.json")
         try:
             d = json.load(open(path))
