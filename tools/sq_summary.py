@@ -19,7 +19,7 @@ def main():
     for f in sorted(glob.glob(tag + "_[0-9]/run_counter_collection.csv")):
         per = defaultdict(lambda: defaultdict(float))
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
             per[(k, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
             per[(k, r["Dispatch_Id"])]["_ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
         for (k, _), c in per.items():
