@@ -406,6 +406,20 @@ def spectrum_ulp_report(dev=0, seed=20261017):
     return out
 
 
+def f64_roofline(N, nz, frames, ms):
+    """HBM roofline of the fp64-interior spectrum (fft64.hip) for one call of `frames` frames in `ms`:
+    algorithmic bytes = the fp32 op's (8 B per input sample in, 4 B per bin out); the two passes also
+    write and read a double2 intermediate (16 + 16 B per transform element, 128-MB chunks kept in the
+    Infinity Cache), reported as `moved_bytes` with its rate."""
+    algo = 8 * nz * frames + 4 * N * frames
+    moved = 8 * nz * frames + (16 + 16 + 4) * N * frames
+    achieved = algo / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes": algo, "moved_bytes": moved,
+            "moved_GBs": round(moved / (ms * 1e-3) / 1e9, 1),
+            "note": "fp64 interior, two passes through a double2 intermediate (N > 4096)"}
+
+
 def spectrum_f64_cost(dev, stream, reps=5):
     """Cost of the fp64-interior parity mode (sdrgpu_fft_set_precision(h, 1)) against the fp32 kernels
     on the same device batch: 64k BH7 over 2^26 samples (1,024 back-to-back frames) and the C2 1M plan
@@ -430,7 +444,8 @@ def spectrum_f64_cost(dev, stream, reps=5):
             del f
         out[f"N{N}"] = {"frames": frames, "samples": nz * frames, "ms_f32": round(r["f32"], 4), "ms_f64": round(r["f64"], 4),
                         "f64_over_f32": round(r["f64"] / r["f32"], 3),
-                        "MSps_f64": round(nz * frames / r["f64"] / 1e3, 1)}
+                        "MSps_f64": round(nz * frames / r["f64"] / 1e3, 1),
+                        "roofline_f64": f64_roofline(N, nz, frames, r["f64"])}
         del x, o
     return out
 
