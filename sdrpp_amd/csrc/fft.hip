@@ -887,6 +887,10 @@ constexpr int k1pPB = 2;   // (PAD) sample rows per load batch: 4 PB loads of x 
 #ifndef SDRGPU_1P_EARLYDMA
 #define SDRGPU_1P_EARLYDMA 1
 #endif
+#ifndef SDRGPU_1P_EARLYW128
+#define SDRGPU_1P_EARLYW128 1   // (A/B builds: 0) quarter r0 + 1's W_128 products during quarter r0's stage-3
+                                // reads: C5 group 1.4748 / 1.4833 vs 1.4782 / 1.4880 ms (r7t, r7u), same bits
+#endif
 #ifdef SDRGPU_1P_TIMING   // (measurement builds) per-workgroup phase stamps of wave 0
 __device__ unsigned long long g_1p_t[16384 * 8];
 #define T1P(k)                                                                                    \
@@ -1078,6 +1082,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
     // the 16k transform of quarter r = r0 + h from its stage-1 registers z. Quarter r0's dB values wait in
     // registers (dA) for quarter r0 + 1's, and the two leave as one 8-byte store per bin pair.
     float dA[2][16];
+    // (the VFO instantiations only: the others spill two registers with it)
+    constexpr bool kEarlyW = SDRGPU_1P_EARLYW128 && VFO;
+    auto w128mul = [&](float2 (&z)[32], int hh) {
+        const double2* w128 = reinterpret_cast<const double2*>(reinterpret_cast<const char*>(lds) + op1::W128D) + 32 * hh;
+#pragma unroll
+        for (int i = 1; i < 32; i++) {
+            const double2 q = zmul(make_double2(z[i].x, z[i].y), w128[i]);
+            z[i] = make_float2((float)q.x, (float)q.y);
+        }
+    };
     auto transform = [&](auto hc, float2 (&z)[32]) {
         constexpr int h = decltype(hc)::value;
         const int r = r0 + h;
@@ -1088,13 +1102,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             // product with an fp32 table (two roundings) the near-peak bins of tonal frames were 1-2 ulp
             // off more often than pocketfft's (AES17: 7 of 22 bins beyond 1 ulp vs pocketfft's 4; 2 in
             // this form), +2.7% kernel time (r5x-r5z; applied at the combine instead: +5%)
-            const double2* w128 = reinterpret_cast<const double2*>(reinterpret_cast<const char*>(lds) + op1::W128D) + 32 * h;
             // (also for quarter 0, where W = 1 and the product is exact: a branch around it spilled)
-#pragma unroll
-            for (int i = 1; i < 32; i++) {
-                const double2 q = zmul(make_double2(z[i].x, z[i].y), w128[i]);
-                z[i] = make_float2((float)q.x, (float)q.y);
-            }
+            if constexpr (!(kEarlyW && h == 1)) w128mul(z, h);
             dft32(z);
             // W_N^(t r) (W_N^(4 t))^k2 as two independent fp64 chains over even / odd k2 (a serial chain of
             // 31 fp64 complex products was the stage's critical path)
@@ -1147,6 +1156,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1))) void f
             const float2* src = lds + k2 * RS + 17 * q1;
 #pragma unroll
             for (int t0 = 0; t0 < 16; t0++) c3[t0] = src[t0 ^ sw];
+            // quarter r0 + 1's W_128 products (registers only) while these reads are in flight
+            if constexpr (kEarlyW && h == 0 && e == 0) w128mul(zb, 1);
             dft16(c3);
             if constexpr (SDRGPU_1P_ABL & 16) {
                 if constexpr (h == 1) {
