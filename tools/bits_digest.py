@@ -4,7 +4,8 @@
   python tools/bits_digest.py            -> one JSON line {case: sha256[:16]}
 
 Cases: RxVFO (C5: 61.44 MHz -> 240 kHz) over ragged host calls; BroadcastFM mono on one big call; the C5 launch group (spectrum rows,
-zoom rows, VFO stage-1 + later stages) over 24 frames; the standalone spectrum over 24 frames."""
+zoom rows, VFO stage-1 + later stages) over 24 frames; the standalone spectrum over 24 frames; the fp64-interior
+spectrum (64k over 300 frames, 1M over 3)."""
 import hashlib
 import json
 import os
@@ -47,6 +48,15 @@ def main():
     dsp.FFTSpectrum(N, N, 6).execute_dev(d_x.data_ptr(), N, F, r2.data_ptr())
     torch.cuda.synchronize()
     out["spectrum_rows"] = h(r2.cpu().numpy())
+    # the fp64-interior mode: 300 64k frames (three chunks, several pass-B tiles per workgroup) and 3 1M frames
+    g = torch.Generator(device="cuda")
+    g.manual_seed(99)
+    for n, nz, f in ((65536, 65536, 300), (1 << 20, 1000000, 3)):
+        xs = torch.rand(2 * nz * f, device="cuda", generator=g) * 2 - 1
+        r = torch.empty(n * f, device="cuda")
+        dsp.FFTSpectrum(n, nz, 6, precision="f64").execute_dev(xs.data_ptr(), nz, f, r.data_ptr())
+        torch.cuda.synchronize()
+        out[f"spectrum_f64_{n}"] = h(r.cpu().numpy())
     print(json.dumps(out))
 
 
