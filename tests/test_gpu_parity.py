@@ -1091,9 +1091,9 @@ def test_spectrum_vfo_fused_xcd(frames_list, pre, chunk_mb, rng, monkeypatch):
 @pytest.mark.parametrize("nz,skip,frames", [(65536, 0, 9), (40000, 123, 3), (65535, 7, 2), (65536, 0, 150),
                                              (50000, 3, 70), (65536, 1, 5)])
 def test_spectrum_onepass_rows_and_zoom(nz, skip, frames, rng, monkeypatch):
-    """The one-pass 64k transform (four 16k sub-transforms per frame on four CUs, radix-4 decimation in
-    frequency; SDRGPU_FFT_1P; persistent workgroups walking several frames each at 70 / 150 frames,
-    a ragged last step): every row meets the spectrum parity bar against the fp64 truth and
+    """The one-pass 64k transform (four 16k sub-transforms per frame, radix-4 decimation in frequency,
+    two workgroups per frame with two sub-transforms each; SDRGPU_FFT_1P; at 70 / 150 frames more
+    workgroups than CUs, and a ragged last group of 8 frames): every row meets the spectrum parity bar against the fp64 truth and
     pocketfft on the same frame, zero-padded frames (nz < N) and reshaper strides included; the zoom
     rows (the two workgroups' partial maxima folded) equal fft_scaler's doZoom of the row bit for bit; and the rows
     agree with the two-pass kernels to the last bits near the peak."""
