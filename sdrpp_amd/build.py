@@ -45,6 +45,15 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _defs(defines):
+    """-D NAME[=V] per define; an entry starting with '-' is passed as compiler flags (A/B builds,
+    e.g. '-mllvm -amdgpu-sched-strategy=max-ilp')."""
+    out = []
+    for d in defines:
+        out += d.split() if d.startswith("-") else ["-D" + d]
+    return out
+
+
 def build_lib(force=False, variant=None, defines=()):
     """variant: an A/B build of the same ABI with extra -D defines, into build/<variant>/ and
     sdrpp_amd/lib_<variant>/libsdrgpu.so (loaded through SDRGPU_LIB_PATH; tools/session.sh)."""
@@ -63,7 +72,7 @@ def build_lib(force=False, variant=None, defines=()):
             lang = ["-x", "hip"] if src.endswith(".hip") else []
             cmds.append([HIPCC, "--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17",
                          "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
-                         "-I", os.path.join(ROOT, "include")] + ["-D" + d for d in defines] + extra + lang +
+                         "-I", os.path.join(ROOT, "include")] + _defs(defines) + extra + lang +
                         ["-c", path, "-o", obj])
     # translation units compile in parallel (at most 8 hipcc processes: the CPU share here and well
     # under the GPU box's -j16)
